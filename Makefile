@@ -1,0 +1,59 @@
+# libhpnn (MI355X-native) build.
+#   make            -> hpnn_amd/lib/libhpnn.so, bin/train_nn, bin/run_nn,
+#                      bin/pmnist, bin/pdif, hpnn_amd/_native*.so
+#   make clean
+# Device code: hipcc --offload-arch=gfx950 only (no other targets).
+ROCM      ?= /opt/rocm
+ARCH      ?= gfx950
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+PYTHON    ?= python3
+BUILD     := build
+LIBDIR    := hpnn_amd/lib
+BINDIR    := bin
+
+INC       := -Iinclude -I$(ROCM)/include
+DEFS      := -D__HIP_PLATFORM_AMD__
+# -ffp-contract=off keeps the FP64 CPU oracle bit-stable across compilers
+CXXFLAGS  := -O2 -std=c++17 -fPIC -fopenmp -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result $(INC) $(DEFS)
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(INC)
+LDFLAGS   := -L$(ROCM)/lib -lamdhip64 -fopenmp
+
+CORE_SRC  := $(wildcard csrc/core/*.cpp) $(wildcard csrc/cpu/*.cpp) $(wildcard csrc/dist/*.cpp) csrc/gpu/gpu_engine.cpp
+HIP_SRC   := $(wildcard csrc/gpu/*.hip)
+CORE_OBJ  := $(patsubst %.cpp,$(BUILD)/%.o,$(CORE_SRC))
+HIP_OBJ   := $(patsubst %.hip,$(BUILD)/%.o,$(HIP_SRC))
+HDRS      := $(wildcard include/*.h include/libhpnn/*.h csrc/*/*.h)
+
+PYEXT     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYINC     := $(shell $(PYTHON) -c "import sysconfig,pybind11;print('-I'+sysconfig.get_paths()['include'],'-I'+pybind11.get_include())")
+PYMOD     := hpnn_amd/_native$(PYEXT)
+
+LIB       := $(LIBDIR)/libhpnn.so
+BINS      := $(BINDIR)/train_nn $(BINDIR)/run_nn $(BINDIR)/pmnist
+
+all: $(LIB) $(BINS) $(PYMOD)
+
+$(BUILD)/%.o: %.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: %.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CORE_OBJ) $(HIP_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ $(LDFLAGS) -Wl,-soname,libhpnn.so
+
+$(BINDIR)/%: tools/%.cpp $(LIB) tools/cli_common.h
+	@mkdir -p $(BINDIR)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lhpnn $(LDFLAGS) -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+$(PYMOD): csrc/python/bind.cpp $(LIB) $(HDRS)
+	$(CXX) $(CXXFLAGS) -shared $(PYINC) $< -o $@ -L$(LIBDIR) -lhpnn $(LDFLAGS) -Wl,-rpath,'$$ORIGIN/lib'
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(BINS) $(PYMOD)
+
+.PHONY: all clean

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training samples/sec (whole node), MNIST 784-128-64-10 SNN.
+
+Config (BASELINE.json): MNIST-shaped 784-128-64-10 softmax SNN, BF16 MFMA compute with FP32
+accumulation / FP32 master weights, BPM (momentum 0.2, lr 0.01), batched mode (one fwd +
+bwd + update per sample), synthetic data, random-init weights (reference init rule).
+Weak scaling: every GPU trains on its own `--batch` samples per step; gradients are
+all-reduced over RCCL (bucketed, overlapped with the backward).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  N>1 is launched by the driver as
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from hpnn_amd.models import MLP  # noqa: E402
+from hpnn_amd.parallel import DataParallel, init_from_env  # noqa: E402
+
+METRIC = "training samples/sec (whole node), MNIST 784-128-64-10 SNN at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=65536, help="per-GPU minibatch (samples per step per GPU)")
+    ap.add_argument("--datasets", type=int, default=4, help="distinct synthetic minibatches cycled per GPU")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--alpha", type=float, default=0.2)
+    ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph (1 GPU)")
+    args = ap.parse_args()
+
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    sizes = [784, 128, 64, 10]
+    m = MLP(sizes, "SNN", batch=args.batch, device=dev, momentum=True, seed=10958)
+    dp = DataParallel(m)
+    dp.broadcast_parameters()
+
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    Xs, Ls = [], []
+    for _ in range(args.datasets):
+        X = torch.rand(m.Bp, sizes[0], device=dev, generator=g)
+        Xs.append(m.prepare_input(X))
+        Ls.append(torch.randint(0, sizes[-1], (m.Bp,), device=dev, generator=g, dtype=torch.int32))
+    torch.cuda.synchronize()
+
+    def step(i):
+        dp.train_step(Xs[i % args.datasets], labels=Ls[i % args.datasets], lr=args.lr, alpha=args.alpha)
+
+    use_graph = args.graph and world == 1
+    graphs = None
+    if use_graph:
+        # one graph per synthetic batch (the input pointer is baked into the graph)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(3):
+                step(i)
+        torch.cuda.current_stream().wait_stream(s)
+        graphs = []
+        for i in range(args.datasets):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                step(i)
+            graphs.append(gr)
+
+    def run(i):
+        if graphs is not None:
+            graphs[i % args.datasets].replay()
+        else:
+            step(i)
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    m.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    loss_sum, correct = m.read_stats()
+    samples = args.steps * m.Bp * world
+    value = samples / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform [0,1) pixels, uniform labels; random-init weights, reference init rule)",
+            "config": {
+                "model": "mnist_snn 784-128-64-10 (SNN, BPM momentum 0.2, lr 0.01, batched mode)",
+                "global_batch": m.Bp * world,
+                "per_gpu_batch": m.Bp,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "hip_graph": bool(use_graph),
+            },
+            "train_loss_mean": loss_sum / max(1, samples // world),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+/*
+ * libhpnn GPU engines (HIP, gfx950) -- host-side interface.
+ *
+ * Two engines live behind this header:
+ *   online  : the reference's batch-1, iterate-to-convergence training
+ *              in FP64.  The WHOLE per-sample convergence loop
+ *             (train step, re-forward, error, argmax, stop test) runs inside
+ *             one persistent single-workgroup kernel, so there is no host
+ *             round trip per iteration (the reference synchronised the host
+ *             on every iteration: ann.c:2329-2332, cuda_ann.cu:1294).
+ *   batched : minibatch SGD / momentum with MFMA GEMMs (BF16 in, FP32
+ *             accumulate, FP32 master weights) or FP32/FP64 MFMA.
+ */
+#ifndef HPNN_GPU_ENGINE_H
+#define HPNN_GPU_ENGINE_H
+#include <libhpnn/ann.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- online (reference semantics) ---- */
+/* uploads the host weights if the device copy is stale */
+BOOL hpnn_gpu_online_prepare(kernel_ann *k, UINT gpu);
+DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train train, const DOUBLE *in,
+                             const DOUBLE *out, DOUBLE lr, DOUBLE alpha, DOUBLE delta, UINT *n_iter,
+                             BOOL *ok, DOUBLE *init_err, BOOL *first_ok);
+/* forward only; result copied to k->output.vec (host) */
+BOOL hpnn_gpu_forward(kernel_ann *k, nn_type type, const DOUBLE *in);
+/* device weights -> host master copy (no-op if host is current) */
+void hpnn_gpu_sync_host(kernel_ann *k);
+/* host master copy changed: mark device copy stale */
+void hpnn_gpu_mark_host_dirty(kernel_ann *k);
+
+/* ---- batched ---- */
+typedef struct {
+    nn_type type;
+    nn_train train;
+    nn_dtype dtype;
+    UINT batch;
+    UINT epochs;
+    DOUBLE lr;
+    DOUBLE alpha;
+    UINT seed;
+    UINT n_gpu;       /* data-parallel replicas driven by this process */
+} hpnn_batched_opts;
+
+typedef struct {
+    DOUBLE last_loss;   /* mean loss of the last minibatch            */
+    DOUBLE epoch_loss;  /* mean loss over the last epoch              */
+    UINT64 samples;     /* samples processed                          */
+    DOUBLE seconds;     /* wall time spent in the training loop       */
+    UINT correct;       /* argmax hits in the last epoch              */
+} hpnn_batched_stats;
+
+/* X: n x n_in, T: n x n_out (host, row-major FP64). Weights are read from
+ * and written back to the host kernel. */
+BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
+                            const hpnn_batched_opts *o, hpnn_batched_stats *st);
+/* batched inference: Y = net(X), n x n_out (host) */
+BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
+                            DOUBLE *Y);
+
+/* CPU batched engine (FP64 oracle for the batched semantics) */
+BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
+                            const hpnn_batched_opts *o, hpnn_batched_stats *st);
+/* one minibatch step on the CPU: returns mean loss before the update */
+DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBLE *X, const DOUBLE *T, UINT b,
+                             DOUBLE lr, BOOL momentum, DOUBLE alpha);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

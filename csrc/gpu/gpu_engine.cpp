@@ -1,0 +1,486 @@
+/*
+ * libhpnn GPU engines -- host orchestration (HIP runtime, gfx950).
+ *
+ * Online engine: one persistent kernel per training sample (online.hip).
+ * Batched engine: per minibatch
+ *     forward   gemm_nt(act) per layer          (MFMA bf16)
+ *     output    output_delta (act/softmax+loss+delta+accuracy)
+ *     backward  gemm_nt(W^T, * f'(h)) per layer (MFMA bf16)
+ *     gradient  gemm_tn split-K FP32 slabs      (MFMA bf16, tr-LDS reads)
+ *     update    sgd_update (slab reduce + BP/BPM + BF16 W / W^T refresh)
+ * All launches go to one HIP stream; nothing synchronises the host inside
+ * an epoch (the reference synchronised every iteration).
+ * Weights: host FP64 kernel_ann is the I/O master; the device keeps FP32
+ * masters (batched) or FP64 (online) and syncs back lazily.
+ */
+#include <hip/hip_runtime_api.h>
+#include <libhpnn/ann.h>
+#include <string.h>
+#include <chrono>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "../core/runtime_internal.h"
+#include "engine.h"
+#include "kernels.h"
+
+#define HIPCHK(x)                                                                           \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            NN_ERROR(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return FALSE;                                                                   \
+        }                                                                                   \
+    } while (0)
+
+extern void (*hpnn_gpu_model_destroy_hook)(kernel_ann *);
+
+namespace {
+
+struct GpuModel {
+    int dev = 0;
+    int L = 0;
+    double *W[16] = {0};
+    double *dW[16] = {0};
+    double *x = nullptr, *t = nullptr, *out = nullptr, *result = nullptr, *scratch = nullptr;
+    bool device_newer = false; /* device weights not yet copied to host */
+    bool host_newer = true;    /* host weights not yet uploaded         */
+};
+
+std::mutex g_mu;
+std::set<kernel_ann *> g_models;
+
+layer_ann *layer_of(kernel_ann *k, int l) { return l < (int)k->n_hiddens ? &k->hiddens[l] : &k->output; }
+
+void free_model(GpuModel *g) {
+    if (!g) return;
+    hipSetDevice(g->dev);
+    for (int l = 0; l < 16; l++) {
+        if (g->W[l]) hipFree(g->W[l]);
+        if (g->dW[l]) hipFree(g->dW[l]);
+    }
+    if (g->x) hipFree(g->x);
+    if (g->t) hipFree(g->t);
+    if (g->out) hipFree(g->out);
+    if (g->result) hipFree(g->result);
+    if (g->scratch) hipFree(g->scratch);
+    delete g;
+}
+
+void destroy_hook(kernel_ann *k) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    free_model((GpuModel *)k->gpu);
+    k->gpu = nullptr;
+    g_models.erase(k);
+}
+
+BOOL ensure_model(kernel_ann *k, UINT gpu) {
+    hpnn_gpu_model_destroy_hook = destroy_hook;
+    GpuModel *g = (GpuModel *)k->gpu;
+    const int L = (int)k->n_hiddens + 1;
+    if (L > 16) {
+        NN_ERROR(stderr, "GPU engine supports at most 15 hidden layers\n");
+        return FALSE;
+    }
+    if (!g) {
+        g = new GpuModel();
+        g->dev = hpnn_rt_device(gpu);
+        g->L = L;
+        HIPCHK(hipSetDevice(g->dev));
+        size_t vec = k->n_inputs;
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            HIPCHK(hipMalloc(&g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs));
+            vec += 3 * (size_t)ly->n_neurons;
+        }
+        HIPCHK(hipMalloc(&g->x, sizeof(double) * k->n_inputs));
+        HIPCHK(hipMalloc(&g->t, sizeof(double) * k->n_outputs));
+        HIPCHK(hipMalloc(&g->out, sizeof(double) * k->n_outputs));
+        HIPCHK(hipMalloc(&g->result, sizeof(double) * 8));
+        HIPCHK(hipMalloc(&g->scratch, sizeof(double) * vec));
+        k->gpu = g;
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_models.insert(k);
+    }
+    HIPCHK(hipSetDevice(g->dev));
+    if (g->host_newer) {
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            HIPCHK(hipMemcpy(g->W[l], ly->weights, sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs,
+                             hipMemcpyHostToDevice));
+        }
+        g->host_newer = false;
+        g->device_newer = false;
+    }
+    return TRUE;
+}
+
+BOOL ensure_momentum(kernel_ann *k) {
+    GpuModel *g = (GpuModel *)k->gpu;
+    for (int l = 0; l < g->L; l++) {
+        layer_ann *ly = layer_of(k, l);
+        size_t n = (size_t)ly->n_neurons * ly->n_inputs;
+        if (!g->dW[l]) HIPCHK(hipMalloc(&g->dW[l], sizeof(double) * n));
+        HIPCHK(hipMemsetAsync(g->dW[l], 0, sizeof(double) * n, hpnn_rt_stream(0, 0)));
+    }
+    return TRUE;
+}
+
+void fill_args(kernel_ann *k, GpuModel *g, nn_type type, hpnn_online_args *a) {
+    memset(a, 0, sizeof(*a));
+    a->L = g->L;
+    a->n_in = (int)k->n_inputs;
+    for (int l = 0; l < g->L; l++) {
+        layer_ann *ly = layer_of(k, l);
+        a->N[l] = (int)ly->n_neurons;
+        a->M[l] = (int)ly->n_inputs;
+        a->W[l] = g->W[l];
+        a->dW[l] = g->dW[l];
+    }
+    a->type = type == NN_TYPE_ANN ? 0 : (type == NN_TYPE_LNN ? 1 : 2);
+    a->x = g->x;
+    a->t = g->t;
+    a->out = g->out;
+    a->scratch = g->scratch;
+    a->result = g->result;
+    a->use_lds = hpnn_online_vec_bytes(a) <= 150 * 1024;
+}
+
+}  // namespace
+
+void hpnn_rt_release_device_state(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (kernel_ann *k : g_models) {
+        GpuModel *g = (GpuModel *)k->gpu;
+        if (g && g->device_newer) {
+            /* keep the host master current before the device goes away */
+            hipSetDevice(g->dev);
+            for (int l = 0; l < g->L; l++) {
+                layer_ann *ly = layer_of(k, l);
+                hipMemcpy(ly->weights, g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs,
+                          hipMemcpyDeviceToHost);
+            }
+        }
+        free_model(g);
+        k->gpu = nullptr;
+    }
+    g_models.clear();
+}
+
+extern "C" BOOL hpnn_gpu_online_prepare(kernel_ann *k, UINT gpu) { return ensure_model(k, gpu); }
+
+extern "C" void hpnn_gpu_sync_host(kernel_ann *k) {
+    if (!k || !k->gpu) return;
+    GpuModel *g = (GpuModel *)k->gpu;
+    if (!g->device_newer) return;
+    hipSetDevice(g->dev);
+    hipStreamSynchronize(hpnn_rt_stream(0, 0));
+    for (int l = 0; l < g->L; l++) {
+        layer_ann *ly = layer_of(k, l);
+        hipMemcpy(ly->weights, g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs, hipMemcpyDeviceToHost);
+    }
+    g->device_newer = false;
+}
+
+extern "C" void hpnn_gpu_mark_host_dirty(kernel_ann *k) {
+    if (!k || !k->gpu) return;
+    ((GpuModel *)k->gpu)->host_newer = true;
+}
+
+extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train train, const DOUBLE *in,
+                                        const DOUBLE *out, DOUBLE lr, DOUBLE alpha, DOUBLE delta, UINT *n_iter,
+                                        BOOL *ok, DOUBLE *init_err, BOOL *first_ok) {
+    if (!ensure_model(k, 0)) return 0.0;
+    GpuModel *g = (GpuModel *)k->gpu;
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    const bool mom = train == NN_TRAIN_BPM;
+    if (mom && !ensure_momentum(k)) return 0.0; /* momentum reset per sample */
+    hpnn_online_args a;
+    fill_args(k, g, type, &a);
+    a.momentum = mom;
+    a.lr = lr;
+    a.alpha = alpha;
+    a.delta = delta > 0 ? delta : (mom ? DELTA_BPM : DELTA_BP);
+    a.min_iter = mom ? MIN_BPM_ITER : MIN_BP_ITER;
+    a.max_iter = mom ? MAX_BPM_ITER : MAX_BP_ITER;
+    a.forward_only = 0;
+    hipMemcpyAsync(g->x, in, sizeof(double) * k->n_inputs, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(g->t, out, sizeof(double) * k->n_outputs, hipMemcpyHostToDevice, s);
+    if (hpnn_online_launch(&a, s) != 0) {
+        NN_ERROR(stderr, "online kernel launch failed\n");
+        return 0.0;
+    }
+    double res[5];
+    hipMemcpyAsync(res, g->result, sizeof(res), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(k->output.vec, g->out, sizeof(double) * k->n_outputs, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    g->device_newer = true;
+    if (n_iter) *n_iter = (UINT)res[2];
+    if (ok) *ok = res[3] != 0.0;
+    if (init_err) *init_err = res[1];
+    if (first_ok) *first_ok = res[4] != 0.0;
+    return res[0];
+}
+
+extern "C" BOOL hpnn_gpu_forward(kernel_ann *k, nn_type type, const DOUBLE *in) {
+    if (!ensure_model(k, 0)) return FALSE;
+    GpuModel *g = (GpuModel *)k->gpu;
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    hpnn_online_args a;
+    fill_args(k, g, type, &a);
+    a.forward_only = 1;
+    hipMemcpyAsync(g->x, in, sizeof(double) * k->n_inputs, hipMemcpyHostToDevice, s);
+    hipMemsetAsync(g->t, 0, sizeof(double) * k->n_outputs, s);
+    if (hpnn_online_launch(&a, s) != 0) return FALSE;
+    hipMemcpyAsync(k->output.vec, g->out, sizeof(double) * k->n_outputs, hipMemcpyDeviceToHost, s);
+    memcpy(k->in, in, sizeof(double) * k->n_inputs);
+    HIPCHK(hipStreamSynchronize(s));
+    return TRUE;
+}
+
+/* ====================================================================== */
+/* batched engine                                                          */
+/* ====================================================================== */
+namespace {
+
+inline int pad32(int v) { return (v + 31) / 32 * 32; }
+inline int pad128(int v) { return (v + 127) / 128 * 128; }
+
+/* split-K factor for the weight-gradient GEMM: aim for ~1024 workgroups */
+int pick_splits(int Np, int Kp, int Bp) {
+    const int tn = (Np % 128 == 0) ? 128 : (Np % 64 == 0 ? 64 : 32);
+    const int tm = (Kp % 128 == 0) ? 128 : (Kp % 64 == 0 ? 64 : 32);
+    const int tiles = (Np / tn) * (Kp / tm);
+    int s = 1024 / (tiles > 0 ? tiles : 1);
+    if (s < 1) s = 1;
+    int maxs = Bp / 256;
+    if (maxs < 1) maxs = 1;
+    if (s > maxs) s = maxs;
+    while (s > 1 && (Bp % (64 * s))) s--;
+    return s;
+}
+
+struct Batched {
+    int L = 0, Bp = 0, n_out = 0, type = 2;
+    int M[16], N[16], Kp[16], Np[16], S[16];
+    float *W32[16] = {0}, *V32[16] = {0}, *slab[16] = {0};
+    void *Wb[16] = {0}, *Wt[16] = {0}, *H[16] = {0}, *D[16] = {0};
+    float *Z = nullptr;
+    float *acc = nullptr; /* [0] loss sum, [1] correct (uint) */
+    hipStream_t s = nullptr;
+
+    ~Batched() {
+        for (int l = 0; l < 16; l++) {
+            hipFree(W32[l]);
+            hipFree(V32[l]);
+            hipFree(slab[l]);
+            hipFree(Wb[l]);
+            hipFree(Wt[l]);
+            hipFree(H[l]);
+            hipFree(D[l]);
+        }
+        hipFree(Z);
+        hipFree(acc);
+    }
+
+    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st) {
+        s = st;
+        L = (int)k->n_hiddens + 1;
+        Bp = pad128(B);
+        n_out = (int)k->n_outputs;
+        type = t == NN_TYPE_ANN ? 0 : (t == NN_TYPE_LNN ? 1 : 2);
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            M[l] = (int)ly->n_inputs;
+            N[l] = (int)ly->n_neurons;
+            Kp[l] = pad32(M[l]);
+            Np[l] = pad32(N[l]);
+            S[l] = pick_splits(Np[l], Kp[l], Bp);
+            const size_t nw = (size_t)Np[l] * Kp[l];
+            HIPCHK(hipMalloc(&W32[l], nw * 4));
+            HIPCHK(hipMalloc(&Wb[l], nw * 2));
+            HIPCHK(hipMalloc(&Wt[l], nw * 2));
+            HIPCHK(hipMalloc(&slab[l], nw * 4 * S[l]));
+            if (momentum) {
+                HIPCHK(hipMalloc(&V32[l], nw * 4));
+                HIPCHK(hipMemsetAsync(V32[l], 0, nw * 4, s));
+            }
+            HIPCHK(hipMalloc(&D[l], (size_t)Bp * Np[l] * 2));
+            if (l < L - 1) HIPCHK(hipMalloc(&H[l], (size_t)Bp * Np[l] * 2));
+            /* FP64 host -> padded FP32 master */
+            std::vector<float> tmp(nw, 0.f);
+            for (int n = 0; n < N[l]; n++)
+                for (int m = 0; m < M[l]; m++) tmp[(size_t)n * Kp[l] + m] = (float)ly->weights[(size_t)n * M[l] + m];
+            HIPCHK(hipMemcpyAsync(W32[l], tmp.data(), nw * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (hpnn_cast_weights(W32[l], Wb[l], Wt[l], Np[l], Kp[l], s)) return FALSE;
+        }
+        HIPCHK(hipMalloc(&Z, (size_t)Bp * Np[L - 1] * 4));
+        HIPCHK(hipMalloc(&acc, 16));
+        HIPCHK(hipMemsetAsync(acc, 0, 16, s));
+        return TRUE;
+    }
+
+    BOOL forward(const void *X) {
+        for (int l = 0; l < L; l++) {
+            const void *A = l ? H[l - 1] : X;
+            const bool last = l == L - 1;
+            int r = hpnn_gemm_nt_bf16(A, Kp[l], Wb[l], Kp[l], last ? (void *)Z : H[l], Np[l], nullptr, 0, Bp, Np[l],
+                                      Kp[l], last ? HPNN_EPI_NONE : HPNN_EPI_ACT, last ? 1 : 0, s);
+            if (r) {
+                NN_ERROR(stderr, "gemm_nt (fwd layer %d) failed: %d\n", l, r);
+                return FALSE;
+            }
+        }
+        return TRUE;
+    }
+
+    BOOL step(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
+        if (!forward(X)) return FALSE;
+        if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
+                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
+            return FALSE;
+        for (int l = L - 1; l >= 1; l--) {
+            /* D[l-1] = (D[l] . W_l) * f'(H[l-1]);  W_l^T is [Kp[l] x Np[l]] */
+            int r = hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp,
+                                      Np[l - 1], Np[l], HPNN_EPI_DACT, 0, s);
+            if (r) {
+                NN_ERROR(stderr, "gemm_nt (bwd layer %d) failed: %d\n", l, r);
+                return FALSE;
+            }
+        }
+        for (int l = 0; l < L; l++) {
+            const void *Hin = l ? H[l - 1] : X;
+            int r = hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s);
+            if (r) {
+                NN_ERROR(stderr, "gemm_tn (layer %d) failed: %d\n", l, r);
+                return FALSE;
+            }
+            r = hpnn_sgd_update(W32[l], V32[l], slab[l], S[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], Np[l], Kp[l], lr,
+                                alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s);
+            if (r) return FALSE;
+        }
+        return TRUE;
+    }
+
+    BOOL download(kernel_ann *k) {
+        HIPCHK(hipStreamSynchronize(s));
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            std::vector<float> tmp((size_t)Np[l] * Kp[l]);
+            HIPCHK(hipMemcpy(tmp.data(), W32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N[l]; n++)
+                for (int m = 0; m < M[l]; m++) ly->weights[(size_t)n * M[l] + m] = tmp[(size_t)n * Kp[l] + m];
+        }
+        return TRUE;
+    }
+};
+
+/* upload n host rows (FP64) as a padded BF16 matrix [rows_p x cols_p] */
+BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t s) {
+    void *tmp = nullptr;
+    HIPCHK(hipMalloc(dst, (size_t)rows_p * cols_p * 2));
+    HIPCHK(hipMalloc(&tmp, (size_t)rows * cols * 8));
+    HIPCHK(hipMemcpyAsync(tmp, src, (size_t)rows * cols * 8, hipMemcpyHostToDevice, s));
+    if (hpnn_pack_bf16(tmp, 1, rows, cols, cols, *dst, rows_p, cols_p, cols_p, s)) return FALSE;
+    HIPCHK(hipStreamSynchronize(s));
+    hipFree(tmp);
+    return TRUE;
+}
+
+}  // namespace
+
+extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
+                                       const hpnn_batched_opts *o, hpnn_batched_stats *st) {
+    if (o->dtype != NN_DTYPE_BF16) {
+        NN_WARN(stderr, "GPU batched engine runs BF16 MFMA; requested dtype promoted to bf16\n");
+    }
+    if (k->n_hiddens + 1 > 16) return FALSE;
+    hpnn_gpu_sync_host(k);
+    HIPCHK(hipSetDevice(hpnn_rt_device(0)));
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    const int B = (int)(o->batch ? o->batch : 256);
+    const bool mom = o->train == NN_TRAIN_BPM;
+    Batched net;
+    if (!net.init(k, B, o->type, mom, s)) return FALSE;
+    const int n_batches = (int)((n + B - 1) / B);
+    const int rows_p = (n_batches - 1) * B + net.Bp; /* last batch reads Bp rows */
+    void *Xd = nullptr;
+    float *Td = nullptr;
+    if (!upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
+    {
+        std::vector<float> tf((size_t)rows_p * k->n_outputs, 0.f);
+        for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (float)T[i];
+        HIPCHK(hipMalloc(&Td, tf.size() * 4));
+        HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice));
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    float h_acc[2] = {0, 0};
+    for (UINT e = 0; e < o->epochs; e++) {
+        HIPCHK(hipMemsetAsync(net.acc, 0, 16, s));
+        for (int b = 0; b < n_batches; b++) {
+            const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
+            const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * 2;
+            const float *tb = Td + (size_t)b * B * k->n_outputs;
+            if (!net.step(xb, tb, (int)k->n_outputs, nv, (float)o->lr, (float)o->alpha, mom)) {
+                hipFree(Xd);
+                hipFree(Td);
+                return FALSE;
+            }
+        }
+        HIPCHK(hipMemcpyAsync(h_acc, net.acc, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    net.download(k);
+    if (st) {
+        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->samples = (UINT64)n * o->epochs;
+        st->epoch_loss = h_acc[0] / (double)n;
+        unsigned int c;
+        memcpy(&c, &h_acc[1], 4);
+        st->correct = c;
+        st->last_loss = st->epoch_loss;
+    }
+    hipFree(Xd);
+    hipFree(Td);
+    /* device FP64 copy of the online engine (if any) is now stale */
+    if (k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
+    return TRUE;
+}
+
+extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
+                                       DOUBLE *Y) {
+    (void)dtype;
+    hpnn_gpu_sync_host(k);
+    HIPCHK(hipSetDevice(hpnn_rt_device(0)));
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    const int B = 4096;
+    Batched net;
+    if (!net.init(k, B, type, false, s)) return FALSE;
+    const int n_batches = (int)((n + B - 1) / B);
+    const int rows_p = (n_batches - 1) * B + net.Bp;
+    void *Xd = nullptr;
+    float *O = nullptr, *Tz = nullptr;
+    if (!upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
+    HIPCHK(hipMalloc(&O, (size_t)net.Bp * net.Np[net.L - 1] * 4));
+    HIPCHK(hipMalloc(&Tz, (size_t)net.Bp * k->n_outputs * 4));
+    HIPCHK(hipMemset(Tz, 0, (size_t)net.Bp * k->n_outputs * 4));
+    std::vector<float> h((size_t)net.Bp * net.Np[net.L - 1]);
+    for (int b = 0; b < n_batches; b++) {
+        const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
+        if (!net.forward((const char *)Xd + (size_t)b * B * net.Kp[0] * 2)) return FALSE;
+        hpnn_output_delta(net.Z, net.Np[net.L - 1], Tz, (int)k->n_outputs, nullptr, 0.f, 0.f, net.D[net.L - 1],
+                          net.Np[net.L - 1], O, net.Np[net.L - 1], nullptr, nullptr, net.Bp, nv, net.n_out, net.type, s);
+        HIPCHK(hipMemcpyAsync(h.data(), O, h.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int r = 0; r < nv; r++)
+            for (UINT c = 0; c < k->n_outputs; c++)
+                Y[((size_t)b * B + r) * k->n_outputs + c] = h[(size_t)r * net.Np[net.L - 1] + c];
+    }
+    hipFree(Xd);
+    hipFree(O);
+    hipFree(Tz);
+    return TRUE;
+}

@@ -1,0 +1,109 @@
+/*
+ * libhpnn HIP kernel launchers (gfx950).  Plain C ABI: device pointers +
+ * hipStream_t, so the native engines and the Python binding share them.
+ *
+ * Layout conventions (see docs/DESIGN.md):
+ *   activations  [rows = samples][cols = features], row-major, BF16
+ *   weights      W [N][K] row-major (one row per neuron, as the reference),
+ *                plus a transposed BF16 copy Wt [K][N] for the dX GEMM
+ *   every feature dimension is padded to a multiple of 32 and every batch
+ *   dimension to a multiple of 128 on the device; padded weights/inputs are
+ *   zero so they never contribute.
+ * Return value of every launcher: 0 = launched, <0 = shape not supported
+ * (caller bug: the kernels never guess).
+ */
+#ifndef HPNN_GPU_KERNELS_H
+#define HPNN_GPU_KERNELS_H
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    HPNN_EPI_NONE = 0,   /* C = acc                                   */
+    HPNN_EPI_ACT = 1,    /* C = 2/(1+e^-acc) - 1                      */
+    HPNN_EPI_DACT = 2,   /* C = acc * (-0.5)(aux^2 - 1)  (f'(h))      */
+};
+
+/* C[M x N] = epi(A[M x K] . B[N x K]^T), A/B BF16, C BF16 (c_f32=0) or
+ * FP32 (c_f32=1).  M % 128 == 0, N % 32 == 0, K % 32 == 0. */
+int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc,
+                      const void *aux, int ldaux, int M, int N, int K, int epi, int c_f32,
+                      hipStream_t stream);
+
+/* slab[s][N x M] = sum_{b in slice s} D[b][n] H[b][m] (FP32 out).
+ * D: [Bt x N] BF16, H: [Bt x M] BF16. Bt % (64*splits) == 0, N,M % 32 == 0.
+ * ldg: row stride of a slab row (>= M); slab stride = N*ldg. */
+int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N,
+                      int M, int Bt, int splits, hipStream_t stream);
+
+/* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
+ *   delta  D [B x ldd] BF16  (zero in padded rows/cols)
+ *   loss_acc[0] += sum of per-sample loss over valid rows
+ *   correct[0]  += argmax hits
+ *   optional O [B x ldo] FP32 network output (NULL to skip)
+ * targets: dense T [B x ldt] FP32 (labels == NULL) or int32 labels with
+ * one-hot values (t_hi at the label, t_lo elsewhere).
+ * type: 0 ANN, 1 LNN, 2 SNN (nn_type). */
+int hpnn_output_delta(const float *Z, int ldz, const float *T, int ldt, const int *labels, float t_hi,
+                      float t_lo, void *D, int ldd, float *O, int ldo, float *loss_acc,
+                      unsigned int *correct, int B, int n_valid, int n_out, int type,
+                      hipStream_t stream);
+
+/* sum S slabs of n floats: out[i] = sum_s slab[s*stride + i] */
+int hpnn_reduce_slabs(const float *slab, int S, long stride, long n, float *out, hipStream_t stream);
+
+/* optimizer step for one layer, W32/V32 FP32 master [N x K]:
+ *   g = scale * sum_s G[s*gstride + i]
+ *   BP : w += lr g              (momentum == 0)
+ *   BPM: v += lr g; w += v; v *= alpha
+ * then writes BF16 W [N x K] and BF16 Wt [K x N] (ldwt = N). */
+int hpnn_sgd_update(float *W32, float *V32, const float *G, int S, long gstride, void *Wbf, void *Wt,
+                    int N, int K, float lr, float alpha, float scale, int momentum,
+                    hipStream_t stream);
+
+/* dense FP64/FP32 host-layout matrix -> padded BF16 device matrix:
+ * dst[r][c] = src[r][c] for r<rows,c<cols, 0 in the padding.
+ * src_f64 selects double vs float input. */
+int hpnn_pack_bf16(const void *src, int src_f64, int rows, int cols, int lds, void *dst, int prow,
+                   int pcol, int ldd, hipStream_t stream);
+
+/* FP32 master <-> BF16 copies without an update (after load/broadcast) */
+int hpnn_cast_weights(const float *W32, void *Wbf, void *Wt, int N, int K, hipStream_t stream);
+
+/* zero-fill helper usable inside graphs */
+int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream);
+
+/* online (batch-1) FP64 persistent engine, see online.hip */
+typedef struct {
+    int L;
+    int n_in;
+    int N[16];
+    int M[16];
+    double *W[16];
+    double *dW[16];
+    int type;     /* 0 ANN 1 LNN 2 SNN */
+    int momentum;
+    double lr;
+    double alpha;
+    double delta;
+    int min_iter;
+    int max_iter;
+    const double *x;
+    const double *t;
+    double *out;       /* n_out, final network output */
+    double *scratch;   /* vectors when they do not fit in LDS */
+    double *result;    /* [0]=dEp [1]=init_err [2]=iter [3]=ok [4]=first_ok */
+    int use_lds;
+    int forward_only;
+} hpnn_online_args;
+
+int hpnn_online_launch(const hpnn_online_args *a, hipStream_t stream);
+/* bytes of vector storage the online kernel needs */
+long hpnn_online_vec_bytes(const hpnn_online_args *a);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

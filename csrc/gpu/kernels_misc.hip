@@ -1,0 +1,261 @@
+/*
+ * libhpnn element-wise / reduction kernels for gfx950.
+ *
+ *   output_delta : output layer activation + loss + output delta + accuracy
+ *                  in one pass (replaces the reference's sigmoid/softmax_acc/
+ *                  fw_scal/amb/amb_smax/dsigmoid_mul_diff/dsmax_diff kernels
+ *                  plus the host-synchronising cublasDasum, cuda_ann.cu:41-113,
+ *                  cuda_snn.cu:42-147).  One wave64 per sample, wave-level
+ *                  shuffles, one atomic per block; correct for any width
+ *                  (the reference reductions read block 0 only: N<=2048).
+ *                  SNN uses the reference softmax e^{z-1}/(TINY+sum e^{z-1})
+ *                  evaluated in the max-shifted form (identical value, no
+ *                  overflow).
+ *   reduce_slabs : deterministic sum of split-K partial slabs.
+ *   sgd_update   : slab reduce + BP / BPM update on the FP32 master, then
+ *                  BF16 W and BF16 W^T (through an LDS transpose so both
+ *                  stores are coalesced).  Replaces cublasDger / Daxpy /
+ *                  Dscal / ger_acc / ger_dw_acc (cuda_ann.cu:124-148).
+ *   pack_bf16    : host-layout FP64/FP32 samples -> padded BF16 tiles.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+/* first index of the maximum (ties -> lowest index), -1 for empty lanes */
+__device__ __forceinline__ void wave_argmax(float &v, int &i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float ov = __shfl_xor(v, o, 64);
+        int oi = __shfl_xor(i, o, 64);
+        if (oi >= 0 && (i < 0 || ov > v || (ov == v && oi < i))) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+constexpr float TINY = 1e-14f;
+
+__global__ __launch_bounds__(256) void output_delta_kernel(const float *__restrict__ Z, int ldz,
+                                                           const float *__restrict__ T, int ldt,
+                                                           const int *__restrict__ labels, float t_hi, float t_lo,
+                                                           __bf16 *__restrict__ D, int ldd, float *__restrict__ O,
+                                                           int ldo, float *__restrict__ loss_acc,
+                                                           unsigned int *__restrict__ correct, int B, int n_valid,
+                                                           int n_out, int type) {
+    __shared__ float sloss[4];
+    __shared__ unsigned int shit[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int row = blockIdx.x * 4 + wave;
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    if (row < B) {
+        const bool valid = row < n_valid;
+        const int lab = (labels && valid) ? labels[row] : -1;
+        /* pass 1: output values (kept in registers, <= 64 columns per lane chunk) */
+        float zmax = -INFINITY;
+        if (type == 2) {
+            for (int c = lane; c < n_out; c += 64) zmax = fmaxf(zmax, Z[(size_t)row * ldz + c]);
+            zmax = wave_max(zmax);
+        }
+        float denom = 0.f;
+        if (type == 2) {
+            for (int c = lane; c < n_out; c += 64) denom += __expf(Z[(size_t)row * ldz + c] - zmax);
+            denom = wave_sum(denom);
+            /* reference: e^{z-1} / (TINY + sum e^{z-1}); shifted by m=zmax */
+            const float tiny_term = __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
+            denom += tiny_term;
+        }
+        const float inv = type == 2 ? 1.0f / denom : 0.f;
+        float bo = -INFINITY, bt = -INFINITY;
+        int io = -1, it = -1;
+        float l = 0.f;
+        for (int c = lane; c < (ldd > n_out ? ldd : n_out); c += 64) {
+            float d = 0.f;
+            if (c < n_out) {
+                const float z = Z[(size_t)row * ldz + c];
+                float o;
+                if (type == 2) o = __expf(z - zmax) * inv;
+                else if (type == 0) o = 2.0f / (1.0f + __expf(-z)) - 1.0f;
+                else o = z;
+                float t = labels ? (c == lab ? t_hi : t_lo) : (valid ? T[(size_t)row * ldt + c] : 0.f);
+                if (valid) {
+                    if (type == 2) {
+                        if (o > 0.f) l += t * logf(o + TINY);
+                        d = t - o;
+                    } else if (type == 0) {
+                        l += (t - o) * (t - o);
+                        d = (t - o) * (-0.5f * (o * o - 1.0f));
+                    } else {
+                        l += (t - o) * (t - o);
+                        d = t - o;
+                    }
+                    if (o > bo) { bo = o; io = c; }
+                    if (t > bt) { bt = t; it = c; }
+                }
+                if (O) O[(size_t)row * ldo + c] = o;
+            }
+            if (c < ldd) D[(size_t)row * ldd + c] = (__bf16)d;
+        }
+        if (valid) {
+            l = wave_sum(l);
+            my_loss = (type == 2) ? -l / (float)n_out : 0.5f * l;
+            wave_argmax(bo, io);
+            wave_argmax(bt, it);
+            my_hit = (io == it) ? 1u : 0u;
+        }
+    }
+    if (lane == 0) {
+        sloss[wave] = my_loss;
+        shit[wave] = my_hit;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = sloss[0] + sloss[1] + sloss[2] + sloss[3];
+        unsigned int h = shit[0] + shit[1] + shit[2] + shit[3];
+        if (loss_acc && s != 0.f) atomicAdd(loss_acc, s);
+        if (correct && h) atomicAdd(correct, h);
+    }
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *__restrict__ slab, int S, long stride, long n4,
+                                                           float *__restrict__ out) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+        f32x4 a = ((const f32x4 *)slab)[i];
+        for (int s = 1; s < S; s++) a += ((const f32x4 *)(slab + s * stride))[i];
+        ((f32x4 *)out)[i] = a;
+    }
+}
+
+/* 32x32 tile per block, 256 threads: thread (ty = tid/8, tx = tid%8) owns
+ * row ty, columns 4tx..4tx+3 of the tile. */
+__global__ __launch_bounds__(256) void sgd_update_kernel(float *__restrict__ W32, float *__restrict__ V32,
+                                                         const float *__restrict__ G, int S, long gstride,
+                                                         __bf16 *__restrict__ Wbf, __bf16 *__restrict__ Wt, int N,
+                                                         int K, float lr, float alpha, float scale, int momentum) {
+    __shared__ float tile[32][33];
+    const int tiles_k = K / 32;
+    const int tn = blockIdx.x / tiles_k, tk = blockIdx.x % tiles_k;
+    const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+    const int n = tn * 32 + ty, k = tk * 32 + tx * 4;
+    const size_t idx = (size_t)n * K + k;
+    f32x4 g = *(const f32x4 *)(G + idx);
+    for (int s = 1; s < S; s++) g += *(const f32x4 *)(G + s * gstride + idx);
+    f32x4 w = *(const f32x4 *)(W32 + idx);
+    if (momentum) {
+        f32x4 v = *(const f32x4 *)(V32 + idx);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            v[r] += lr * (g[r] * scale);
+            w[r] += v[r];
+            v[r] *= alpha;
+        }
+        *(f32x4 *)(V32 + idx) = v;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) w[r] += lr * (g[r] * scale);
+    }
+    *(f32x4 *)(W32 + idx) = w;
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 wb;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        wb[r] = (__bf16)w[r];
+        tile[ty][tx * 4 + r] = w[r];
+    }
+    *(bf16x4 *)(Wbf + idx) = wb;
+    __syncthreads();
+    /* transposed: thread writes Wt[k = tk*32 + ty][n = tn*32 + 4tx .. +3] */
+    bf16x4 tb;
+#pragma unroll
+    for (int r = 0; r < 4; r++) tb[r] = (__bf16)tile[tx * 4 + r][ty];
+    *(bf16x4 *)(Wt + (size_t)(tk * 32 + ty) * N + tn * 32 + tx * 4) = tb;
+}
+
+__global__ void pack_bf16_kernel(const void *__restrict__ src, int src_f64, int rows, int cols, int lds,
+                                 __bf16 *__restrict__ dst, int prow, int pcol, int ldd) {
+    const long total = (long)prow * pcol;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(i / pcol), c = (int)(i % pcol);
+        float v = 0.f;
+        if (r < rows && c < cols)
+            v = src_f64 ? (float)((const double *)src)[(size_t)r * lds + c] : ((const float *)src)[(size_t)r * lds + c];
+        dst[(size_t)r * ldd + c] = (__bf16)v;
+    }
+}
+
+__global__ void fill_kernel(float *p, long n, float v) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+
+inline int grid_for(long n, int bs) {
+    long g = (n + bs - 1) / bs;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ldt, const int *labels, float t_hi,
+                                 float t_lo, void *D, int ldd, float *O, int ldo, float *loss_acc,
+                                 unsigned int *correct, int B, int n_valid, int n_out, int type,
+                                 hipStream_t stream) {
+    if (B <= 0 || n_out <= 0 || ldz < n_out || ldd < n_out) return -1;
+    if (!labels && !T) return -1;
+    hipLaunchKernelGGL(output_delta_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
+                       t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_reduce_slabs(const float *slab, int S, long stride, long n, float *out, hipStream_t stream) {
+    if (n % 4 || stride % 4 || S < 1) return -2;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, stream, slab, S, stride, n / 4,
+                       out);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_sgd_update(float *W32, float *V32, const float *G, int S, long gstride, void *Wbf, void *Wt,
+                               int N, int K, float lr, float alpha, float scale, int momentum, hipStream_t stream) {
+    if (N % 32 || K % 32 || S < 1) return -2;
+    if (momentum && !V32) return -1;
+    hipLaunchKernelGGL(sgd_update_kernel, dim3((N / 32) * (K / 32)), dim3(256), 0, stream, W32, V32, G, S, gstride,
+                       (__bf16 *)Wbf, (__bf16 *)Wt, N, K, lr, alpha, scale, momentum);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_cast_weights(const float *W32, void *Wbf, void *Wt, int N, int K, hipStream_t stream) {
+    /* an update with lr = 0 and a zero gradient is exactly a cast: reuse the
+     * same kernel with G = W32 and scale 0 */
+    return hpnn_sgd_update((float *)W32, NULL, W32, 1, 0, Wbf, Wt, N, K, 0.f, 0.f, 0.f, 0, stream);
+}
+
+extern "C" int hpnn_pack_bf16(const void *src, int src_f64, int rows, int cols, int lds, void *dst, int prow,
+                              int pcol, int ldd, hipStream_t stream) {
+    if (rows > prow || cols > pcol || ldd < pcol) return -1;
+    hipLaunchKernelGGL(pack_bf16_kernel, dim3(grid_for((long)prow * pcol, 256)), dim3(256), 0, stream, src, src_f64,
+                       rows, cols, lds, (__bf16 *)dst, prow, pcol, ldd);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream) {
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, n, v);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}

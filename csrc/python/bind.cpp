@@ -1,0 +1,83 @@
+/*
+ * Python binding of the libhpnn HIP kernel launchers (pybind11).
+ *
+ * Deliberately torch-free: tensors cross the boundary as raw device
+ * addresses (tensor.data_ptr()) and the HIP stream as an integer handle
+ * (torch.cuda.current_stream().cuda_stream), so the module is a thin,
+ * ABI-stable shim over libhpnn.so and every launch is captured by
+ * torch.cuda.graph like any other kernel on that stream.
+ */
+#include <pybind11/pybind11.h>
+#include <hip/hip_runtime_api.h>
+#include <libhpnn.h>
+#include <stdexcept>
+#include <string>
+
+#include "../gpu/kernels.h"
+
+namespace py = pybind11;
+using uptr = uintptr_t;
+
+static inline void *P(uptr p) { return reinterpret_cast<void *>(p); }
+static inline hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
+static void check(int rc, const char *what) {
+    if (rc != 0) throw std::runtime_error(std::string(what) + " failed (rc=" + std::to_string(rc) + ")");
+}
+
+PYBIND11_MODULE(_native, m) {
+    m.doc() = "libhpnn gfx950 kernels (MFMA GEMMs, fused output/optimizer kernels)";
+    m.attr("EPI_NONE") = (int)HPNN_EPI_NONE;
+    m.attr("EPI_ACT") = (int)HPNN_EPI_ACT;
+    m.attr("EPI_DACT") = (int)HPNN_EPI_DACT;
+
+    m.def("version", []() { return std::string(nn_return_version()); });
+
+    m.def(
+        "gemm_nt_bf16",
+        [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M, int N, int K, int epi,
+           int c_f32, uptr stream) {
+            check(hpnn_gemm_nt_bf16(P(A), lda, P(B), ldb, P(C), ldc, P(aux), ldaux, M, N, K, epi, c_f32, S(stream)),
+                  "gemm_nt_bf16");
+        },
+        "C = epi(A . B^T), bf16 MFMA");
+    m.def(
+        "gemm_tn_bf16",
+        [](uptr D, int ldd, uptr H, int ldh, uptr slab, int ldg, int N, int M, int Bt, int splits, uptr stream) {
+            check(hpnn_gemm_tn_bf16(P(D), ldd, P(H), ldh, (float *)P(slab), ldg, N, M, Bt, splits, S(stream)),
+                  "gemm_tn_bf16");
+        },
+        "slab[s] = D^T . H over batch slice s, bf16 MFMA");
+    m.def(
+        "output_delta",
+        [](uptr Z, int ldz, uptr T, int ldt, uptr labels, float t_hi, float t_lo, uptr D, int ldd, uptr O, int ldo,
+           uptr loss, uptr correct, int B, int n_valid, int n_out, int type, uptr stream) {
+            check(hpnn_output_delta((const float *)P(Z), ldz, (const float *)P(T), ldt, (const int *)P(labels), t_hi,
+                                    t_lo, P(D), ldd, (float *)P(O), ldo, (float *)P(loss), (unsigned int *)P(correct),
+                                    B, n_valid, n_out, type, S(stream)),
+                  "output_delta");
+        });
+    m.def("reduce_slabs", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
+        check(hpnn_reduce_slabs((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)), "reduce_slabs");
+    });
+    m.def("sgd_update", [](uptr W32, uptr V32, uptr G, int Sn, long gstride, uptr Wbf, uptr Wt, int N, int K, float lr,
+                           float alpha, float scale, int momentum, uptr stream) {
+        check(hpnn_sgd_update((float *)P(W32), (float *)P(V32), (const float *)P(G), Sn, gstride, P(Wbf), P(Wt), N, K,
+                              lr, alpha, scale, momentum, S(stream)),
+              "sgd_update");
+    });
+    m.def("cast_weights", [](uptr W32, uptr Wbf, uptr Wt, int N, int K, uptr stream) {
+        check(hpnn_cast_weights((const float *)P(W32), P(Wbf), P(Wt), N, K, S(stream)), "cast_weights");
+    });
+    m.def("pack_bf16", [](uptr src, int src_f64, int rows, int cols, int lds, uptr dst, int prow, int pcol, int ldd,
+                          uptr stream) {
+        check(hpnn_pack_bf16(P(src), src_f64, rows, cols, lds, P(dst), prow, pcol, ldd, S(stream)), "pack_bf16");
+    });
+    m.def("fill_f32", [](uptr p, long n, float v, uptr stream) {
+        check(hpnn_fill_f32((float *)P(p), n, v, S(stream)), "fill_f32");
+    });
+    m.def("device_count", []() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        return n;
+    });
+}

@@ -1,0 +1,182 @@
+"""Bias-free MLP (libhpnn ANN / SNN / LNN) on the gfx950 kernels.
+
+Math (reference SURVEY 2.4; ann.c / snn.c):
+  h_l = f(W_l h_{l-1}),  f(x) = 2/(1+e^-x) - 1   (every hidden layer; ANN output too)
+  SNN output  o = e^{z-1} / (TINY + sum e^{z-1}),  delta_L = t - o
+  ANN output  o = f(z),                             delta_L = (t - o) f'(o)
+  hidden      delta_l = (W_{l+1}^T delta_{l+1}) * f'(h_l),  f'(y) = -0.5 (y^2 - 1)
+  update      BP : W += lr * G ;  BPM: dW += lr * G; W += dW; dW *= alpha
+  with G = mean over the minibatch of delta_l (x) h_{l-1} (batched mode, see
+  csrc/cpu/cpu_batched.cpp for the FP64 oracle of exactly these semantics).
+
+Device layout (csrc/gpu/kernels.h): activations [batch, features] BF16, feature dims
+padded to 32, batch padded to 128; W [N, K] BF16 + W^T [K, N] BF16 for the dX GEMM;
+FP32 master weights and momentum; FP32 split-K gradient slabs.
+"""
+import ctypes
+import ctypes.util
+import math
+
+import torch
+
+from .. import ops
+
+TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
+
+
+def reference_init(sizes, seed):
+    """Bit-identical to libhpnn ann_generate (ann.c:632-766): glibc srandom(seed),
+    w = 2 (random()/RAND_MAX - 0.5) / sqrt(M), hidden layers first, row-major."""
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    libc.random.restype = ctypes.c_long
+    libc.srandom(ctypes.c_uint(seed))
+    rand_max = 2147483647.0
+    out = []
+    for l in range(len(sizes) - 1):
+        M, N = sizes[l], sizes[l + 1]
+        n = N * M
+        if n > 4_000_000:
+            raise ValueError("reference_init is meant for small nets; use init='fast'")
+        w = torch.tensor([libc.random() for _ in range(n)], dtype=torch.float64)
+        w = 2.0 * (w / rand_max - 0.5) / math.sqrt(M)
+        out.append(w.view(N, M))
+    return out
+
+
+def fast_init(sizes, seed):
+    """Same distribution U(-1,1)/sqrt(M) from torch's generator (large benchmark nets)."""
+    g = torch.Generator().manual_seed(seed)
+    return [((torch.rand(sizes[l + 1], sizes[l], generator=g, dtype=torch.float64) - 0.5) * 2.0
+             / math.sqrt(sizes[l])) for l in range(len(sizes) - 1)]
+
+
+class MLP:
+    """Network + device state for batched BF16 MFMA training on one GPU.
+
+    sizes: [n_in, h_1, ..., n_out]; net_type: 'ANN' | 'SNN' | 'LNN'.
+    batch: per-step (per-GPU) minibatch; padded to a multiple of 128 internally.
+    """
+
+    def __init__(self, sizes, net_type="SNN", batch=256, device="cuda", momentum=False, weights=None, seed=10958,
+                 init="reference", splits=None):
+        self.sizes = list(sizes)
+        self.L = len(sizes) - 1
+        self.type = TYPES[net_type] if isinstance(net_type, str) else int(net_type)
+        self.type_name = net_type if isinstance(net_type, str) else {v: k for k, v in TYPES.items()}[net_type]
+        self.device = torch.device(device)
+        self.batch = batch
+        self.Bp = ops.pad_to(batch, 128)
+        self.momentum = momentum
+        self.Kp = [ops.pad_to(sizes[l], 32) for l in range(self.L)]
+        self.Np = [ops.pad_to(sizes[l + 1], 32) for l in range(self.L)]
+        self.n_out = sizes[-1]
+        if weights is None:
+            weights = reference_init(sizes, seed) if init == "reference" else fast_init(sizes, seed)
+        dev = self.device
+        self.W32, self.V32, self.Wb, self.Wt, self.slab, self.S = [], [], [], [], [], []
+        for l in range(self.L):
+            N, K = self.Np[l], self.Kp[l]
+            w = torch.zeros(N, K, dtype=torch.float32)
+            w[:sizes[l + 1], :sizes[l]] = weights[l].to(torch.float32)
+            self.W32.append(w.to(dev))
+            self.V32.append(torch.zeros(N, K, dtype=torch.float32, device=dev) if momentum else None)
+            self.Wb.append(torch.empty(N, K, dtype=torch.bfloat16, device=dev))
+            self.Wt.append(torch.empty(K, N, dtype=torch.bfloat16, device=dev))
+            S = splits[l] if splits else self._pick_splits(N, K, self.Bp)
+            self.S.append(S)
+            self.slab.append(torch.empty(S, N, K, dtype=torch.float32, device=dev))
+        # flat FP32 gradient buffer (one view per layer: the DP all-reduce buckets)
+        sizes_g = [self.Np[l] * self.Kp[l] for l in range(self.L)]
+        self.grad_flat = torch.zeros(sum(sizes_g), dtype=torch.float32, device=dev)
+        self.G, off = [], 0
+        for l in range(self.L):
+            self.G.append(self.grad_flat[off:off + sizes_g[l]].view(self.Np[l], self.Kp[l]))
+            off += sizes_g[l]
+        self.H = [torch.empty(self.Bp, self.Np[l], dtype=torch.bfloat16, device=dev) for l in range(self.L - 1)]
+        self.D = [torch.empty(self.Bp, self.Np[l], dtype=torch.bfloat16, device=dev) for l in range(self.L)]
+        self.Z = torch.empty(self.Bp, self.Np[-1], dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)  # [loss sum, correct (uint32 bits)]
+        self.refresh_bf16()
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _pick_splits(N, K, Bp):
+        tn = 128 if N % 128 == 0 else (64 if N % 64 == 0 else 32)
+        tm = 128 if K % 128 == 0 else (64 if K % 64 == 0 else 32)
+        tiles = (N // tn) * (K // tm)
+        s = max(1, 1024 // max(tiles, 1))
+        s = min(s, max(1, Bp // 256))
+        while s > 1 and Bp % (64 * s):
+            s -= 1
+        return s
+
+    def refresh_bf16(self):
+        for l in range(self.L):
+            ops.cast_weights(self.W32[l], self.Wb[l], self.Wt[l])
+
+    def host_weights(self):
+        """FP64 [N, M] weights (unpadded), for kernel.opt dumps / parity checks."""
+        return [self.W32[l][:self.sizes[l + 1], :self.sizes[l]].double().cpu() for l in range(self.L)]
+
+    def prepare_input(self, X):
+        """float/double [n, n_in] -> padded BF16 [Bp, Kp0] device tensor."""
+        Xd = X.to(self.device)
+        out = torch.empty(ops.pad_to(X.shape[0], 128), self.Kp[0], dtype=torch.bfloat16, device=self.device)
+        return ops.pack_bf16(Xd.contiguous(), out)
+
+    # ------------------------------------------------------------------ phases
+    def forward(self, X):
+        for l in range(self.L):
+            A = X if l == 0 else self.H[l - 1]
+            if l == self.L - 1:
+                ops.gemm_nt(A, self.Wb[l], ops.EPI_NONE, out_f32=True, out=self.Z)
+            else:
+                ops.gemm_nt(A, self.Wb[l], ops.EPI_ACT, out=self.H[l])
+        return self.Z
+
+    def output(self, labels=None, T=None, n_valid=None, O=None):
+        t_hi, t_lo = (1.0, 0.0) if self.type == ops.TYPE_SNN else (1.0, -1.0)
+        ops.output_delta(self.Z, self.n_out, self.type, self.D[-1], labels=labels, T=T, t_hi=t_hi, t_lo=t_lo,
+                         n_valid=n_valid, O=O, loss_acc=self.stats[0:1], correct=self.stats[1:2])
+
+    def backward_layer(self, l):
+        """D[l-1] = (D[l] @ W_l) * f'(H[l-1]) (uses pre-update W_l^T)."""
+        ops.gemm_nt(self.D[l], self.Wt[l], ops.EPI_DACT, aux=self.H[l - 1], out=self.D[l - 1])
+
+    def grad_layer(self, l, X, reduce=False):
+        Hin = X if l == 0 else self.H[l - 1]
+        ops.gemm_tn(self.D[l], Hin, splits=self.S[l], out=self.slab[l])
+        if reduce:
+            ops.reduce_slabs(self.slab[l], self.G[l])
+
+    def update_layer(self, l, lr, alpha, scale, from_G=False):
+        G = self.G[l] if from_G else self.slab[l]
+        ops.sgd_update(self.W32[l], self.V32[l], G, self.Wb[l], self.Wt[l], lr, alpha, scale, self.momentum)
+
+    def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
+        """One minibatch fwd + bwd + update on the current stream (no host sync)."""
+        n_valid = self.Bp if n_valid is None else n_valid
+        self.forward(X)
+        self.output(labels=labels, T=T, n_valid=n_valid)
+        scale = 1.0 / n_valid
+        for l in range(self.L - 1, -1, -1):
+            if l > 0:
+                self.backward_layer(l)
+            self.grad_layer(l, X)
+            self.update_layer(l, lr, alpha, scale)
+
+    def predict(self, X, n_valid=None):
+        """network outputs [n_valid, n_out] (fp32)."""
+        n_valid = X.shape[0] if n_valid is None else n_valid
+        self.forward(X)
+        O = torch.empty(self.Bp, self.Np[-1], dtype=torch.float32, device=self.device)
+        Tz = torch.zeros(self.Bp, self.n_out, dtype=torch.float32, device=self.device)
+        ops.output_delta(self.Z, self.n_out, self.type, self.D[-1], T=Tz, n_valid=n_valid, O=O)
+        return O[:n_valid, :self.n_out]
+
+    def reset_stats(self):
+        self.stats.zero_()
+
+    def read_stats(self):
+        s = self.stats.cpu()
+        return float(s[0]), int(s[1:2].view(torch.int32)[0])

@@ -1,0 +1,192 @@
+"""gfx950 kernel wrappers (torch tensors in, raw pointers to libhpnn launchers).
+
+Every function launches on torch's current HIP stream, so it composes with torch
+streams/events and is captured by torch.cuda.graph.  `ref_*` functions are the plain
+PyTorch FP32 references used by the numerics tests (and by the CPU path of the
+distributed tests, which exercise the orchestration, not the kernels).
+"""
+import torch
+
+from .._lib import native
+
+EPI_NONE, EPI_ACT, EPI_DACT = 0, 1, 2
+TYPE_ANN, TYPE_LNN, TYPE_SNN = 0, 1, 2
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _cpu(t):
+    """CPU tensors run the PyTorch emulation of the kernel (same rounding points);
+    device tensors always run the native gfx950 kernel -- never a silent fallback."""
+    return t.device.type == "cpu"
+
+
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def pad_to(v, m):
+    return (v + m - 1) // m * m
+
+
+# --------------------------------------------------------------------------- kernels
+def gemm_nt(A, B, epi=EPI_NONE, aux=None, out_f32=False, out=None):
+    """C[M,N] = epi(A[M,K] @ B[N,K]^T); A, B bf16 row-major (row strides may exceed K).
+
+    epi: EPI_NONE, EPI_ACT (bipolar sigmoid), EPI_DACT (C *= -0.5(aux^2-1)).
+    Shapes: M % 128 == 0, N % 32 == 0, K % 32 == 0."""
+    M, K = A.shape
+    N = B.shape[0]
+    assert B.shape[1] == K and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32 if out_f32 else torch.bfloat16, device=A.device)
+    if _cpu(A):
+        out.copy_(ref_gemm_nt(A, B, epi, aux))
+        return out
+    native().gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), out.data_ptr(), out.stride(0),
+                          _ptr(aux), aux.stride(0) if aux is not None else 0, M, N, K, epi, int(out_f32), _stream())
+    return out
+
+
+def gemm_tn(D, H, splits=1, out=None):
+    """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m]  (FP32)."""
+    Bt, N = D.shape
+    M = H.shape[1]
+    if out is None:
+        out = torch.empty(splits, N, M, dtype=torch.float32, device=D.device)
+    if _cpu(D):
+        c = Bt // splits
+        for s_ in range(splits):
+            out[s_].copy_(ref_gemm_tn(D[s_ * c:(s_ + 1) * c], H[s_ * c:(s_ + 1) * c]))
+        return out
+    native().gemm_tn_bf16(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), out.data_ptr(), out.stride(1), N, M,
+                          Bt, splits, _stream())
+    return out
+
+
+def output_delta(Z, n_out, net_type, D, labels=None, T=None, t_hi=1.0, t_lo=0.0, n_valid=None, O=None,
+                 loss_acc=None, correct=None):
+    """Output layer: activation/softmax, loss sum, delta (bf16) and argmax hits."""
+    B = Z.shape[0]
+    if _cpu(Z):
+        return _cpu_output_delta(Z, n_out, net_type, D, labels, T, t_hi, t_lo, B if n_valid is None else int(n_valid),
+                                 O, loss_acc, correct)
+    native().output_delta(Z.data_ptr(), Z.stride(0), _ptr(T), T.stride(0) if T is not None else 0, _ptr(labels),
+                          float(t_hi), float(t_lo), D.data_ptr(), D.stride(0), _ptr(O),
+                          O.stride(0) if O is not None else 0, _ptr(loss_acc), _ptr(correct), B,
+                          B if n_valid is None else int(n_valid), n_out, net_type, _stream())
+    return D
+
+
+def reduce_slabs(slab, out):
+    S = slab.shape[0]
+    n = slab[0].numel()
+    if _cpu(slab):
+        out.view(-1).copy_(slab.reshape(S, -1).sum(0))
+        return out
+    native().reduce_slabs(slab.data_ptr(), S, slab.stride(0), n, out.data_ptr(), _stream())
+    return out
+
+
+def sgd_update(W32, V32, G, Wbf, Wt, lr, alpha=0.0, scale=1.0, momentum=False):
+    """W32[N,K] FP32 master; G: [S,N,K] or [N,K] FP32 gradient sum(s)."""
+    N, K = W32.shape
+    S = G.shape[0] if G.dim() == 3 else 1
+    gstride = G.stride(0) if G.dim() == 3 else 0
+    if _cpu(W32):
+        g = (G.sum(0) if G.dim() == 3 else G) * scale
+        if momentum:
+            V32 += lr * g
+            W32 += V32
+            V32 *= alpha
+        else:
+            W32 += lr * g
+        Wbf.copy_(W32.bfloat16())
+        Wt.copy_(W32.bfloat16().t())
+        return
+    native().sgd_update(W32.data_ptr(), _ptr(V32), G.data_ptr(), S, gstride, Wbf.data_ptr(), Wt.data_ptr(), N, K,
+                        float(lr), float(alpha), float(scale), int(momentum), _stream())
+
+
+def cast_weights(W32, Wbf, Wt):
+    N, K = W32.shape
+    if _cpu(W32):
+        Wbf.copy_(W32.bfloat16())
+        Wt.copy_(W32.bfloat16().t())
+        return
+    native().cast_weights(W32.data_ptr(), Wbf.data_ptr(), Wt.data_ptr(), N, K, _stream())
+
+
+def pack_bf16(src, dst):
+    """dst (bf16, padded) <- src (float32/float64 [rows, cols]); padding zero-filled."""
+    rows, cols = src.shape
+    if _cpu(dst):
+        dst.zero_()
+        dst[:rows, :cols] = src.float().bfloat16()
+        return dst
+    native().pack_bf16(src.data_ptr(), int(src.dtype == torch.float64), rows, cols, src.stride(0), dst.data_ptr(),
+                       dst.shape[0], dst.shape[1], dst.stride(0), _stream())
+    return dst
+
+
+# --------------------------------------------------------------------------- references
+def bipolar(x):
+    return 2.0 / (1.0 + torch.exp(-x)) - 1.0
+
+
+def dbipolar(y):
+    return -0.5 * (y * y - 1.0)
+
+
+def ref_gemm_nt(A, B, epi=EPI_NONE, aux=None):
+    C = A.float() @ B.float().t()
+    if epi == EPI_ACT:
+        C = bipolar(C)
+    elif epi == EPI_DACT:
+        C = C * dbipolar(aux.float())
+    return C
+
+
+def ref_gemm_tn(D, H):
+    return D.float().t() @ H.float()
+
+
+def ref_output(Z, n_out, net_type, T):
+    """returns (O, delta, per-sample loss) in fp32 following the reference formulas."""
+    z = Z[:, :n_out].float()
+    if net_type == TYPE_SNN:
+        m = z.max(dim=1, keepdim=True).values
+        e = torch.exp(z - m)
+        tiny = torch.exp(torch.clamp(torch.log(torch.tensor(1e-14)) + 1.0 - m, max=80.0))
+        o = e / (e.sum(1, keepdim=True) + tiny)
+        d = T - o
+        loss = -(T * torch.log(o + 1e-14) * (o > 0)).sum(1) / n_out
+    elif net_type == TYPE_ANN:
+        o = bipolar(z)
+        d = (T - o) * dbipolar(o)
+        loss = 0.5 * ((T - o) ** 2).sum(1)
+    else:
+        o = z
+        d = T - o
+        loss = 0.5 * ((T - o) ** 2).sum(1)
+    return o, d, loss
+
+
+def _cpu_output_delta(Z, n_out, net_type, D, labels, T, t_hi, t_lo, n_valid, O, loss_acc, correct):
+    B = Z.shape[0]
+    if T is None:
+        T = torch.full((B, n_out), t_lo, dtype=torch.float32)
+        T[torch.arange(B), labels.long()] = t_hi
+    o, d, loss = ref_output(Z, n_out, net_type, T[:, :n_out].float())
+    D.zero_()
+    D[:n_valid, :n_out] = d[:n_valid].bfloat16()
+    if O is not None:
+        O[:, :n_out] = o
+    if loss_acc is not None:
+        loss_acc += loss[:n_valid].sum()
+    if correct is not None:
+        hits = (o[:n_valid].argmax(1) == T[:n_valid, :n_out].argmax(1)).sum().to(torch.int32)
+        correct.view(torch.int32).add_(hits)
+    return D

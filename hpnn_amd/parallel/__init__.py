@@ -1,0 +1,2 @@
+"""Parallelism: data parallel (RCCL all-reduce) and row-sharded tensor parallel."""
+from .dp import DataParallel, init_from_env  # noqa: F401

@@ -1,0 +1,135 @@
+"""Numerics of the gfx950 kernels against plain PyTorch FP32 references."""
+import pytest
+import torch
+
+from hpnn_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, scale=1.0, dev="cuda"):
+    return ((torch.rand(*shape, device=dev) * 2 - 1) * scale)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 32, 32), (256, 64, 64), (384, 128, 800), (128, 96, 96), (256, 256, 4096),
+                                   (128, 32, 64), (256, 160, 224)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nt(gpu, M, N, K, epi):
+    torch.manual_seed(M + N + K + epi)
+    A = _rand(M, K).bfloat16()
+    # asymmetric B so a transposed store cannot pass
+    B = (_rand(N, K) + torch.arange(N, device="cuda")[:, None] * 0.01).bfloat16()
+    aux = _rand(M, N).bfloat16() if epi == ops.EPI_DACT else None
+    for f32 in (False, True):
+        C = ops.gemm_nt(A, B, epi, aux=aux, out_f32=f32)
+        R = ops.ref_gemm_nt(A, B, epi, aux)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (C.float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+
+
+def test_gemm_nt_identity(gpu):
+    """A = I checks the C layout with an asymmetric B (cdna guide section 3)."""
+    M, N, K = 128, 64, 128
+    A = torch.eye(M, K, device="cuda").bfloat16()
+    B = torch.arange(N * K, device="cuda", dtype=torch.float32).remainder(97).view(N, K).bfloat16()
+    C = ops.gemm_nt(A, B, out_f32=True)
+    assert torch.equal(C, B.float().t()[:M])
+
+
+def test_gemm_nt_strided(gpu):
+    M, N, K = 256, 64, 96
+    A_big = _rand(M, 160).bfloat16()
+    A = A_big[:, :K]
+    B = _rand(N, K).bfloat16()
+    C = ops.gemm_nt(A, B, out_f32=True)
+    R = ops.ref_gemm_nt(A, B)
+    assert (C - R).abs().max().item() < 2e-3 * R.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("Bt,N,M,S", [(64, 32, 32, 1), (256, 64, 64, 2), (512, 128, 800, 4), (1024, 32, 128, 8),
+                                      (256, 96, 160, 1), (2048, 256, 256, 4)])
+def test_gemm_tn(gpu, Bt, N, M, S):
+    torch.manual_seed(Bt + N + M)
+    D = (_rand(Bt, N) + torch.arange(N, device="cuda")[None, :] * 0.01).bfloat16()
+    H = _rand(Bt, M).bfloat16()
+    slab = ops.gemm_tn(D, H, splits=S)
+    G = slab.sum(0)
+    R = ops.ref_gemm_tn(D, H)
+    assert (G - R).abs().max().item() <= 1e-3 * R.abs().max().item() + 1e-4
+    # each slab is its own batch slice
+    c = Bt // S
+    R0 = ops.ref_gemm_tn(D[:c], H[:c])
+    assert (slab[0] - R0).abs().max().item() <= 1e-3 * R0.abs().max().item() + 1e-4
+
+
+def test_gemm_tn_integer_exact(gpu):
+    """small integers are exact in bf16/fp32: any index permutation shows up."""
+    Bt, N, M = 128, 32, 64
+    D = torch.randint(-3, 4, (Bt, N), device="cuda").float().bfloat16()
+    H = torch.randint(-3, 4, (Bt, M), device="cuda").float().bfloat16()
+    G = ops.gemm_tn(D, H, splits=2).sum(0)
+    assert torch.equal(G, ops.ref_gemm_tn(D, H))
+
+
+@pytest.mark.parametrize("net_type", [ops.TYPE_SNN, ops.TYPE_ANN, ops.TYPE_LNN])
+@pytest.mark.parametrize("n_out,ldz", [(10, 32), (230, 256), (64, 64)])
+def test_output_delta(gpu, net_type, n_out, ldz):
+    B, n_valid = 256, 200
+    torch.manual_seed(n_out + net_type)
+    Z = _rand(B, ldz, scale=3.0)
+    labels = torch.randint(0, n_out, (B,), device="cuda", dtype=torch.int32)
+    hi, lo = (1.0, 0.0) if net_type == ops.TYPE_SNN else (1.0, -1.0)
+    T = torch.full((B, n_out), lo, device="cuda")
+    T[torch.arange(B), labels.long()] = hi
+    D = torch.empty(B, ldz, dtype=torch.bfloat16, device="cuda")
+    O = torch.empty(B, ldz, device="cuda")
+    loss = torch.zeros(1, device="cuda")
+    corr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.output_delta(Z, n_out, net_type, D, labels=labels, t_hi=hi, t_lo=lo, n_valid=n_valid, O=O, loss_acc=loss,
+                     correct=corr)
+    o, d, l = ops.ref_output(Z, n_out, net_type, T)
+    assert (O[:, :n_out] - o).abs().max().item() < 1e-5
+    assert (D[:n_valid, :n_out].float() - d[:n_valid]).abs().max().item() < 1e-2 * max(1, d.abs().max().item())
+    assert D[n_valid:].float().abs().max().item() == 0.0
+    assert D[:, n_out:].float().abs().max().item() == 0.0
+    assert abs(loss.item() - l[:n_valid].sum().item()) < 1e-3 * max(1.0, abs(l[:n_valid].sum().item()))
+    hits = (o[:n_valid].argmax(1) == labels[:n_valid].long()).sum().item()
+    assert corr.item() == hits
+    # dense targets give the same delta
+    D2 = torch.empty_like(D)
+    ops.output_delta(Z, n_out, net_type, D2, T=T, n_valid=n_valid)
+    assert torch.equal(D, D2)
+
+
+@pytest.mark.parametrize("momentum", [False, True])
+def test_sgd_update(gpu, momentum):
+    N, K, S = 64, 96, 3
+    W = _rand(N, K)
+    V = _rand(N, K, scale=0.1) if momentum else None
+    G = _rand(S, N, K)
+    Wb = torch.empty(N, K, dtype=torch.bfloat16, device="cuda")
+    Wt = torch.empty(K, N, dtype=torch.bfloat16, device="cuda")
+    W0, V0 = W.clone(), (V.clone() if momentum else None)
+    lr, alpha, scale = 0.05, 0.2, 1.0 / 7
+    ops.sgd_update(W, V, G, Wb, Wt, lr, alpha, scale, momentum)
+    g = G.sum(0) * scale
+    if momentum:
+        v = V0 + lr * g
+        w = W0 + v
+        v = v * alpha
+        assert (V - v).abs().max().item() < 1e-6
+    else:
+        w = W0 + lr * g
+    assert (W - w).abs().max().item() < 1e-6
+    assert torch.equal(Wb, W.bfloat16())
+    assert torch.equal(Wt, W.bfloat16().t())
+
+
+def test_pack_bf16(gpu):
+    X = torch.rand(100, 784, dtype=torch.float64, device="cuda")
+    out = torch.full((128, 800), 7.0, dtype=torch.bfloat16, device="cuda")
+    ops.pack_bf16(X, out)
+    assert torch.equal(out[:100, :784], X.float().bfloat16())
+    assert out[100:].abs().max().item() == 0 and out[:, 784:].abs().max().item() == 0

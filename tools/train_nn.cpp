@@ -1,0 +1,83 @@
+/*
+ * train_nn -- train a libhpnn network from a configuration file.
+ *
+ * Workflow parity with the reference CLI (tests/train_nn.c:59-255):
+ *   init library -> parse flags -> load conf (generate or load weights)
+ *   -> dump kernel.tmp (weights before training) -> nn_train_kernel
+ *   -> dump kernel.opt (weights after training) -> deinit.
+ * With -x (dry run) the two dumps are skipped.
+ */
+#include <libhpnn.h>
+#include "cli_common.h"
+
+static void dump_help(void) {
+    _OUT(stdout, "***********************************\n");
+    _OUT(stdout, "usage:  train_nn [-options] [input]\n");
+    _OUT(stdout, "***********************************\n");
+    _OUT(stdout, "options:\n");
+    _OUT(stdout, "-h \tdisplay this help;\n");
+    _OUT(stdout, "-v \tincrease verbosity;\n");
+    _OUT(stdout, "-x \tdry run (do not write kernel files).\n");
+    _OUT(stdout, "-O N\thost threads.\n");
+    _OUT(stdout, "-B N\tBLAS threads (accepted, unused).\n");
+    _OUT(stdout, "-S N\tHIP streams per GPU.\n");
+    _OUT(stdout, "-G N\tnumber of GPUs.\n");
+    _OUT(stdout, "-b N\tminibatch size (batched mode).\n");
+    _OUT(stdout, "-e N\tepochs (batched mode).\n");
+    _OUT(stdout, "-m M\tmode: online | batched.\n");
+    _OUT(stdout, "-d D\tdtype: f64 | f32 | bf16.\n");
+    _OUT(stdout, "-l X\tlearning rate.  -a X momentum.\n");
+    _OUT(stdout, "-c \tforce the CPU engine.\n");
+    _OUT(stdout, "***********************************\n");
+    _OUT(stdout, "input: neural network conf file\n");
+    _OUT(stdout, "(default ./nn.conf)\n");
+    _OUT(stdout, "***********************************\n");
+}
+
+int main(int argc, char *argv[]) {
+    cli_opts o;
+    _NN(init, all)(0);
+    if (cli_parse(argc, argv, &o, 1)) {
+        dump_help();
+        _NN(deinit, all)();
+        return -1;
+    }
+    if (o.help) {
+        dump_help();
+        _NN(deinit, all)();
+        return 0;
+    }
+    cli_apply_runtime(&o);
+    nn_def *neural = _NN(load, conf)(o.conf);
+    if (!neural) {
+        _OUT(stderr, "FAILED to read NN configuration file! (ABORTING)\n");
+        _NN(deinit, all)();
+        return -1;
+    }
+    cli_apply_conf(&o, neural);
+    if (_NN(return, verbose)() > 1) _NN(dump, conf)(neural, stdout);
+    if (!_NN(return, dry)()) {
+        FILE *f = fopen("./kernel.tmp", "w");
+        if (!f) {
+            _OUT(stderr, "FAILED to open kernel.tmp for writing!\n");
+        } else {
+            _NN(dump, kernel)(neural, f);
+            fclose(f);
+        }
+    }
+    BOOL ok = _NN(train, kernel)(neural);
+    if (!ok) _OUT(stderr, "Training FAILED!\n");
+    if (!_NN(return, dry)()) {
+        FILE *f = fopen("./kernel.opt", "w");
+        if (!f) {
+            _OUT(stderr, "FAILED to open kernel.opt for writing!\n");
+        } else {
+            _NN(dump, kernel)(neural, f);
+            fclose(f);
+        }
+    }
+    _NN(deinit, conf)(neural);
+    free(neural);
+    _NN(deinit, all)();
+    return ok ? 0 : 1;
+}
