@@ -247,16 +247,21 @@ namespace {
 inline int pad32(int v) { return (v + 31) / 32 * 32; }
 inline int pad128(int v) { return (v + 127) / 128 * 128; }
 
-/* split-K factor for the weight-gradient GEMM: aim for ~1024 workgroups */
+/* split-K factor for the weight-gradient GEMM: ~512 workgroups, >= 1024 rows per
+ * split (fewer slabs keep the optimizer's slab reduction cheap). Mirrors
+ * hpnn_amd/models/mlp.py:MLP.pick_splits. */
+int tn_tile_m(int K) {
+    return K % 128 == 0 ? 128 : (K % 160 == 0 ? 160 : (K % 96 == 0 ? 96 : (K % 64 == 0 ? 64 : 32)));
+}
 int pick_splits(int Np, int Kp, int Bp) {
     const int tn = (Np % 128 == 0) ? 128 : (Np % 64 == 0 ? 64 : 32);
-    const int tm = (Kp % 128 == 0) ? 128 : (Kp % 64 == 0 ? 64 : 32);
+    const int tm = tn_tile_m(Kp);
     const int tiles = (Np / tn) * (Kp / tm);
-    int s = 1024 / (tiles > 0 ? tiles : 1);
-    if (s < 1) s = 1;
-    int maxs = Bp / 256;
+    int s = (512 + tiles - 1) / (tiles > 0 ? tiles : 1);
+    int maxs = Bp / 1024;
     if (maxs < 1) maxs = 1;
     if (s > maxs) s = maxs;
+    if (s < 1) s = 1;
     while (s > 1 && (Bp % (64 * s))) s--;
     return s;
 }

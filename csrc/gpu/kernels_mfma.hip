@@ -172,22 +172,15 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const __bf16 *__restrict__
 /* ---------------------------------------------------------------------- */
 /* TN GEMM (weight gradient)                                               */
 /* ---------------------------------------------------------------------- */
-/* LDS tile: 64 sample rows x W columns (bf16), rows of W*2 bytes split in
- * 32-byte segments XOR-swizzled so that the 8 rows a 32-lane half reads with
- * ds_read_b64_tr_b16 (rows 8g+q, g in {0,1}, q in 0..3) fall on distinct
- * banks. */
-template <int W>
-__device__ __forceinline__ int tn_seg_swz(int r) {
-    if constexpr (W == 32) return (r >> 3) & 1;
-    else if constexpr (W == 64) return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
-    else return (r & 3) | (((r >> 3) & 1) << 2);
-}
-/* byte offset of column `col` (multiple of 4) of row r */
+/* LDS tile: 64 sample rows x W columns (bf16, W any multiple of 32), stored as W/32
+ * sub-tiles of [64 rows][32 cols] (64-byte rows).  Inside a sub-tile the two 32-byte
+ * halves of a row are swapped for rows 8..15 mod 16, so the 8 rows that one 32-lane
+ * half reads with ds_read_b64_tr_b16 (rows 8g+q, g in {0,1}, q in 0..3) cover all 64
+ * banks exactly once. */
 template <int W>
 __device__ __forceinline__ int tn_off(int r, int col) {
-    constexpr int NSEG = W / 16;
-    const int seg = (col >> 4) ^ (tn_seg_swz<W>(r) & (NSEG - 1));
-    return r * (W * 2) + seg * 32 + (col & 15) * 2;
+    const int sub = col >> 5, c = col & 31;
+    return sub * (64 * 64) + r * 64 + ((((c >> 4) ^ (r >> 3)) & 1) << 5) + (c & 15) * 2;
 }
 
 template <int W>
@@ -368,6 +361,8 @@ extern "C" int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh,
     if (N % 32 || M % 32 || Bt % (64 * splits)) return -2;
     if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
     if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
+    if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
+    if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
     if (M % 64 == 0) return launch_tn_m<64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
     return launch_tn_m<32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
 }

@@ -53,6 +53,105 @@ __device__ __forceinline__ void wave_argmax(float &v, int &i) {
 
 constexpr float TINY = 1e-14f;
 
+__device__ __forceinline__ void block_reduce_store(float my_loss, unsigned int my_hit, float *loss_acc,
+                                                   unsigned int *correct) {
+    __shared__ float sloss[4];
+    __shared__ unsigned int shit[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    my_loss = wave_sum(my_loss);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) my_hit += __shfl_xor(my_hit, o, 64);
+    if (lane == 0) {
+        sloss[wave] = my_loss;
+        shit[wave] = my_hit;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = sloss[0] + sloss[1] + sloss[2] + sloss[3];
+        unsigned int h = shit[0] + shit[1] + shit[2] + shit[3];
+        if (loss_acc && s != 0.f) atomicAdd(loss_acc, s);
+        if (correct && h) atomicAdd(correct, h);
+    }
+}
+
+/* narrow outputs (n_out <= 64): one LANE per sample row, grid-stride, <= 256 blocks
+ * so the loss/accuracy atomics stay few (one per block) */
+template <int MAXO>
+__global__ __launch_bounds__(256) void output_delta_rows_kernel(const float *__restrict__ Z, int ldz,
+                                                                const float *__restrict__ T, int ldt,
+                                                                const int *__restrict__ labels, float t_hi, float t_lo,
+                                                                __bf16 *__restrict__ D, int ldd, float *__restrict__ O,
+                                                                int ldo, float *__restrict__ loss_acc,
+                                                                unsigned int *__restrict__ correct, int B, int n_valid,
+                                                                int n_out, int type) {
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < B; row += gridDim.x * blockDim.x) {
+        const bool valid = row < n_valid;
+        float z[MAXO];
+        const float *zr = Z + (size_t)row * ldz;
+#pragma unroll
+        for (int c = 0; c < MAXO; c++) z[c] = c < n_out ? zr[c] : 0.f;
+        float zmax = -INFINITY;
+        if (type == 2) {
+#pragma unroll
+            for (int c = 0; c < MAXO; c++)
+                if (c < n_out) zmax = fmaxf(zmax, z[c]);
+        }
+        float denom = 0.f;
+        if (type == 2) {
+#pragma unroll
+            for (int c = 0; c < MAXO; c++)
+                if (c < n_out) denom += __expf(z[c] - zmax);
+            denom += __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
+        }
+        const float inv = type == 2 ? 1.0f / denom : 0.f;
+        const int lab = (labels && valid) ? labels[row] : -1;
+        float l = 0.f, bo = -INFINITY, bt = -INFINITY;
+        int io = -1, it = -1;
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        __bf16 dv[MAXO];
+#pragma unroll
+        for (int c = 0; c < MAXO; c++) {
+            float d = 0.f;
+            if (c < n_out) {
+                float o;
+                if (type == 2) o = __expf(z[c] - zmax) * inv;
+                else if (type == 0) o = 2.0f / (1.0f + __expf(-z[c])) - 1.0f;
+                else o = z[c];
+                if (valid) {
+                    const float t = labels ? (c == lab ? t_hi : t_lo) : T[(size_t)row * ldt + c];
+                    if (type == 2) {
+                        if (o > 0.f) l += t * logf(o + TINY);
+                        d = t - o;
+                    } else if (type == 0) {
+                        l += (t - o) * (t - o);
+                        d = (t - o) * (-0.5f * (o * o - 1.0f));
+                    } else {
+                        l += (t - o) * (t - o);
+                        d = t - o;
+                    }
+                    if (o > bo) { bo = o; io = c; }
+                    if (t > bt) { bt = t; it = c; }
+                }
+                if (O) O[(size_t)row * ldo + c] = o;
+            }
+            dv[c] = (__bf16)d;
+        }
+        /* delta row: ldd bf16 (ldd <= MAXO, multiple of 4) */
+        __bf16 *dr = D + (size_t)row * ldd;
+#pragma unroll
+        for (int c = 0; c < MAXO; c += 4)
+            if (c < ldd) *(bf16x4 *)(dr + c) = bf16x4{dv[c], dv[c + 1], dv[c + 2], dv[c + 3]};
+        if (valid) {
+            my_loss += (type == 2) ? -l / (float)n_out : 0.5f * l;
+            my_hit += (io == it) ? 1u : 0u;
+        }
+    }
+    block_reduce_store(my_loss, my_hit, loss_acc, correct);
+}
+
+/* wide outputs: one WAVE per sample row, grid-stride */
 __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restrict__ Z, int ldz,
                                                            const float *__restrict__ T, int ldt,
                                                            const int *__restrict__ labels, float t_hi, float t_lo,
@@ -60,16 +159,12 @@ __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restri
                                                            int ldo, float *__restrict__ loss_acc,
                                                            unsigned int *__restrict__ correct, int B, int n_valid,
                                                            int n_out, int type) {
-    __shared__ float sloss[4];
-    __shared__ unsigned int shit[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int row = blockIdx.x * 4 + wave;
     float my_loss = 0.f;
     unsigned int my_hit = 0;
-    if (row < B) {
+    for (int row = blockIdx.x * 4 + wave; row < B; row += gridDim.x * 4) {
         const bool valid = row < n_valid;
         const int lab = (labels && valid) ? labels[row] : -1;
-        /* pass 1: output values (kept in registers, <= 64 columns per lane chunk) */
         float zmax = -INFINITY;
         if (type == 2) {
             for (int c = lane; c < n_out; c += 64) zmax = fmaxf(zmax, Z[(size_t)row * ldz + c]);
@@ -80,8 +175,7 @@ __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restri
             for (int c = lane; c < n_out; c += 64) denom += __expf(Z[(size_t)row * ldz + c] - zmax);
             denom = wave_sum(denom);
             /* reference: e^{z-1} / (TINY + sum e^{z-1}); shifted by m=zmax */
-            const float tiny_term = __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
-            denom += tiny_term;
+            denom += __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
         }
         const float inv = type == 2 ? 1.0f / denom : 0.f;
         float bo = -INFINITY, bt = -INFINITY;
@@ -95,8 +189,8 @@ __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restri
                 if (type == 2) o = __expf(z - zmax) * inv;
                 else if (type == 0) o = 2.0f / (1.0f + __expf(-z)) - 1.0f;
                 else o = z;
-                float t = labels ? (c == lab ? t_hi : t_lo) : (valid ? T[(size_t)row * ldt + c] : 0.f);
                 if (valid) {
+                    const float t = labels ? (c == lab ? t_hi : t_lo) : T[(size_t)row * ldt + c];
                     if (type == 2) {
                         if (o > 0.f) l += t * logf(o + TINY);
                         d = t - o;
@@ -114,25 +208,15 @@ __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restri
             }
             if (c < ldd) D[(size_t)row * ldd + c] = (__bf16)d;
         }
-        if (valid) {
-            l = wave_sum(l);
-            my_loss = (type == 2) ? -l / (float)n_out : 0.5f * l;
-            wave_argmax(bo, io);
-            wave_argmax(bt, it);
-            my_hit = (io == it) ? 1u : 0u;
+        l = wave_sum(l);
+        wave_argmax(bo, io);
+        wave_argmax(bt, it);
+        if (valid && lane == 0) {
+            my_loss += (type == 2) ? -l / (float)n_out : 0.5f * l;
+            my_hit += (io == it) ? 1u : 0u;
         }
     }
-    if (lane == 0) {
-        sloss[wave] = my_loss;
-        shit[wave] = my_hit;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float s = sloss[0] + sloss[1] + sloss[2] + sloss[3];
-        unsigned int h = shit[0] + shit[1] + shit[2] + shit[3];
-        if (loss_acc && s != 0.f) atomicAdd(loss_acc, s);
-        if (correct && h) atomicAdd(correct, h);
-    }
+    block_reduce_store(my_loss, my_hit, loss_acc, correct);
 }
 
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *__restrict__ slab, int S, long stride, long n4,
@@ -157,7 +241,19 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float *__restrict__ W32
     const int n = tn * 32 + ty, k = tk * 32 + tx * 4;
     const size_t idx = (size_t)n * K + k;
     f32x4 g = *(const f32x4 *)(G + idx);
-    for (int s = 1; s < S; s++) g += *(const f32x4 *)(G + s * gstride + idx);
+    {
+        /* four independent partial sums keep several slab loads in flight */
+        f32x4 g1 = {0.f, 0.f, 0.f, 0.f}, g2 = g1, g3 = g1;
+        int s = 1;
+        for (; s + 3 < S; s += 4) {
+            g += *(const f32x4 *)(G + (long)s * gstride + idx);
+            g1 += *(const f32x4 *)(G + (long)(s + 1) * gstride + idx);
+            g2 += *(const f32x4 *)(G + (long)(s + 2) * gstride + idx);
+            g3 += *(const f32x4 *)(G + (long)(s + 3) * gstride + idx);
+        }
+        for (; s < S; s++) g += *(const f32x4 *)(G + (long)s * gstride + idx);
+        g += (g1 + g2) + g3;
+    }
     f32x4 w = *(const f32x4 *)(W32 + idx);
     if (momentum) {
         f32x4 v = *(const f32x4 *)(V32 + idx);
@@ -220,8 +316,15 @@ extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ld
                                  hipStream_t stream) {
     if (B <= 0 || n_out <= 0 || ldz < n_out || ldd < n_out) return -1;
     if (!labels && !T) return -1;
-    hipLaunchKernelGGL(output_delta_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
-                       t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    if (ldd <= 32 && ldd % 4 == 0) {
+        const int grid = (B + 255) / 256 < 256 ? (B + 255) / 256 : 256;
+        hipLaunchKernelGGL(output_delta_rows_kernel<32>, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels,
+                           t_hi, t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    } else {
+        const int grid = (B + 3) / 4 < 256 ? (B + 3) / 4 : 256;
+        hipLaunchKernelGGL(output_delta_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
+                           t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -101,11 +101,12 @@ class MLP:
     # ------------------------------------------------------------------ helpers
     @staticmethod
     def _pick_splits(N, K, Bp):
+        """split-K factor of the weight-gradient GEMM (mirrors csrc/gpu/gpu_engine.cpp)."""
         tn = 128 if N % 128 == 0 else (64 if N % 64 == 0 else 32)
-        tm = 128 if K % 128 == 0 else (64 if K % 64 == 0 else 32)
+        tm = next(t for t in (128, 160, 96, 64, 32) if K % t == 0)
         tiles = (N // tn) * (K // tm)
-        s = max(1, 1024 // max(tiles, 1))
-        s = min(s, max(1, Bp // 256))
+        s = -(-512 // max(tiles, 1))
+        s = max(1, min(s, max(1, Bp // 1024)))
         while s > 1 and Bp % (64 * s):
             s -= 1
         return s

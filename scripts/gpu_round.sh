@@ -24,6 +24,6 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
 fi
 if [ "$what" = prof ] || [ "$what" = all ]; then
   export TMPDIR=/tmp
-  step rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0
+  step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0
 fi
 echo DONE

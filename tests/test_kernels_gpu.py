@@ -93,7 +93,8 @@ def test_output_delta(gpu, net_type, n_out, ldz):
     assert (O[:, :n_out] - o).abs().max().item() < 1e-5
     assert (D[:n_valid, :n_out].float() - d[:n_valid]).abs().max().item() < 1e-2 * max(1, d.abs().max().item())
     assert D[n_valid:].float().abs().max().item() == 0.0
-    assert D[:, n_out:].float().abs().max().item() == 0.0
+    if ldz > n_out:
+        assert D[:, n_out:].float().abs().max().item() == 0.0
     assert abs(loss.item() - l[:n_valid].sum().item()) < 1e-3 * max(1.0, abs(l[:n_valid].sum().item()))
     hits = (o[:n_valid].argmax(1) == labels[:n_valid].long()).sum().item()
     assert corr.item() == hits

@@ -28,14 +28,12 @@ def test_train_step_matches_oracle(gpu, net_type, sizes, momentum):
     T[torch.arange(B), labels] = 1.0
     # the oracle sees the same bf16-rounded inputs and weights the kernels see
     Xb = X.float().bfloat16().double()
-    Wb = [w.float().bfloat16().double() for w in W64]
     Xd = m.prepare_input(X)
     lab = labels.to(torch.int32).cuda()
+    loss_total = 0.0
     for step in range(3):
         m.train_step(Xd, labels=lab, lr=0.05, alpha=0.2)
-        loss = ref.batched_step(W64, Xb, T, net_type, 0.05, V64, 0.2)
-        Wb_ = Wb  # noqa: F841
-        Xb = Xb
+        loss_total += ref.batched_step(W64, Xb, T, net_type, 0.05, V64, 0.2).item()
     torch.cuda.synchronize()
     got = m.host_weights()
     W0 = [w.float().double() for w in MLP(sizes, net_type, batch=B, momentum=momentum, seed=7).host_weights()]
@@ -45,7 +43,7 @@ def test_train_step_matches_oracle(gpu, net_type, sizes, momentum):
         rel = (dg - dr).norm() / (dr.norm() + 1e-30)
         assert rel < 0.05, (l, rel.item())
     lsum, corr = m.read_stats()
-    assert lsum == pytest.approx(3 * loss.item() * B, rel=0.1)
+    assert lsum == pytest.approx(loss_total * B, rel=0.05)
 
 
 def test_predict_matches_forward(gpu):
