@@ -75,6 +75,16 @@ int hpnn_cast_weights(const float *W32, void *Wbf, void *Wt, int N, int K, hipSt
 /* zero-fill helper usable inside graphs */
 int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream);
 
+/* fused middle of a 3-layer MLP (kernels_mlp3.hip): H1 [Bp x 128] -> delta1
+ * [Bp x 128] + per-block [G1 (64 x 128) | G2 (32 x 64)] FP32 slabs (grid of them),
+ * loss / accuracy.  Dims must be h1=128, h2=64, no=32 (padded), n_out <= 32. */
+int hpnn_mlp3_mid(const void *H1g, const void *W1, const void *W1t, const void *W2, const void *W2t,
+                  const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
+                  float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int h1, int h2,
+                  int no, int grid, hipStream_t stream);
+/* slab reduction with 4 waves per 256 outputs (many loads in flight) */
+int hpnn_reduce_slabs_wide(const float *slab, int S, long stride, long n, float *out, hipStream_t stream);
+
 /* online (batch-1) FP64 persistent engine, see online.hip */
 typedef struct {
     int L;

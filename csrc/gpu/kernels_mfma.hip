@@ -20,15 +20,19 @@
  *             transposing LDS read), so neither the input nor the deltas are
  *             ever transposed in memory.
  *
- * Structure: 256 threads (4 wave64), LDS double buffer, register staging
- * with 16-byte global loads, one barrier per K step, XOR-swizzled LDS rows
- * so the 16-lane ds_read_b128 / ds_read_b64_tr_b16 groups hit distinct
- * banks.
+ * Structure: 256 threads (4 wave64); operands stream HBM -> LDS with
+ * global_load_lds_dwordx4 (LDS-DMA, no VGPR staging) through a STAGES-deep
+ * ring sized to ~64-72 KiB (2 workgroups per CU); one counted
+ * `s_waitcnt vmcnt(N)` + raw s_barrier per K step keeps STAGES-1 stages in
+ * flight (a __syncthreads() would drain them); the swizzles of the LDS images
+ * are applied on the DMA source address and were checked with a bank
+ * simulation (conflict-free ds_read_b128 / ds_read_b64_tr_b16).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "kernels.h"
+#include "mfma_common.h"
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -38,7 +42,7 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 namespace {
 
-__device__ __forceinline__ float bipolar(float x) { return 2.0f / (1.0f + __expf(-x)) - 1.0f; }
+using hpnn::bipolar;
 
 /* ---------------------------------------------------------------------- */
 /* NT GEMM                                                                 */
@@ -47,62 +51,87 @@ __device__ __forceinline__ float bipolar(float x) { return 2.0f / (1.0f + __expf
 template <int CPR>
 __device__ __forceinline__ int nt_off(int r, int c) {
     if constexpr (CPR == 8) return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
-    else return r * 64 + ((c ^ ((r >> 2) & 3)) << 4);
+    else return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); /* bank-simulated: conflict-free */
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int EPI, bool CF32>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(const __bf16 *__restrict__ A, int lda,
-                                                      const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
-                                                      int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
-                                                      int tiles_n) {
-    constexpr int NT = 256;
+/* ---------------------------------------------------------------------- */
+/* NT GEMM, LDS-DMA pipelined (global_load_lds_dwordx4, STAGES-deep ring)   */
+/* ---------------------------------------------------------------------- */
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+/* wait until at most LPS*rem LDS-DMA loads of this wave are outstanding */
+template <int LPS, int STAGES>
+__device__ __forceinline__ void wait_stage(int rem) {
+    static_assert(LPS * (STAGES - 1) < 64, "vmcnt budget");
+    if constexpr (STAGES >= 8) { if (rem >= 7) { wait_vm<LPS * 7>(); return; } }
+    if constexpr (STAGES >= 7) { if (rem >= 6) { wait_vm<LPS * 6>(); return; } }
+    if constexpr (STAGES >= 6) { if (rem >= 5) { wait_vm<LPS * 5>(); return; } }
+    if constexpr (STAGES >= 5) { if (rem >= 4) { wait_vm<LPS * 4>(); return; } }
+    if constexpr (STAGES >= 4) { if (rem >= 3) { wait_vm<LPS * 3>(); return; } }
+    if constexpr (STAGES >= 3) { if (rem >= 2) { wait_vm<LPS * 2>(); return; } }
+    if (rem >= 1) { wait_vm<LPS>(); return; }
+    wait_vm<0>();
+}
+
+/* One 1-KiB LDS-DMA piece of a [rows][BK] bf16 tile: lane i writes LDS bytes
+ * [16i, 16i+16) of the piece, i.e. physical chunk (16i % RB)/16 of row 16i/RB;
+ * it fetches the LOGICAL chunk that nt_off<> maps there (source-side swizzle). */
+template <int BK>
+__device__ __forceinline__ void glds_piece(const char *gbase, size_t ld_bytes, char *lds_piece, int row0, int lane) {
+    constexpr int RB = BK * 2;           /* bytes per LDS row */
+    constexpr int CPR = BK / 8;
+    const int r = row0 + (lane * 16) / RB;
+    const int cp = (lane * 16 % RB) >> 4;
+    const int cl = (CPR == 8) ? (cp ^ ((r >> 1) & 7)) : (cp ^ ((r >> 1) & 3));
+    const char *src = gbase + (size_t)r * ld_bytes + cl * 16;
+    __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)lds_piece, 16, 0, 0);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int EPI, bool CF32>
+__global__ __launch_bounds__(256) void gemm_nt_pipe_kernel(const __bf16 *__restrict__ A, int lda,
+                                                           const __bf16 *__restrict__ B, int ldb,
+                                                           void *__restrict__ C, int ldc,
+                                                           const __bf16 *__restrict__ aux, int ldaux, int K,
+                                                           int tiles_n) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int FM = WTM / 16, FN = WTN / 16;
     constexpr int CPR = BK / 8;
-    constexpr int A_CH = BM * CPR, B_CH = BN * CPR;
-    constexpr int A_PER = (A_CH + NT - 1) / NT, B_PER = (B_CH + NT - 1) / NT;
-    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-    constexpr int STAGE = A_BYTES + B_BYTES;
-    static_assert(WM * WN == 4, "4 waves");
-    static_assert(FM >= 1 && FN >= 1, "wave tile");
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    constexpr int RB = BK * 2;
+    constexpr int ROWS_PER_PIECE = 1024 / RB;
+    constexpr int A_PIECES = BM / ROWS_PER_PIECE, B_PIECES = BN / ROWS_PER_PIECE;
+    constexpr int PIECES = A_PIECES + B_PIECES;
+    /* every wave issues exactly LPS LDS-DMA loads per stage (a wave short of work
+     * re-issues the last piece: same bytes to the same place), so one counted
+     * vmcnt is exact for all waves */
+    constexpr int LPS = (PIECES + 3) / 4;
+    constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
+    static_assert(WM * WN == 4 && FM >= 1 && FN >= 1, "wave tiling");
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int KT = K / BK;
-
     const char *Ag = (const char *)(A + (size_t)m0 * lda);
     const char *Bg = (const char *)(B + (size_t)n0 * ldb);
+    const size_t lda_b = (size_t)lda * 2, ldb_b = (size_t)ldb * 2;
 
-    uint4 ra[A_PER], rb[B_PER];
-    auto gload = [&](int kt) {
+    auto issue = [&](int slot, int kt) {
+        char *sa = lds + slot * STAGE, *sb = sa + A_BYTES;
+        const char *ga = Ag + (size_t)kt * RB, *gb = Bg + (size_t)kt * RB;
 #pragma unroll
-        for (int i = 0; i < A_PER; i++) {
-            int c = tid + i * NT, r = c / CPR, ch = c % CPR;
-            if (A_PER * NT == A_CH || c < A_CH)
-                ra[i] = *(const uint4 *)(Ag + ((size_t)r * lda + (size_t)kt * BK + ch * 8) * 2);
-        }
-#pragma unroll
-        for (int i = 0; i < B_PER; i++) {
-            int c = tid + i * NT, r = c / CPR, ch = c % CPR;
-            if (B_PER * NT == B_CH || c < B_CH)
-                rb[i] = *(const uint4 *)(Bg + ((size_t)r * ldb + (size_t)kt * BK + ch * 8) * 2);
-        }
-    };
-    auto lstore = [&](int buf) {
-        char *sa = lds + buf * STAGE, *sb = sa + A_BYTES;
-#pragma unroll
-        for (int i = 0; i < A_PER; i++) {
-            int c = tid + i * NT, r = c / CPR, ch = c % CPR;
-            if (A_PER * NT == A_CH || c < A_CH) *(uint4 *)(sa + nt_off<CPR>(r, ch)) = ra[i];
-        }
-#pragma unroll
-        for (int i = 0; i < B_PER; i++) {
-            int c = tid + i * NT, r = c / CPR, ch = c % CPR;
-            if (B_PER * NT == B_CH || c < B_CH) *(uint4 *)(sb + nt_off<CPR>(r, ch)) = rb[i];
+        for (int i = 0; i < LPS; i++) {
+            int c = wave + 4 * i;
+            c = c < PIECES ? c : PIECES - 1;
+            if (c < A_PIECES) glds_piece<BK>(ga, lda_b, sa + c * 1024, c * ROWS_PER_PIECE, lane);
+            else glds_piece<BK>(gb, ldb_b, sb + (c - A_PIECES) * 1024, (c - A_PIECES) * ROWS_PER_PIECE, lane);
         }
     };
 
@@ -112,14 +141,17 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const __bf16 *__restrict__
 #pragma unroll
         for (int j = 0; j < FM; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    gload(0);
-    lstore(0);
-    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < STAGES - 1; st++)
+        if (st < KT) issue(st, st);
     const int r16 = lane & 15, q = lane >> 4;
     for (int kt = 0; kt < KT; kt++) {
-        const int cur = kt & 1;
-        if (kt + 1 < KT) gload(kt + 1);
-        const char *sa = lds + cur * STAGE, *sb = sa + A_BYTES;
+        const int nxt = kt + STAGES - 1;
+        if (nxt < KT) issue(nxt % STAGES, nxt);
+        const int last = nxt < KT ? nxt : KT - 1;
+        wait_stage<LPS, STAGES>(last - kt);
+        __builtin_amdgcn_s_barrier();
+        const char *sa = lds + (kt % STAGES) * STAGE, *sb = sa + A_BYTES;
 #pragma unroll
         for (int kk = 0; kk < BK / 32; kk++) {
             const int ch = kk * 4 + q;
@@ -134,11 +166,11 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const __bf16 *__restrict__
                 for (int j = 0; j < FM; j++)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < KT) lstore(cur ^ 1);
-        __syncthreads();
+        /* every wave's LDS reads of this slot retire before anyone refills it */
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
 
-    /* epilogue: lane holds D[f = 4q + r][b = r16] of each 16x16 tile */
 #pragma unroll
     for (int i = 0; i < FN; i++) {
 #pragma unroll
@@ -172,85 +204,52 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const __bf16 *__restrict__
 /* ---------------------------------------------------------------------- */
 /* TN GEMM (weight gradient)                                               */
 /* ---------------------------------------------------------------------- */
-/* LDS tile: 64 sample rows x W columns (bf16, W any multiple of 32), stored as W/32
- * sub-tiles of [64 rows][32 cols] (64-byte rows).  Inside a sub-tile the two 32-byte
- * halves of a row are swapped for rows 8..15 mod 16, so the 8 rows that one 32-lane
- * half reads with ds_read_b64_tr_b16 (rows 8g+q, g in {0,1}, q in 0..3) cover all 64
- * banks exactly once. */
-template <int W>
-__device__ __forceinline__ int tn_off(int r, int col) {
-    const int sub = col >> 5, c = col & 31;
-    return sub * (64 * 64) + r * 64 + ((((c >> 4) ^ (r >> 3)) & 1) << 5) + (c & 15) * 2;
+/* TN GEMM, LDS-DMA pipelined.  Stage = BKR sample rows of the H tile (TM cols) and
+ * of the D tile (TN cols), both as T32 images (mfma_common.h) with BKR rows. */
+template <int BKR>
+__device__ __forceinline__ void glds_tn_piece(const char *gbase, size_t ld_bytes, char *lds_tile, int piece,
+                                              int lane) {
+    hpnn::glds_t32_piece<BKR>(gbase, ld_bytes, lds_tile, piece, lane);
+}
+template <int BKR>
+__device__ __forceinline__ bf16x8 tnp_frag(const char *tile, int kbase, int c0, int lane) {
+    return hpnn::frag_tr<BKR>(tile, kbase, c0, lane);
 }
 
-template <int W>
-__device__ __forceinline__ bf16x8 tn_frag(const char *tile, int kbase, int c0, int lane) {
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int row = kbase + 8 * g + q;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tile + tn_off<W>(row, c0 + 4 * p)));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tile + tn_off<W>(row + 4, c0 + 4 * p)));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-}
-
-template <int TM, int TN>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(const __bf16 *__restrict__ D, int ldd,
-                                                      const __bf16 *__restrict__ H, int ldh, float *__restrict__ slab,
-                                                      int ldg, int N, int chunk, int tiles_n) {
-    constexpr int NT = 256, BK = 64;
+template <int TM, int TN, int BKR, int STAGES>
+__global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
+                                                           const __bf16 *__restrict__ H, int ldh,
+                                                           float *__restrict__ slab, int ldg, int N, int chunk,
+                                                           int tiles_n) {
     constexpr int WTM = TM / 2, WTN = TN / 2;
     constexpr int FM = WTM / 16, FN = WTN / 16;
-    constexpr int H_CH = BK * TM / 8, D_CH = BK * TN / 8; /* 16-byte chunks per stage */
-    constexpr int H_PER = (H_CH + NT - 1) / NT, D_PER = (D_CH + NT - 1) / NT;
-    constexpr int H_BYTES = BK * TM * 2, D_BYTES = BK * TN * 2, STAGE = H_BYTES + D_BYTES;
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    constexpr int H_PIECES = (TM / 32) * (BKR / 16), D_PIECES = (TN / 32) * (BKR / 16);
+    constexpr int PIECES = H_PIECES + D_PIECES;
+    constexpr int LPS = (PIECES + 3) / 4;
+    constexpr int H_BYTES = BKR * TM * 2, STAGE = BKR * (TM + TN) * 2;
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
     const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
     const int m0 = tm * TM, n0 = tn * TN;
     const int split = blockIdx.y;
     const int b0 = split * chunk;
-    const int KT = chunk / BK;
+    const int KT = chunk / BKR;
+    const size_t ldh_b = (size_t)ldh * 2, ldd_b = (size_t)ldd * 2;
+    const char *Hg = (const char *)(H + (size_t)b0 * ldh + m0);
+    const char *Dg = (const char *)(D + (size_t)b0 * ldd + n0);
 
-    uint4 rh[H_PER], rd[D_PER];
-    auto gload = [&](int kt) {
-        const int rbase = b0 + kt * BK;
+    auto issue = [&](int slot, int kt) {
+        char *sh = lds + slot * STAGE, *sd = sh + H_BYTES;
+        const char *gh = Hg + (size_t)kt * BKR * ldh_b, *gd = Dg + (size_t)kt * BKR * ldd_b;
 #pragma unroll
-        for (int i = 0; i < H_PER; i++) {
-            int c = tid + i * NT;
-            if (H_PER * NT == H_CH || c < H_CH) {
-                int r = c / (TM / 8), ch = c % (TM / 8);
-                rh[i] = *(const uint4 *)(H + (size_t)(rbase + r) * ldh + m0 + ch * 8);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < D_PER; i++) {
-            int c = tid + i * NT;
-            if (D_PER * NT == D_CH || c < D_CH) {
-                int r = c / (TN / 8), ch = c % (TN / 8);
-                rd[i] = *(const uint4 *)(D + (size_t)(rbase + r) * ldd + n0 + ch * 8);
-            }
-        }
-    };
-    auto lstore = [&](int buf) {
-        char *sh = lds + buf * STAGE, *sd = sh + H_BYTES;
-#pragma unroll
-        for (int i = 0; i < H_PER; i++) {
-            int c = tid + i * NT;
-            if (H_PER * NT == H_CH || c < H_CH) {
-                int r = c / (TM / 8), ch = c % (TM / 8);
-                *(uint4 *)(sh + tn_off<TM>(r, ch * 8)) = rh[i];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < D_PER; i++) {
-            int c = tid + i * NT;
-            if (D_PER * NT == D_CH || c < D_CH) {
-                int r = c / (TN / 8), ch = c % (TN / 8);
-                *(uint4 *)(sd + tn_off<TN>(r, ch * 8)) = rd[i];
-            }
+        for (int i = 0; i < LPS; i++) {
+            int c = wave + 4 * i;
+            c = c < PIECES ? c : PIECES - 1;
+            if (c < H_PIECES) glds_tn_piece<BKR>(gh, ldh_b, sh, c, lane);
+            else glds_tn_piece<BKR>(gd, ldd_b, sd, c - H_PIECES, lane);
         }
     };
 
@@ -260,30 +259,32 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const __bf16 *__restrict__
 #pragma unroll
         for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    for (int kt = 0; kt < KT; kt++) {
-        const int cur = kt & 1;
-        if (kt + 1 < KT) gload(kt + 1);
-        const char *sh = lds + cur * STAGE, *sd = sh + H_BYTES;
 #pragma unroll
-        for (int kk = 0; kk < BK / 32; kk++) {
+    for (int st = 0; st < STAGES - 1; st++)
+        if (st < KT) issue(st, st);
+    for (int kt = 0; kt < KT; kt++) {
+        const int nxt = kt + STAGES - 1;
+        if (nxt < KT) issue(nxt % STAGES, nxt);
+        const int last = nxt < KT ? nxt : KT - 1;
+        wait_stage<LPS, STAGES>(last - kt);
+        __builtin_amdgcn_s_barrier();
+        const char *sh = lds + (kt % STAGES) * STAGE, *sd = sh + H_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < BKR / 32; kk++) {
             bf16x8 fh[FM], fd[FN];
 #pragma unroll
-            for (int i = 0; i < FM; i++) fh[i] = tn_frag<TM>(sh, kk * 32, wm * WTM + i * 16, lane);
+            for (int i = 0; i < FM; i++) fh[i] = tnp_frag<BKR>(sh, kk * 32, wm * WTM + i * 16, lane);
 #pragma unroll
-            for (int j = 0; j < FN; j++) fd[j] = tn_frag<TN>(sd, kk * 32, wn * WTN + j * 16, lane);
+            for (int j = 0; j < FN; j++) fd[j] = tnp_frag<BKR>(sd, kk * 32, wn * WTN + j * 16, lane);
 #pragma unroll
             for (int i = 0; i < FM; i++)
 #pragma unroll
                 for (int j = 0; j < FN; j++)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], fd[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < KT) lstore(cur ^ 1);
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
-    /* lane holds acc[m = 4*(lane>>4) + r][n = lane & 15] */
     float *out = slab + (size_t)split * N * ldg;
     const int r16 = lane & 15, q = lane >> 4;
 #pragma unroll
@@ -302,9 +303,13 @@ int launch_nt_bn(const void *A, int lda, const void *B, int ldb, void *C, int ld
     constexpr int BM = 128;
     constexpr int WM = (BN == 128) ? 2 : 4;
     constexpr int WN = 4 / WM;
+    /* ring depth: ~64 KiB of staging -> 2 workgroups per CU */
+    constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
+    constexpr int ST = (65536 / STAGE_BYTES) < 2 ? 2 : ((65536 / STAGE_BYTES) > 5 ? 5 : (65536 / STAGE_BYTES));
     const int tiles_n = N / BN, tiles_m = M / BM;
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, WM, WN, EPI, CF32>), dim3(tiles_m * tiles_n), dim3(256), 0, s,
-                       (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n);
+    hipLaunchKernelGGL((gemm_nt_pipe_kernel<BM, BN, BK, WM, WN, ST, EPI, CF32>), dim3(tiles_m * tiles_n), dim3(256), 0,
+                       s, (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K,
+                       tiles_n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -325,8 +330,14 @@ template <int TM, int TN>
 int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s) {
     const int tiles_n = N / TN, tiles_m = M / TM;
-    hipLaunchKernelGGL((gemm_tn_kernel<TM, TN>), dim3(tiles_m * tiles_n, splits), dim3(256), 0, s, (const __bf16 *)D,
-                       ldd, (const __bf16 *)H, ldh, slab, ldg, N, Bt / splits, tiles_n);
+    const int chunk = Bt / splits;
+    /* 32-row stages, ring of ~72 KiB (2 workgroups per CU) */
+    constexpr int BKR = 32;
+    constexpr int STAGE = BKR * (TM + TN) * 2;
+    constexpr int ST = (73728 / STAGE) < 2 ? 2 : ((73728 / STAGE) > 6 ? 6 : (73728 / STAGE));
+    if (chunk % BKR) return -2;
+    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles_m * tiles_n, splits), dim3(256), 0, s,
+                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, chunk, tiles_n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -1,0 +1,96 @@
+/*
+ * Shared gfx950 MFMA / LDS helpers for the libhpnn HIP kernels.
+ *
+ * LDS activation image ("T32 image"): a [rows][cols] bf16 tile stored as cols/32
+ * sub-tiles of [rows][32] (64-byte rows); inside a sub-tile the four 16-byte chunks
+ * of row r are permuted by chunk ^ g(r), g(r) = bit1(r) | bit3(r) << 1 (found by
+ * an exhaustive bank simulation: conflict-free ds_read_b128 row reads and
+ * ds_read_b64_tr_b16 transposed reads, 2-way -- the minimum for this shape --
+ * ds_write_b64 of MFMA accumulator rows).  One image serves
+ *   - row reads      (ds_read_b128, 8 consecutive columns of one row: MFMA operand
+ *                     whose k runs along the features)
+ *   - transposed reads (ds_read_b64_tr_b16: MFMA operand whose k runs along the rows,
+ *                     i.e. the samples -- weight-gradient products)
+ * MFMA: v_mfma_f32_16x16x32_bf16; operand lane maps (cdna guide section 3):
+ *   A[row = l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col = l&15],
+ *   D[row = 4(l>>4)+r][col = l&15].
+ */
+#ifndef HPNN_MFMA_COMMON_H
+#define HPNN_MFMA_COMMON_H
+#include <hip/hip_runtime.h>
+
+namespace hpnn {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+/* f(x) = 2/(1+e^-x) - 1 with the hardware exp / reciprocal (bf16 outputs) */
+__device__ __forceinline__ float bipolar(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-x)) - 1.0f; }
+__device__ __forceinline__ float dbipolar(float y) { return -0.5f * (y * y - 1.0f); }
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+/* byte offset of element (r, col) in a T32 image with R rows */
+__device__ __forceinline__ int t32_g(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+template <int R>
+__device__ __forceinline__ int t32(int r, int col) {
+    const int sub = col >> 5, c = col & 31;
+    return sub * (R * 64) + r * 64 + ((((c >> 3) ^ t32_g(r)) & 3) << 4) + (c & 7) * 2;
+}
+
+/* row-read fragment: 8 consecutive columns [col0 + 8(l>>4), +8) of row r0 + (l&15) */
+template <int R>
+__device__ __forceinline__ bf16x8 frag_row(const char *img, int r0, int col0, int lane) {
+    return *(const bf16x8 *)(img + t32<R>(r0 + (lane & 15), col0 + 8 * (lane >> 4)));
+}
+
+/* transposed fragment: column c0 + (l&15), rows kbase + 8(l>>4) + 0..7 */
+template <int R>
+__device__ __forceinline__ bf16x8 frag_tr(const char *img, int kbase, int c0, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int row = kbase + 8 * g + q;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R>(row, c0 + 4 * p)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R>(row + 4, c0 + 4 * p)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+/* LDS-DMA: one 1 KiB piece = 16 rows x 32 cols of sub-tile `sub` of a T32 image with
+ * R rows, from a row-major global matrix (ld_bytes per row); lane i fills bytes
+ * [16i, 16i+16) of the piece, fetching the logical columns the half-swap puts there */
+template <int R>
+__device__ __forceinline__ void glds_t32_piece(const char *gbase, size_t ld_bytes, char *img, int piece, int lane) {
+    constexpr int PPS = R / 16;
+    const int sub = piece / PPS, rp = (piece % PPS) * 16;
+    const int r = rp + (lane >> 2), cp = lane & 3;
+    const int col = sub * 32 + ((cp ^ t32_g(r)) & 3) * 8;
+    const char *src = gbase + (size_t)r * ld_bytes + (size_t)col * 2;
+    __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(img + sub * (R * 64) + rp * 64), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+/* workgroup barrier that orders LDS traffic but does NOT wait for outstanding
+ * vector-memory ops (an in-flight LDS-DMA prefetch survives it; __syncthreads()
+ * would emit vmcnt(0) and drain it) */
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace hpnn
+#endif

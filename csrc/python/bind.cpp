@@ -75,6 +75,18 @@ PYBIND11_MODULE(_native, m) {
     m.def("fill_f32", [](uptr p, long n, float v, uptr stream) {
         check(hpnn_fill_f32((float *)P(p), n, v, S(stream)), "fill_f32");
     });
+    m.def("mlp3_mid", [](uptr H1, uptr W1, uptr W1t, uptr W2, uptr W2t, uptr labels, uptr T, int ldt, float t_hi,
+                         float t_lo, uptr D1, uptr gslab, uptr loss, uptr correct, int Bp, int n_valid, int n_out,
+                         int type, int h1, int h2, int no, int grid, uptr stream) {
+        check(hpnn_mlp3_mid(P(H1), P(W1), P(W1t), P(W2), P(W2t), (const int *)P(labels), (const float *)P(T), ldt,
+                            t_hi, t_lo, P(D1), (float *)P(gslab), (float *)P(loss), (unsigned int *)P(correct), Bp,
+                            n_valid, n_out, type, h1, h2, no, grid, S(stream)),
+              "mlp3_mid");
+    });
+    m.def("reduce_slabs_wide", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
+        check(hpnn_reduce_slabs_wide((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)),
+              "reduce_slabs_wide");
+    });
     m.def("device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

@@ -58,7 +58,7 @@ class MLP:
     """
 
     def __init__(self, sizes, net_type="SNN", batch=256, device="cuda", momentum=False, weights=None, seed=10958,
-                 init="reference", splits=None):
+                 init="reference", splits=None, fused=None, mid_grid=128):
         self.sizes = list(sizes)
         self.L = len(sizes) - 1
         self.type = TYPES[net_type] if isinstance(net_type, str) else int(net_type)
@@ -96,6 +96,15 @@ class MLP:
         self.D = [torch.empty(self.Bp, self.Np[l], dtype=torch.bfloat16, device=dev) for l in range(self.L)]
         self.Z = torch.empty(self.Bp, self.Np[-1], dtype=torch.float32, device=dev)
         self.stats = torch.zeros(2, dtype=torch.float32, device=dev)  # [loss sum, correct (uint32 bits)]
+        # fused 3-layer path (csrc/gpu/kernels_mlp3.hip) for n_in-128-64-(<=32) nets
+        eligible = self.L == 3 and tuple(self.Np) == ops.MLP3_DIMS
+        self.fused = eligible if fused is None else (bool(fused) and eligible)
+        if fused and not eligible:
+            raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
+        if self.fused:
+            grid = max(1, min(mid_grid, self.Bp // 128))
+            self.midslab = torch.empty(grid, self.Np[1] * self.Kp[1] + self.Np[2] * self.Kp[2], dtype=torch.float32,
+                                       device=dev)
         self.refresh_bf16()
 
     # ------------------------------------------------------------------ helpers
@@ -154,12 +163,52 @@ class MLP:
         G = self.G[l] if from_G else self.slab[l]
         ops.sgd_update(self.W32[l], self.V32[l], G, self.Wb[l], self.Wt[l], lr, alpha, scale, self.momentum)
 
+    def _t_hilo(self):
+        return (1.0, 0.0) if self.type == ops.TYPE_SNN else (1.0, -1.0)
+
+    def backward_grads(self, X, labels=None, T=None, n_valid=None, reduce=False, on_ready=None):
+        """forward + backward of one minibatch.  Weight gradients end in self.slab[l]
+        (split-K slabs) or, with reduce=True, summed in self.G[l] (the all-reduce
+        buckets).  on_ready(l) is called as soon as layer l's gradient is final (layers
+        become ready from the last to the first)."""
+        n_valid = self.Bp if n_valid is None else n_valid
+        if self.fused:
+            t_hi, t_lo = self._t_hilo()
+            ops.gemm_nt(X, self.Wb[0], ops.EPI_ACT, out=self.H[0])
+            ops.mlp3_mid(self.H[0], self.Wb[1], self.Wt[1], self.Wb[2], self.Wt[2], self.D[0], self.midslab,
+                         self.n_out, self.type, labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid,
+                         loss_acc=self.stats[0:1], correct=self.stats[1:2])
+            # G1 | G2 are contiguous in grad_flat, exactly the per-block slab layout
+            g12 = self.grad_flat[self.G[1].data_ptr() // 4 - self.grad_flat.data_ptr() // 4:]
+            ops.reduce_slabs_wide(self.midslab, g12[:self.midslab.shape[1]])
+            if on_ready:
+                on_ready(2)
+                on_ready(1)
+            self.grad_layer(0, X, reduce=reduce)
+            if on_ready:
+                on_ready(0)
+            return
+        self.forward(X)
+        self.output(labels=labels, T=T, n_valid=n_valid)
+        for l in range(self.L - 1, -1, -1):
+            if l > 0:
+                self.backward_layer(l)
+            self.grad_layer(l, X, reduce=reduce)
+            if on_ready:
+                on_ready(l)
+
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         """One minibatch fwd + bwd + update on the current stream (no host sync)."""
         n_valid = self.Bp if n_valid is None else n_valid
+        scale = 1.0 / n_valid
+        if self.fused:
+            self.backward_grads(X, labels=labels, T=T, n_valid=n_valid)
+            self.update_layer(0, lr, alpha, scale)
+            self.update_layer(1, lr, alpha, scale, from_G=True)
+            self.update_layer(2, lr, alpha, scale, from_G=True)
+            return
         self.forward(X)
         self.output(labels=labels, T=T, n_valid=n_valid)
-        scale = 1.0 / n_valid
         for l in range(self.L - 1, -1, -1):
             if l > 0:
                 self.backward_layer(l)

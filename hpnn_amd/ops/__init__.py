@@ -90,6 +90,38 @@ def reduce_slabs(slab, out):
     return out
 
 
+def reduce_slabs_wide(slab, out):
+    """out = slab.sum(0) with the many-loads-in-flight reduction (small layers, many slabs)."""
+    S = slab.shape[0]
+    n = slab[0].numel()
+    if _cpu(slab):
+        out.view(-1).copy_(slab.reshape(S, -1).sum(0))
+        return out
+    native().reduce_slabs_wide(slab.data_ptr(), S, slab.stride(0), n, out.data_ptr(), _stream())
+    return out
+
+
+MLP3_DIMS = (128, 64, 32)
+
+
+def mlp3_mid(H1, W1, W1t, W2, W2t, D1, gslab, n_out, net_type, labels=None, T=None, t_hi=1.0, t_lo=0.0,
+             n_valid=None, loss_acc=None, correct=None):
+    """Fused middle of the n_in-128-64-(<=32) MLP step (csrc/gpu/kernels_mlp3.hip):
+    H1 -> H2 -> output/loss -> delta3 -> delta2 -> delta1 (into D1), per-block
+    [G1 | G2] FP32 slabs into gslab [grid, 64*128 + 32*64]."""
+    Bp = H1.shape[0]
+    grid = gslab.shape[0]
+    n_valid = Bp if n_valid is None else int(n_valid)
+    if _cpu(H1):
+        return _cpu_mlp3_mid(H1, W1, W1t, W2, W2t, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid,
+                             loss_acc, correct)
+    native().mlp3_mid(H1.data_ptr(), W1.data_ptr(), W1t.data_ptr(), W2.data_ptr(), W2t.data_ptr(), _ptr(labels),
+                      _ptr(T), T.stride(0) if T is not None else 0, float(t_hi), float(t_lo), D1.data_ptr(),
+                      gslab.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid, n_out, net_type, *MLP3_DIMS,
+                      grid, _stream())
+    return D1
+
+
 def sgd_update(W32, V32, G, Wbf, Wt, lr, alpha=0.0, scale=1.0, momentum=False):
     """W32[N,K] FP32 master; G: [S,N,K] or [N,K] FP32 gradient sum(s)."""
     N, K = W32.shape
@@ -190,3 +222,21 @@ def _cpu_output_delta(Z, n_out, net_type, D, labels, T, t_hi, t_lo, n_valid, O, 
         hits = (o[:n_valid].argmax(1) == T[:n_valid, :n_out].argmax(1)).sum().to(torch.int32)
         correct.view(torch.int32).add_(hits)
     return D
+
+
+def _cpu_mlp3_mid(H1, W1, W1t, W2, W2t, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid, loss_acc,
+                  correct):
+    """PyTorch emulation with the kernel's rounding points (bf16 H2 / deltas)."""
+    Bp = H1.shape[0]
+    H2 = bipolar(H1.float() @ W1.float().t()).bfloat16()
+    Z = (H2.float() @ W2.float().t())
+    D3 = torch.zeros(Bp, W2.shape[0], dtype=torch.bfloat16)
+    _cpu_output_delta(Z, n_out, net_type, D3, labels, T, t_hi, t_lo, n_valid, None, loss_acc, correct)
+    D2 = ((D3.float() @ W2.float()) * dbipolar(H2.float())).bfloat16()
+    D1.copy_(((D2.float() @ W1.float()) * dbipolar(H1.float())).bfloat16())
+    G1 = D2.float().t() @ H1.float()
+    G2 = D3.float().t() @ H2.float()
+    gslab.zero_()
+    gslab[0, :G1.numel()] = G1.reshape(-1)
+    gslab[0, G1.numel():] = G2.reshape(-1)
+    return D1

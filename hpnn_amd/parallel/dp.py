@@ -61,18 +61,16 @@ class DataParallel:
         n_valid = m.Bp if n_valid is None else n_valid
         if self.world == 1:
             return m.train_step(X, labels=labels, T=T, n_valid=n_valid, lr=lr, alpha=alpha)
-        m.forward(X)
-        m.output(labels=labels, T=T, n_valid=n_valid)
         works = []
         done = set()
-        for l in range(m.L - 1, -1, -1):
-            if l > 0:
-                m.backward_layer(l)
-            m.grad_layer(l, X, reduce=True)
+
+        def ready(l):
             done.add(l)
             for b in self.buckets:
                 if b[-1] == l and all(x in done for x in b):
                     works.append(dist.all_reduce(self._bucket_view(b), group=self.group, async_op=True))
+
+        m.backward_grads(X, labels=labels, T=T, n_valid=n_valid, reduce=True, on_ready=ready)
         scale = 1.0 / (n_valid * self.world)
         for w in works:
             w.wait()

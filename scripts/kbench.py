@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of the MNIST SNN training step (one process, interleaved reps).
+
+usage: python scripts/kbench.py [--batch 65536] [--reps 50] [--mid-grid 128,256]
+Prints one line per phase: median microseconds over reps (HIP events)."""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hpnn_amd import ops  # noqa: E402
+from hpnn_amd.models import MLP  # noqa: E402
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--mid-grid", default="128,256")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    for mg in [int(x) for x in args.mid_grid.split(",")]:
+        m = MLP([784, 128, 64, 10], "SNN", batch=args.batch, momentum=True, mid_grid=mg)
+        X = m.prepare_input(torch.rand(m.Bp, 784, device=dev))
+        lab = torch.randint(0, 10, (m.Bp,), device=dev, dtype=torch.int32)
+        bytes_x = X.numel() * 2
+        red_out = torch.empty(m.midslab.shape[1], device=dev)
+        phases = {
+            "fwd_l0 (gemm_nt X.W0^T)": lambda: ops.gemm_nt(X, m.Wb[0], ops.EPI_ACT, out=m.H[0]),
+            "mlp3_mid": lambda: ops.mlp3_mid(m.H[0], m.Wb[1], m.Wt[1], m.Wb[2], m.Wt[2], m.D[0], m.midslab, 10,
+                                             ops.TYPE_SNN, labels=lab, loss_acc=m.stats[0:1],
+                                             correct=m.stats[1:2]),
+            "grad_l0 (gemm_tn D1^T.X)": lambda: ops.gemm_tn(m.D[0], X, splits=m.S[0], out=m.slab[0]),
+            "reduce_mid_slabs": lambda: ops.reduce_slabs_wide(m.midslab, red_out),
+            "update_l0": lambda: m.update_layer(0, 0.01, 0.2, 1.0 / m.Bp),
+            "update_l1": lambda: m.update_layer(1, 0.01, 0.2, 1.0 / m.Bp, from_G=True),
+            "update_l2": lambda: m.update_layer(2, 0.01, 0.2, 1.0 / m.Bp, from_G=True),
+            "full train_step": lambda: m.train_step(X, labels=lab),
+        }
+        for f in phases.values():
+            f()
+        torch.cuda.synchronize()
+        print(f"--- batch {m.Bp} mid_grid {m.midslab.shape[0]} splits {m.S}")
+        for name, f in phases.items():
+            med, mn = timeit(f, args.reps)
+            extra = ""
+            if name.startswith("fwd_l0") or name.startswith("grad_l0"):
+                extra = f"  X stream {bytes_x / med / 1e6:.2f} TB/s"
+            print(f"{name:32s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
+
+
+if __name__ == "__main__":
+    main()

@@ -53,3 +53,28 @@ def test_predict_matches_forward(gpu):
     R = ref.forward([w.float().bfloat16().double() for w in m.host_weights()], X.float().bfloat16().double(), "SNN")[-1]
     assert (O - R).abs().max().item() < 2e-2
     assert torch.allclose(O.sum(1), torch.ones(100, dtype=torch.float64), atol=1e-4)
+
+
+@pytest.mark.parametrize("net_type", ["SNN", "ANN", "LNN"])
+@pytest.mark.parametrize("B,n_valid", [(1024, 1024), (640, 600)])
+def test_fused_matches_layerwise(gpu, net_type, B, n_valid):
+    """fused mlp3 path == per-layer path (same math, different summation order)."""
+    torch.manual_seed(1)
+    sizes = [784, 128, 64, 10]
+    mf = MLP(sizes, net_type, batch=B, momentum=True, seed=5, fused=True, mid_grid=3)
+    ml = MLP(sizes, net_type, batch=B, momentum=True, seed=5, fused=False)
+    assert mf.fused and not ml.fused
+    X = torch.rand(mf.Bp, 784)
+    labels = torch.randint(0, 10, (mf.Bp,), dtype=torch.int32).cuda()
+    Xd = mf.prepare_input(X)
+    for _ in range(2):
+        mf.train_step(Xd, labels=labels, n_valid=n_valid, lr=0.05)
+        ml.train_step(Xd, labels=labels, n_valid=n_valid, lr=0.05)
+    torch.cuda.synchronize()
+    for a, b in zip(mf.host_weights(), ml.host_weights()):
+        assert (a - b).abs().max().item() < 2e-3 * (b.abs().max().item() + 1e-3)
+    la, ca = mf.read_stats()
+    lb, cb = ml.read_stats()
+    assert la == pytest.approx(lb, rel=2e-2)
+    assert abs(ca - cb) <= max(2, 0.01 * n_valid)
+    assert torch.equal(mf.D[0][n_valid:], torch.zeros_like(mf.D[0][n_valid:]))
