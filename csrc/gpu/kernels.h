@@ -20,6 +20,15 @@
 extern "C" {
 #endif
 
+/* Loss / accuracy statistics are accumulated into HPNN_STAT_SLOTS slots spaced
+ * HPNN_STAT_STRIDE floats apart (one 64-byte line each) -- block b adds into slot
+ * b % HPNN_STAT_SLOTS -- so thousands of workgroups never serialise on a single
+ * atomic address.  `loss_acc` / `correct` arguments point at slot 0; readers sum
+ * the slots. */
+#define HPNN_STAT_SLOTS 64
+#define HPNN_STAT_STRIDE 16
+#define HPNN_STAT_SLOT(b) ((size_t)((b) % HPNN_STAT_SLOTS) * HPNN_STAT_STRIDE)
+
 enum {
     HPNN_EPI_NONE = 0,   /* C = acc                                   */
     HPNN_EPI_ACT = 1,    /* C = 2/(1+e^-acc) - 1                      */
@@ -40,8 +49,8 @@ int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *sla
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)
- *   loss_acc[0] += sum of per-sample loss over valid rows
- *   correct[0]  += argmax hits
+ *   loss_acc[slot] += sum of per-sample loss over valid rows (slot array, above)
+ *   correct[slot]  += argmax hits
  *   optional O [B x ldo] FP32 network output (NULL to skip)
  * targets: dense T [B x ldt] FP32 (labels == NULL) or int32 labels with
  * one-hot values (t_hi at the label, t_lo elsewhere).
@@ -77,13 +86,18 @@ int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream);
 
 /* fused middle of a 3-layer MLP (kernels_mlp3.hip): H1 [Bp x 128] -> delta1
  * [Bp x 128] + per-block [G1 (64 x 128) | G2 (32 x 64)] FP32 slabs (grid of them),
- * loss / accuracy.  Dims must be h1=128, h2=64, no=32 (padded), n_out <= 32. */
+ * loss / accuracy.  Dims must be h1=128, h2=64, no=32 (padded), n_out <= 32,
+ * Bp % 64 == 0.  W1t / W2t are unused (transposed LDS reads of W1 / W2). */
 int hpnn_mlp3_mid(const void *H1g, const void *W1, const void *W1t, const void *W2, const void *W2t,
                   const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                   float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int h1, int h2,
                   int no, int grid, hipStream_t stream);
-/* slab reduction with 4 waves per 256 outputs (many loads in flight) */
-int hpnn_reduce_slabs_wide(const float *slab, int S, long stride, long n, float *out, hipStream_t stream);
+/* floats per block slab written by hpnn_mlp3_mid */
+int hpnn_mlp3_slab_floats(void);
+/* deterministic 2-pass slab reduction: groups of slabs into tmp (>= 16*n floats,
+ * NULL = single pass), then the groups into out */
+int hpnn_reduce_slabs2(const float *slab, int S, long stride, long n, float *tmp, float *out,
+                       hipStream_t stream);
 
 /* online (batch-1) FP64 persistent engine, see online.hip */
 typedef struct {

@@ -69,8 +69,8 @@ __device__ __forceinline__ void block_reduce_store(float my_loss, unsigned int m
     if (threadIdx.x == 0) {
         float s = sloss[0] + sloss[1] + sloss[2] + sloss[3];
         unsigned int h = shit[0] + shit[1] + shit[2] + shit[3];
-        if (loss_acc && s != 0.f) atomicAdd(loss_acc, s);
-        if (correct && h) atomicAdd(correct, h);
+        if (loss_acc && s != 0.f) atomicAdd(loss_acc + HPNN_STAT_SLOT(blockIdx.x), s);
+        if (correct && h) atomicAdd(correct + HPNN_STAT_SLOT(blockIdx.x), h);
     }
 }
 

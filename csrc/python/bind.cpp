@@ -83,10 +83,11 @@ PYBIND11_MODULE(_native, m) {
                             n_valid, n_out, type, h1, h2, no, grid, S(stream)),
               "mlp3_mid");
     });
-    m.def("reduce_slabs_wide", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
-        check(hpnn_reduce_slabs_wide((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)),
-              "reduce_slabs_wide");
+    m.def("reduce_slabs2", [](uptr slab, int Sn, long stride, long n, uptr tmp, uptr out, uptr stream) {
+        check(hpnn_reduce_slabs2((const float *)P(slab), Sn, stride, n, (float *)P(tmp), (float *)P(out), S(stream)),
+              "reduce_slabs2");
     });
+    m.def("mlp3_slab_floats", []() { return hpnn_mlp3_slab_floats(); });
     m.def("device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

@@ -58,7 +58,7 @@ class MLP:
     """
 
     def __init__(self, sizes, net_type="SNN", batch=256, device="cuda", momentum=False, weights=None, seed=10958,
-                 init="reference", splits=None, fused=None, mid_grid=128):
+                 init="reference", splits=None, fused=None, mid_grid=512):
         self.sizes = list(sizes)
         self.L = len(sizes) - 1
         self.type = TYPES[net_type] if isinstance(net_type, str) else int(net_type)
@@ -95,16 +95,19 @@ class MLP:
         self.H = [torch.empty(self.Bp, self.Np[l], dtype=torch.bfloat16, device=dev) for l in range(self.L - 1)]
         self.D = [torch.empty(self.Bp, self.Np[l], dtype=torch.bfloat16, device=dev) for l in range(self.L)]
         self.Z = torch.empty(self.Bp, self.Np[-1], dtype=torch.float32, device=dev)
-        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)  # [loss sum, correct (uint32 bits)]
+        # loss / accuracy: 64 slots x 16 floats ([0] loss sum, [1] hits as uint32 bits),
+        # see HPNN_STAT_SLOTS in csrc/gpu/kernels.h
+        self.stats = torch.zeros(64, 16, dtype=torch.float32, device=dev)
         # fused 3-layer path (csrc/gpu/kernels_mlp3.hip) for n_in-128-64-(<=32) nets
         eligible = self.L == 3 and tuple(self.Np) == ops.MLP3_DIMS
         self.fused = eligible if fused is None else (bool(fused) and eligible)
         if fused and not eligible:
             raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
         if self.fused:
-            grid = max(1, min(mid_grid, self.Bp // 128))
+            grid = max(1, min(mid_grid, self.Bp // 64))
             self.midslab = torch.empty(grid, self.Np[1] * self.Kp[1] + self.Np[2] * self.Kp[2], dtype=torch.float32,
                                        device=dev)
+            self.midtmp = torch.empty(16 * self.midslab.shape[1], dtype=torch.float32, device=dev)
         self.refresh_bf16()
 
     # ------------------------------------------------------------------ helpers
@@ -147,7 +150,7 @@ class MLP:
     def output(self, labels=None, T=None, n_valid=None, O=None):
         t_hi, t_lo = (1.0, 0.0) if self.type == ops.TYPE_SNN else (1.0, -1.0)
         ops.output_delta(self.Z, self.n_out, self.type, self.D[-1], labels=labels, T=T, t_hi=t_hi, t_lo=t_lo,
-                         n_valid=n_valid, O=O, loss_acc=self.stats[0:1], correct=self.stats[1:2])
+                         n_valid=n_valid, O=O, loss_acc=self.stats[0, 0:1], correct=self.stats[0, 1:2])
 
     def backward_layer(self, l):
         """D[l-1] = (D[l] @ W_l) * f'(H[l-1]) (uses pre-update W_l^T)."""
@@ -177,10 +180,10 @@ class MLP:
             ops.gemm_nt(X, self.Wb[0], ops.EPI_ACT, out=self.H[0])
             ops.mlp3_mid(self.H[0], self.Wb[1], self.Wt[1], self.Wb[2], self.Wt[2], self.D[0], self.midslab,
                          self.n_out, self.type, labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid,
-                         loss_acc=self.stats[0:1], correct=self.stats[1:2])
+                         loss_acc=self.stats[0, 0:1], correct=self.stats[0, 1:2])
             # G1 | G2 are contiguous in grad_flat, exactly the per-block slab layout
             g12 = self.grad_flat[self.G[1].data_ptr() // 4 - self.grad_flat.data_ptr() // 4:]
-            ops.reduce_slabs_wide(self.midslab, g12[:self.midslab.shape[1]])
+            ops.reduce_slabs2(self.midslab, g12[:self.midslab.shape[1]], self.midtmp)
             if on_ready:
                 on_ready(2)
                 on_ready(1)
@@ -229,4 +232,4 @@ class MLP:
 
     def read_stats(self):
         s = self.stats.cpu()
-        return float(s[0]), int(s[1:2].view(torch.int32)[0])
+        return float(s[:, 0].double().sum()), int(s[:, 1].contiguous().view(torch.int32).long().sum())

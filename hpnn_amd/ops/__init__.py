@@ -90,14 +90,15 @@ def reduce_slabs(slab, out):
     return out
 
 
-def reduce_slabs_wide(slab, out):
-    """out = slab.sum(0) with the many-loads-in-flight reduction (small layers, many slabs)."""
+def reduce_slabs2(slab, out, tmp=None):
+    """out = slab.sum(0), deterministic two-pass reduction (tmp: >= 16 * slab[0].numel()
+    floats of scratch; None = single pass)."""
     S = slab.shape[0]
     n = slab[0].numel()
     if _cpu(slab):
         out.view(-1).copy_(slab.reshape(S, -1).sum(0))
         return out
-    native().reduce_slabs_wide(slab.data_ptr(), S, slab.stride(0), n, out.data_ptr(), _stream())
+    native().reduce_slabs2(slab.data_ptr(), S, slab.stride(0), n, _ptr(tmp), out.data_ptr(), _stream())
     return out
 
 
@@ -221,6 +222,7 @@ def _cpu_output_delta(Z, n_out, net_type, D, labels, T, t_hi, t_lo, n_valid, O, 
     if correct is not None:
         hits = (o[:n_valid].argmax(1) == T[:n_valid, :n_out].argmax(1)).sum().to(torch.int32)
         correct.view(torch.int32).add_(hits)
+    # (GPU kernels spread these over 64 slots of 16 floats; slot 0 is used here)
     return D
 
 

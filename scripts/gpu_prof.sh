@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python scripts/kbench.py --reps 30 ${KB_ARGS:---mid-grid 128,256} > gpurun_out/kbench.log 2>&1
+timeout -k 10 300 python scripts/kbench.py --reps 10 ${KB_ARGS:---mid-grid 128,256} > gpurun_out/kbench.log 2>&1
 rc=$?; echo "kbench rc=$rc"; grep -v amdgpu.ids gpurun_out/kbench.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ -n "$PMC" ]; then

@@ -15,23 +15,26 @@ from hpnn_amd import ops  # noqa: E402
 from hpnn_amd.models import MLP  # noqa: E402
 
 
-def timeit(fn, reps):
+def timeit(fn, reps, inner=20):
+    """per-launch time of `inner` back-to-back launches between two events (removes
+    the ~8 us event/launch overhead a single-launch measurement carries)."""
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        for _ in range(inner):
+            fn()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b) * 1e3)
+        ts.append(a.elapsed_time(b) * 1e3 / inner)
     return statistics.median(ts), min(ts)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--mid-grid", default="128,256")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--mid-grid", default="256,512")
     args = ap.parse_args()
     dev = torch.device("cuda")
     for mg in [int(x) for x in args.mid_grid.split(",")]:
@@ -43,10 +46,10 @@ def main():
         phases = {
             "fwd_l0 (gemm_nt X.W0^T)": lambda: ops.gemm_nt(X, m.Wb[0], ops.EPI_ACT, out=m.H[0]),
             "mlp3_mid": lambda: ops.mlp3_mid(m.H[0], m.Wb[1], m.Wt[1], m.Wb[2], m.Wt[2], m.D[0], m.midslab, 10,
-                                             ops.TYPE_SNN, labels=lab, loss_acc=m.stats[0:1],
-                                             correct=m.stats[1:2]),
+                                             ops.TYPE_SNN, labels=lab, loss_acc=m.stats[0, 0:1],
+                                             correct=m.stats[0, 1:2]),
             "grad_l0 (gemm_tn D1^T.X)": lambda: ops.gemm_tn(m.D[0], X, splits=m.S[0], out=m.slab[0]),
-            "reduce_mid_slabs": lambda: ops.reduce_slabs_wide(m.midslab, red_out),
+            "reduce_mid_slabs": lambda: ops.reduce_slabs2(m.midslab, red_out, m.midtmp),
             "update_l0": lambda: m.update_layer(0, 0.01, 0.2, 1.0 / m.Bp),
             "update_l1": lambda: m.update_layer(1, 0.01, 0.2, 1.0 / m.Bp, from_G=True),
             "update_l2": lambda: m.update_layer(2, 0.01, 0.2, 1.0 / m.Bp, from_G=True),

@@ -85,10 +85,11 @@ def test_output_delta(gpu, net_type, n_out, ldz):
     T[torch.arange(B), labels.long()] = hi
     D = torch.empty(B, ldz, dtype=torch.bfloat16, device="cuda")
     O = torch.empty(B, ldz, device="cuda")
-    loss = torch.zeros(1, device="cuda")
-    corr = torch.zeros(1, dtype=torch.int32, device="cuda")
-    ops.output_delta(Z, n_out, net_type, D, labels=labels, t_hi=hi, t_lo=lo, n_valid=n_valid, O=O, loss_acc=loss,
-                     correct=corr)
+    stats = torch.zeros(64, 16, device="cuda")  # HPNN_STAT_SLOTS x HPNN_STAT_STRIDE
+    ops.output_delta(Z, n_out, net_type, D, labels=labels, t_hi=hi, t_lo=lo, n_valid=n_valid, O=O,
+                     loss_acc=stats[0, 0:1], correct=stats[0, 1:2])
+    loss = stats[:, 0].sum()
+    corr = stats[:, 1].contiguous().view(torch.int32).sum()
     o, d, l = ops.ref_output(Z, n_out, net_type, T)
     assert (O[:, :n_out] - o).abs().max().item() < 1e-5
     assert (D[:n_valid, :n_out].float() - d[:n_valid]).abs().max().item() < 1e-2 * max(1, d.abs().max().item())
