@@ -272,7 +272,13 @@ struct Batched {
     float *W32[16] = {0}, *V32[16] = {0}, *slab[16] = {0};
     void *Wb[16] = {0}, *Wt[16] = {0}, *H[16] = {0}, *D[16] = {0};
     float *Z = nullptr;
-    float *acc = nullptr; /* [0] loss sum, [1] correct (uint) */
+    /* loss / accuracy slots: HPNN_STAT_SLOTS x HPNN_STAT_STRIDE floats ([0] loss, [1] hits) */
+    float *acc = nullptr;
+    static constexpr size_t ACC_BYTES = HPNN_STAT_SLOTS * HPNN_STAT_STRIDE * 4;
+    /* fused n_in-128-64-(<=32) path (kernels_mlp3.hip) */
+    bool fused = false;
+    int mid_grid = 0;
+    float *midslab = nullptr, *midtmp = nullptr, *G12 = nullptr;
     hipStream_t s = nullptr;
 
     ~Batched() {
@@ -287,6 +293,27 @@ struct Batched {
         }
         hipFree(Z);
         hipFree(acc);
+        hipFree(midslab);
+        hipFree(midtmp);
+        hipFree(G12);
+    }
+
+    /* sum the stat slots: returns (loss sum, hits) */
+    BOOL read_stats(double *loss, unsigned int *hits) {
+        std::vector<float> h(HPNN_STAT_SLOTS * HPNN_STAT_STRIDE);
+        HIPCHK(hipMemcpyAsync(h.data(), acc, ACC_BYTES, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double l = 0.0;
+        unsigned int c = 0;
+        for (int i = 0; i < HPNN_STAT_SLOTS; i++) {
+            l += h[(size_t)i * HPNN_STAT_STRIDE];
+            unsigned int u;
+            memcpy(&u, &h[(size_t)i * HPNN_STAT_STRIDE + 1], 4);
+            c += u;
+        }
+        *loss = l;
+        *hits = c;
+        return TRUE;
     }
 
     BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st) {
@@ -322,8 +349,16 @@ struct Batched {
             if (hpnn_cast_weights(W32[l], Wb[l], Wt[l], Np[l], Kp[l], s)) return FALSE;
         }
         HIPCHK(hipMalloc(&Z, (size_t)Bp * Np[L - 1] * 4));
-        HIPCHK(hipMalloc(&acc, 16));
-        HIPCHK(hipMemsetAsync(acc, 0, 16, s));
+        HIPCHK(hipMalloc(&acc, ACC_BYTES));
+        HIPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
+        fused = (L == 3 && Np[0] == 128 && Np[1] == 64 && Np[2] == 32);
+        if (fused) {
+            const int slab_f = hpnn_mlp3_slab_floats();
+            mid_grid = Bp / 64 < 512 ? Bp / 64 : 512;
+            HIPCHK(hipMalloc(&midslab, (size_t)mid_grid * slab_f * 4));
+            HIPCHK(hipMalloc(&midtmp, (size_t)16 * slab_f * 4));
+            HIPCHK(hipMalloc(&G12, (size_t)slab_f * 4));
+        }
         return TRUE;
     }
 
@@ -341,7 +376,30 @@ struct Batched {
         return TRUE;
     }
 
+    BOOL step_fused(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
+        const float scale = 1.0f / (float)n_valid;
+        const float t_lo = type == 2 ? 0.f : -1.f;
+        (void)t_lo;
+        int r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0], HPNN_EPI_ACT, 0, s);
+        if (!r)
+            r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, 0.f, D[0], midslab, acc,
+                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid, s);
+        if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
+        if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, hpnn_mlp3_slab_floats(), hpnn_mlp3_slab_floats(), midtmp, G12, s);
+        if (!r)
+            r = hpnn_sgd_update(W32[0], V32[0], slab[0], S[0], (long)Np[0] * Kp[0], Wb[0], Wt[0], Np[0], Kp[0], lr,
+                                alpha, scale, mom ? 1 : 0, s);
+        if (!r)
+            r = hpnn_sgd_update(W32[1], V32[1], G12, 1, 0, Wb[1], Wt[1], Np[1], Kp[1], lr, alpha, scale, mom ? 1 : 0, s);
+        if (!r)
+            r = hpnn_sgd_update(W32[2], V32[2], G12 + (size_t)Np[1] * Kp[1], 1, 0, Wb[2], Wt[2], Np[2], Kp[2], lr,
+                                alpha, scale, mom ? 1 : 0, s);
+        if (r) NN_ERROR(stderr, "fused step failed: %d\n", r);
+        return r == 0;
+    }
+
     BOOL step(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
+        if (fused) return step_fused(X, T, ldt, n_valid, lr, alpha, mom);
         if (!forward(X)) return FALSE;
         if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
                               (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
@@ -421,9 +479,10 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice));
     }
     auto t0 = std::chrono::steady_clock::now();
-    float h_acc[2] = {0, 0};
+    double ep_loss = 0.0;
+    unsigned int ep_hits = 0;
     for (UINT e = 0; e < o->epochs; e++) {
-        HIPCHK(hipMemsetAsync(net.acc, 0, 16, s));
+        HIPCHK(hipMemsetAsync(net.acc, 0, Batched::ACC_BYTES, s));
         for (int b = 0; b < n_batches; b++) {
             const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
             const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * 2;
@@ -434,18 +493,15 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
                 return FALSE;
             }
         }
-        HIPCHK(hipMemcpyAsync(h_acc, net.acc, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if (!net.read_stats(&ep_loss, &ep_hits)) return FALSE;
     }
     auto t1 = std::chrono::steady_clock::now();
     net.download(k);
     if (st) {
         st->seconds = std::chrono::duration<double>(t1 - t0).count();
         st->samples = (UINT64)n * o->epochs;
-        st->epoch_loss = h_acc[0] / (double)n;
-        unsigned int c;
-        memcpy(&c, &h_acc[1], 4);
-        st->correct = c;
+        st->epoch_loss = ep_loss / (double)n;
+        st->correct = ep_hits;
         st->last_loss = st->epoch_loss;
     }
     hipFree(Xd);

@@ -1,0 +1,166 @@
+"""Native C API / CLIs on the CPU engine (FP64 oracle), against the PyTorch reference.
+
+No GPU: HPNN_FORCE_CPU=1 keeps the C runtime on the CPU engine even on a GPU box."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from hpnn_amd.models import reference as ref
+from hpnn_amd.models.mlp import reference_init
+from hpnn_amd.utils import formats
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def _env():
+    e = dict(os.environ)
+    e["HPNN_FORCE_CPU"] = "1"
+    return e
+
+
+def _make_dataset(d, n, n_in, n_out, snn, seed=1):
+    rng = np.random.default_rng(seed)
+    os.makedirs(d, exist_ok=True)
+    X, T = [], []
+    for i in range(n):
+        x = rng.uniform(-1, 1, n_in)
+        c = int(np.argmax(x[:n_out])) if n_in >= n_out else int(rng.integers(n_out))
+        t = np.full(n_out, 0.0 if snn else -1.0)
+        t[c] = 1.0
+        formats.write_sample(os.path.join(d, f"s{i:04d}.txt"), x, t)
+        X.append(np.round(x, 5))
+        T.append(t)
+    return np.array(X), np.array(T)
+
+
+def _run(cmd, cwd):
+    r = subprocess.run(cmd, cwd=cwd, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("net,train", [("ANN", "BP"), ("ANN", "BPM"), ("SNN", "BP"), ("SNN", "BPM")])
+def test_train_nn_online_matches_reference(tmp_path, net, train):
+    """train_nn (online mode, 2 samples) == PyTorch FP64 loop with the same init and order."""
+    d = str(tmp_path)
+    X, T = _make_dataset(os.path.join(d, "samples"), 2, 4, 4, net == "SNN")
+    formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=10958, inputs=4, hiddens=[8],
+                       outputs=4, train=train, sample_dir="./samples", test_dir="./samples")
+    out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d)
+    assert out.count("TRAINING FILE") == 2
+    k0 = formats.read_kernel(os.path.join(d, "kernel.tmp"))
+    W0 = [w.clone() for w in reference_init([4, 8, 4], 10958)]
+    for a, b in zip(k0["weights"], W0):
+        assert np.abs(a - b.numpy()).max() < 1e-14  # bit-identical generation (modulo %17.15f)
+    # reference loop: same file order as the C seeded permutation -> replay from the log
+    order = [ln.split("TRAINING FILE:")[1].split()[0] for ln in out.splitlines() if "TRAINING FILE" in ln]
+    W = [torch.tensor(formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"][i]) for i in range(2)]
+    lr = {"ANN": {"BP": 0.001, "BPM": 0.0005}, "SNN": {"BP": 0.01, "BPM": 0.01}}[net][train]
+    mom = train == "BPM"
+    for f in order:
+        x, t = formats.read_sample(os.path.join(d, "samples", f))
+        x, t = torch.tensor(x), torch.tensor(t)
+        V = [torch.zeros_like(w) for w in W] if mom else None
+        mn, mx = (15, 102399) if mom else (31, 102399)
+        it = 0
+        while True:
+            it += 1
+            dEp, o = ref.online_step(W, x, t, net, lr, V, 0.2)
+            ok = int(torch.argmax(o)) == int(torch.nonzero(t == 1.0)[-1])
+            if it > mx:
+                break
+            ok = ok and it > mn
+            if dEp <= 1e-6 and ok:
+                break
+    k1 = formats.read_kernel(os.path.join(d, "kernel.opt"))
+    for a, b in zip(k1["weights"], W):
+        assert np.abs(a - b.numpy()).max() < 1e-9, np.abs(a - b.numpy()).max()
+
+
+@pytest.mark.parametrize("net,train", [("SNN", "BPM"), ("ANN", "BP"), ("LNN", "BPM")])
+def test_train_nn_batched_matches_reference(tmp_path, net, train):
+    d = str(tmp_path)
+    n = 12
+    _make_dataset(os.path.join(d, "samples"), n, 6, 3, net == "SNN")
+    formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=7, inputs=6, hiddens=[5, 4],
+                       outputs=3, train=train, sample_dir="./samples", test_dir="./samples", mode="batched",
+                       batch=4, epochs=3, lr=0.05)
+    _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d)
+    W = [torch.tensor(w) for w in formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"]]
+    # batched mode loads samples in the seeded permutation; reproduce it via the C order printed?
+    # the order is the same seeded permutation used by online mode: recover it from the sorted list
+    files = sorted(os.listdir(os.path.join(d, "samples")))
+    import ctypes, ctypes.util
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    libc.random.restype = ctypes.c_long
+    libc.srandom(7)
+    used, order = set(), []
+    while len(order) < n:
+        idx = int(float(libc.random()) * n / 2147483647.0)
+        if idx >= n or idx in used:
+            continue
+        used.add(idx)
+        order.append(idx)
+    data = [formats.read_sample(os.path.join(d, "samples", files[i])) for i in order]
+    X = torch.tensor(np.array([a for a, _ in data]))
+    T = torch.tensor(np.array([b for _, b in data]))
+    V = [torch.zeros_like(w) for w in W] if train == "BPM" else None
+    for _ in range(3):
+        for s in range(0, n, 4):
+            ref.batched_step(W, X[s:s + 4], T[s:s + 4], net, 0.05, V, 0.2)
+    k1 = formats.read_kernel(os.path.join(d, "kernel.opt"))
+    for a, b in zip(k1["weights"], W):
+        assert np.abs(a - b.numpy()).max() < 1e-12
+
+
+def test_run_nn_and_conf_errors(tmp_path):
+    d = str(tmp_path)
+    _make_dataset(os.path.join(d, "samples"), 6, 4, 4, False)
+    formats.write_conf(os.path.join(d, "nn.conf"), name="t", type="ANN", seed=3, inputs=4, hiddens=[8], outputs=4,
+                       train="BP", sample_dir="./samples", test_dir="./samples")
+    _run([os.path.join(BIN, "train_nn"), "nn.conf"], d)
+    formats.write_conf(os.path.join(d, "run.conf"), name="t", type="ANN", init="kernel.opt", seed=3,
+                       train="BP", sample_dir="./samples", test_dir="./samples")
+    out = _run([os.path.join(BIN, "run_nn"), "-vv", "run.conf"], d)
+    assert out.count("TESTING FILE") == 6
+    assert out.count("[PASS]") + out.count("[FAIL") == 6
+    # malformed conf -> non-zero exit, error message
+    with open(os.path.join(d, "bad.conf"), "w") as f:
+        f.write("[type] ANN\n[init] generate\n[input] 4\n[output] 4\n")
+    r = subprocess.run([os.path.join(BIN, "train_nn"), "bad.conf"], cwd=d, env=_env(), capture_output=True, text=True)
+    assert r.returncode != 0 and "hidden" in (r.stdout + r.stderr)
+
+
+def test_dry_run_writes_nothing(tmp_path):
+    d = str(tmp_path)
+    _make_dataset(os.path.join(d, "samples"), 2, 4, 4, False)
+    formats.write_conf(os.path.join(d, "nn.conf"), name="t", type="ANN", seed=3, inputs=4, hiddens=[8], outputs=4,
+                       train="BP", sample_dir="./samples", test_dir="./samples")
+    _run([os.path.join(BIN, "train_nn"), "-x", "nn.conf"], d)
+    assert not os.path.exists(os.path.join(d, "kernel.opt"))
+
+
+def test_capi_python_binding(tmp_path):
+    os.environ["HPNN_FORCE_CPU"] = "1"
+    from hpnn_amd import capi
+    capi.init(0)
+    d = str(tmp_path)
+    _make_dataset(os.path.join(d, "samples"), 4, 5, 3, True)
+    conf = os.path.join(d, "nn.conf")
+    formats.write_conf(conf, name="t", type="SNN", seed=3, inputs=5, hiddens=[6], outputs=3, train="BPM",
+                       sample_dir=os.path.join(d, "samples"), test_dir=os.path.join(d, "samples"))
+    net = capi.Network(conf)
+    assert net.dims == [5, 6, 3]
+    net.set(mode="batched", batch=2, epochs=5, lr=0.1)
+    assert net.train()
+    p, t = net.run()
+    assert t == 4 and 0 <= p <= 4
+    net.dump_kernel(os.path.join(d, "k.opt"), exact=True)
+    net.dump_conf(os.path.join(d, "dump.conf"))
+    c = formats.read_conf(os.path.join(d, "dump.conf"))
+    assert c["hidden"] == [6] and c["type"] == "SNN"
+    net.close()

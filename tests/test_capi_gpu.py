@@ -1,0 +1,77 @@
+"""Native engines on the GPU (train_nn / run_nn through libhpnn) vs the FP64 CPU engine."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from hpnn_amd.utils import formats
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def _run(cmd, cwd, cpu=False):
+    env = dict(os.environ)
+    if cpu:
+        env["HPNN_FORCE_CPU"] = "1"
+    else:
+        env.pop("HPNN_FORCE_CPU", None)
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _data(d, n, n_in, n_out, snn, seed=0):
+    rng = np.random.default_rng(seed)
+    os.makedirs(d, exist_ok=True)
+    for i in range(n):
+        x = rng.uniform(0, 1, n_in)
+        t = np.full(n_out, 0.0 if snn else -1.0)
+        t[int(rng.integers(n_out))] = 1.0
+        formats.write_sample(os.path.join(d, f"s{i:05d}.txt"), x, t)
+
+
+@pytest.mark.parametrize("net,train", [("SNN", "BP"), ("ANN", "BPM")])
+def test_online_gpu_matches_cpu(tmp_path, net, train):
+    """FP64 persistent online kernel == FP64 CPU engine (reference semantics)."""
+    for dev in ("cpu", "gpu"):
+        d = str(tmp_path / dev)
+        _data(os.path.join(d, "samples"), 3, 40, 5, net == "SNN")
+        formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=5, inputs=40, hiddens=[24, 16],
+                           outputs=5, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, cpu=(dev == "cpu"))
+        assert out.count("TRAINING FILE") == 3
+    kc = formats.read_kernel(str(tmp_path / "cpu" / "kernel.opt"))["weights"]
+    kg = formats.read_kernel(str(tmp_path / "gpu" / "kernel.opt"))["weights"]
+    for a, b in zip(kc, kg):
+        assert np.abs(a - b).max() < 1e-9, np.abs(a - b).max()
+
+
+def test_batched_gpu_fused_close_to_cpu(tmp_path):
+    """native batched engine on the GPU (fused MNIST-shaped path, BF16 MFMA) vs FP64 CPU."""
+    res = {}
+    for dev in ("cpu", "gpu"):
+        d = str(tmp_path / dev)
+        _data(os.path.join(d, "samples"), 300, 784, 10, True)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=784, hiddens=[128, 64],
+                           outputs=10, train="BPM", sample_dir="./samples", test_dir="./samples", mode="batched",
+                           batch=128, epochs=2, lr=0.05)
+        _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, cpu=(dev == "cpu"))
+        res[dev] = (formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"],
+                    formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"])
+    for (w0c, w1c, w1g) in zip(res["cpu"][0], res["cpu"][1], res["gpu"][1]):
+        dc, dg = w1c - w0c, w1g - w0c
+        rel = np.linalg.norm(dc - dg) / (np.linalg.norm(dc) + 1e-30)
+        assert rel < 0.08, rel
+
+
+def test_run_nn_gpu(tmp_path):
+    d = str(tmp_path)
+    _data(os.path.join(d, "samples"), 20, 50, 4, True)
+    formats.write_conf(os.path.join(d, "nn.conf"), name="t", type="SNN", seed=5, inputs=50, hiddens=[16], outputs=4,
+                       train="BP", sample_dir="./samples", test_dir="./samples")
+    out_g = _run([os.path.join(BIN, "run_nn"), "-vv", "nn.conf"], d)
+    out_c = _run([os.path.join(BIN, "run_nn"), "-vv", "nn.conf"], d, cpu=True)
+    assert out_g.count("[PASS]") == out_c.count("[PASS]")

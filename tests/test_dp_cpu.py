@@ -1,0 +1,75 @@
+"""Data parallel over torch.distributed (gloo, 2 CPU ranks) == one process on the whole
+batch.  Exercises the bucketing / all-reduce / update orchestration of
+hpnn_amd.parallel.DataParallel with the PyTorch emulation of the kernels (CPU tensors)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hpnn_amd.models import MLP
+from hpnn_amd.parallel import DataParallel
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, sizes, net, fused, B, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    Xall = torch.rand(B * world, sizes[0])
+    Lall = torch.randint(0, sizes[-1], (B * world,), dtype=torch.int32)
+    m = MLP(sizes, net, batch=B, device="cpu", momentum=True, seed=11, fused=fused)
+    dp = DataParallel(m, bucket_bytes=16 * 1024)
+    dp.broadcast_parameters()
+    X = m.prepare_input(Xall[rank * B:(rank + 1) * B])
+    L = Lall[rank * B:(rank + 1) * B]
+    for _ in range(steps):
+        dp.train_step(X, labels=L, lr=0.05, alpha=0.2)
+    if rank == 0:
+        q.put([w.clone() for w in m.host_weights()])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes,net,fused", [([32, 128, 64, 10], "SNN", True), ([32, 128, 64, 10], "SNN", False),
+                                             ([16, 24, 5], "ANN", False)])
+def test_dp_equals_single(sizes, net, fused):
+    world, B, steps = 2, 128, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, net, fused, B, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    Xall = torch.rand(B * world, sizes[0])
+    Lall = torch.randint(0, sizes[-1], (B * world,), dtype=torch.int32)
+    m = MLP(sizes, net, batch=B * world, device="cpu", momentum=True, seed=11, fused=fused)
+    X = m.prepare_input(Xall)
+    for _ in range(steps):
+        m.train_step(X, labels=Lall, lr=0.05, alpha=0.2)
+    for a, b in zip(got, m.host_weights()):
+        assert (a - b).abs().max().item() < 1e-5, (a - b).abs().max().item()
+
+
+def test_bucket_plan():
+    m = MLP([784, 128, 64, 10], "SNN", batch=128, device="cpu")
+    dp = DataParallel(m, bucket_bytes=64 * 1024)
+    flat = [l for b in dp.buckets for l in b]
+    assert sorted(flat) == [0, 1, 2] and dp.buckets[0][0] == 2
+    for b in dp.buckets:
+        v = dp._bucket_view(b)
+        assert v.numel() == sum(m.G[l].numel() for l in b)
