@@ -1,2 +1,3 @@
 """Parallelism: data parallel (RCCL all-reduce) and row-sharded tensor parallel."""
 from .dp import DataParallel, init_from_env  # noqa: F401
+from .tp import TensorParallelMLP  # noqa: F401
