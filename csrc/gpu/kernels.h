@@ -41,6 +41,10 @@ int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, i
                       const void *aux, int ldaux, int M, int N, int K, int epi, int c_f32,
                       hipStream_t stream);
 
+/* weight-stationary variant for N <= 128, K in {512, 800, 1024}: returns 1 if no instance */
+int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C, int ldc, int M, int N, int K,
+                         int epi, int c_f32, hipStream_t stream);
+
 /* slab[s][N x M] = sum_{b in slice s} D[b][n] H[b][m] (FP32 out).
  * D: [Bt x N] BF16, H: [Bt x M] BF16. Bt % (64*splits) == 0, N,M % 32 == 0.
  * ldg: row stride of a slab row (>= M); slab stride = N*ldg. */
@@ -72,6 +76,24 @@ int hpnn_sgd_update(float *W32, float *V32, const float *G, int S, long gstride,
                     int N, int K, float lr, float alpha, float scale, int momentum,
                     hipStream_t stream);
 
+/* all layers' optimizer steps in ONE launch (same math as hpnn_sgd_update per layer).
+ * Wf (optional, may be NULL): BF16 copy of W in MFMA-fragment-major order, the operand
+ * layout of the register-resident first-layer weights (hpnn_mlp3_fused):
+ *   element (n, k) at (((n/16)*(K/32) + k/32)*64 + n%16 + 16*((k/8)%4))*8 + k%8 */
+#define HPNN_UPD_MAX 8
+typedef struct {
+    float *W32;
+    float *V32;
+    const float *G;
+    long gstride;
+    void *Wbf;
+    void *Wt;
+    void *Wf;
+    int S, N, K;
+} hpnn_upd_layer;
+int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float lr, float alpha, float scale, int momentum,
+                          hipStream_t stream);
+
 /* dense FP64/FP32 host-layout matrix -> padded BF16 device matrix:
  * dst[r][c] = src[r][c] for r<rows,c<cols, 0 in the padding.
  * src_f64 selects double vs float input. */
@@ -92,12 +114,27 @@ int hpnn_mlp3_mid(const void *H1g, const void *W1, const void *W1t, const void *
                   const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                   float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int h1, int h2,
                   int no, int grid, hipStream_t stream);
+/* the whole 3-layer step up to delta1 in one persistent kernel (kernels_mlp3.hip):
+ *   X [Bp x K0] -> H1 = f(X W0^T) -> H2 -> output/loss -> delta3 -> delta2 -> delta1 (D1)
+ * plus per-block [G1 | G2] slabs (grid of them, same layout as hpnn_mlp3_mid).  W0 is
+ * read once per workgroup into registers from its fragment-major copy W0f (see
+ * hpnn_sgd_update_multi); K0 in {256, 512, 800, 832, 896}, Bp % 32 == 0.  grid <= 0:
+ * one workgroup per CU.  Returns the grid used (> 0) or an error (< 0). */
+int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,
+                    const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
+                    float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
+                    hipStream_t stream);
+/* grid hpnn_mlp3_fused will use for Bp samples (slab rows to allocate) */
+int hpnn_mlp3_fused_grid(int Bp, int grid);
 /* floats per block slab written by hpnn_mlp3_mid */
 int hpnn_mlp3_slab_floats(void);
 /* deterministic 2-pass slab reduction: groups of slabs into tmp (>= 16*n floats,
  * NULL = single pass), then the groups into out */
 int hpnn_reduce_slabs2(const float *slab, int S, long stride, long n, float *tmp, float *out,
                        hipStream_t stream);
+
+/* first pass of hpnn_reduce_slabs2 only: out[g*n + i], g < groups (groups <= S) */
+int hpnn_reduce_groups(const float *slab, int S, long stride, long n, int groups, float *out, hipStream_t stream);
 
 /* online (batch-1) FP64 persistent engine, see online.hip */
 typedef struct {

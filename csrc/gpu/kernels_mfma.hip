@@ -30,6 +30,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 #include "mfma_common.h"
@@ -89,7 +90,7 @@ __device__ __forceinline__ void glds_piece(const char *gbase, size_t ld_bytes, c
     const int cp = (lane * 16 % RB) >> 4;
     const int cl = (CPR == 8) ? (cp ^ ((r >> 1) & 7)) : (cp ^ ((r >> 1) & 3));
     const char *src = gbase + (size_t)r * ld_bytes + cl * 16;
-    __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)lds_piece, 16, 0, 0);
+    hpnn::glds16(src, lds_piece);
 }
 
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int EPI, bool CF32>
@@ -220,7 +221,7 @@ template <int TM, int TN, int BKR, int STAGES>
 __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
                                                            const __bf16 *__restrict__ H, int ldh,
                                                            float *__restrict__ slab, int ldg, int N, int chunk,
-                                                           int tiles_n) {
+                                                           int tiles_n, int tiles, int xcd_map) {
     constexpr int WTM = TM / 2, WTN = TN / 2;
     constexpr int FM = WTM / 16, FN = WTN / 16;
     constexpr int H_PIECES = (TM / 32) * (BKR / 16), D_PIECES = (TN / 32) * (BKR / 16);
@@ -232,9 +233,20 @@ __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restr
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+    /* XCD-aware order: workgroups are dealt round-robin to the 8 XCDs in dispatch order;
+     * put all output tiles of one batch slice on the same XCD, back to back, so the
+     * slice's D (shared by every tile of the slice) is fetched once into that XCD's L2 */
+    int tile, split;
+    if (xcd_map) {
+        const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+        tile = j % tiles;
+        split = xcd + 8 * (j / tiles);
+    } else {
+        tile = blockIdx.x % tiles;
+        split = blockIdx.x / tiles;
+    }
+    const int tn = tile % tiles_n, tm = tile / tiles_n;
     const int m0 = tm * TM, n0 = tn * TN;
-    const int split = blockIdx.y;
     const int b0 = split * chunk;
     const int KT = chunk / BKR;
     const size_t ldh_b = (size_t)ldh * 2, ldd_b = (size_t)ldd * 2;
@@ -336,8 +348,10 @@ int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int
     constexpr int STAGE = BKR * (TM + TN) * 2;
     constexpr int ST = (73728 / STAGE) < 2 ? 2 : ((73728 / STAGE) > 6 ? 6 : (73728 / STAGE));
     if (chunk % BKR) return -2;
-    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles_m * tiles_n, splits), dim3(256), 0, s,
-                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, chunk, tiles_n);
+    const int tiles = tiles_m * tiles_n;
+    const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits), dim3(256), 0, s,
+                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, chunk, tiles_n, tiles, xcd_map);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -354,6 +368,12 @@ int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int
 extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {
     if (M <= 0 || N <= 0 || K <= 0) return -1;
+    /* wide-input layer with a small weight matrix and a large batch: weight-stationary kernel */
+    static const int ws_off = [] { const char *e = getenv("HPNN_NO_WS"); return e && atoi(e) ? 1 : 0; }();
+    if (!ws_off && M % 32 == 0 && M >= 16384 && N <= 128) {
+        int rc = hpnn_gemm_nt_ws_bf16(A, lda, B, ldb, C, ldc, M, N, K, epi, c_f32, stream);
+        if (rc <= 0) return rc;
+    }
     if (M % 128 || N % 32 || K % 32) return -2;
     if (lda % 8 || ldb % 8 || ldc % 8 || ((epi == HPNN_EPI_DACT) && (ldaux % 4 || !aux))) return -3;
     if (c_f32) {

@@ -230,13 +230,13 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *__restri
 
 /* 32x32 tile per block, 256 threads: thread (ty = tid/8, tx = tid%8) owns
  * row ty, columns 4tx..4tx+3 of the tile. */
-__global__ __launch_bounds__(256) void sgd_update_kernel(float *__restrict__ W32, float *__restrict__ V32,
-                                                         const float *__restrict__ G, int S, long gstride,
-                                                         __bf16 *__restrict__ Wbf, __bf16 *__restrict__ Wt, int N,
-                                                         int K, float lr, float alpha, float scale, int momentum) {
-    __shared__ float tile[32][33];
+/* one 32x32 tile of the optimizer step (see hpnn_sgd_update); tile = (tn, tk) */
+__device__ __forceinline__ void sgd_tile(float *__restrict__ W32, float *__restrict__ V32, const float *__restrict__ G,
+                                         int S, long gstride, __bf16 *__restrict__ Wbf, __bf16 *__restrict__ Wt,
+                                         __bf16 *__restrict__ Wf, int N, int K, int tile, float lr, float alpha,
+                                         float scale, int momentum, float (*tilebuf)[33]) {
     const int tiles_k = K / 32;
-    const int tn = blockIdx.x / tiles_k, tk = blockIdx.x % tiles_k;
+    const int tn = tile / tiles_k, tk = tile % tiles_k;
     const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
     const int n = tn * 32 + ty, k = tk * 32 + tx * 4;
     const size_t idx = (size_t)n * K + k;
@@ -274,15 +274,45 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float *__restrict__ W32
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         wb[r] = (__bf16)w[r];
-        tile[ty][tx * 4 + r] = w[r];
+        tilebuf[ty][tx * 4 + r] = w[r];
     }
     *(bf16x4 *)(Wbf + idx) = wb;
+    if (Wf) {
+        /* MFMA-fragment-major copy (kernels.h): 4 consecutive k stay contiguous */
+        const size_t fo = (((size_t)(n >> 4) * tiles_k + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+        *(bf16x4 *)(Wf + fo) = wb;
+    }
     __syncthreads();
     /* transposed: thread writes Wt[k = tk*32 + ty][n = tn*32 + 4tx .. +3] */
     bf16x4 tb;
 #pragma unroll
-    for (int r = 0; r < 4; r++) tb[r] = (__bf16)tile[tx * 4 + r][ty];
+    for (int r = 0; r < 4; r++) tb[r] = (__bf16)tilebuf[tx * 4 + r][ty];
     *(bf16x4 *)(Wt + (size_t)(tk * 32 + ty) * N + tn * 32 + tx * 4) = tb;
+}
+
+__global__ __launch_bounds__(256) void sgd_update_kernel(float *__restrict__ W32, float *__restrict__ V32,
+                                                         const float *__restrict__ G, int S, long gstride,
+                                                         __bf16 *__restrict__ Wbf, __bf16 *__restrict__ Wt, int N,
+                                                         int K, float lr, float alpha, float scale, int momentum) {
+    __shared__ float tile[32][33];
+    sgd_tile(W32, V32, G, S, gstride, Wbf, Wt, nullptr, N, K, blockIdx.x, lr, alpha, scale, momentum, tile);
+}
+
+struct UpdArgs {
+    hpnn_upd_layer L[HPNN_UPD_MAX];
+    int tile0[HPNN_UPD_MAX + 1];
+    int n;
+    float lr, alpha, scale;
+    int momentum;
+};
+
+__global__ __launch_bounds__(256) void sgd_update_multi_kernel(UpdArgs a) {
+    __shared__ float tile[32][33];
+    int l = 0;
+    while (l + 1 < a.n && (int)blockIdx.x >= a.tile0[l + 1]) l++;
+    const hpnn_upd_layer &L = a.L[l];
+    sgd_tile(L.W32, L.V32, L.G, L.S, L.gstride, (__bf16 *)L.Wbf, (__bf16 *)L.Wt, (__bf16 *)L.Wf, L.N, L.K,
+             blockIdx.x - a.tile0[l], a.lr, a.alpha, a.scale, a.momentum, tile);
 }
 
 __global__ void pack_bf16_kernel(const void *__restrict__ src, int src_f64, int rows, int cols, int lds,
@@ -341,6 +371,29 @@ extern "C" int hpnn_sgd_update(float *W32, float *V32, const float *G, int S, lo
     if (momentum && !V32) return -1;
     hipLaunchKernelGGL(sgd_update_kernel, dim3((N / 32) * (K / 32)), dim3(256), 0, stream, W32, V32, G, S, gstride,
                        (__bf16 *)Wbf, (__bf16 *)Wt, N, K, lr, alpha, scale, momentum);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float lr, float alpha, float scale,
+                                     int momentum, hipStream_t stream) {
+    if (n < 1 || n > HPNN_UPD_MAX) return -1;
+    UpdArgs a;
+    a.n = n;
+    a.lr = lr;
+    a.alpha = alpha;
+    a.scale = scale;
+    a.momentum = momentum;
+    int t = 0;
+    for (int l = 0; l < n; l++) {
+        const hpnn_upd_layer &L = layers[l];
+        if (L.N % 32 || L.K % 32 || L.S < 1) return -2;
+        if (momentum && !L.V32) return -1;
+        a.L[l] = L;
+        a.tile0[l] = t;
+        t += (L.N / 32) * (L.K / 32);
+    }
+    a.tile0[n] = t;
+    hipLaunchKernelGGL(sgd_update_multi_kernel, dim3(t), dim3(256), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -18,6 +18,7 @@
 #ifndef HPNN_MFMA_COMMON_H
 #define HPNN_MFMA_COMMON_H
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 namespace hpnn {
 
@@ -62,6 +63,28 @@ __device__ __forceinline__ bf16x8 frag_tr(const char *img, int kbase, int c0, in
     return __builtin_bit_cast(bf16x8, v);
 }
 
+/* One LDS-DMA instruction (global_load_lds_dwordx4): lane i copies 16 bytes from
+ * gsrc (per lane) to LDS byte lds_dst + 16 i (lds_dst wave-uniform, via M0).
+ * Emitted as inline asm on purpose: the compiler's waitcnt pass treats every pending
+ * builtin LDS-DMA as a possible alias of any later ds_read and inserts a full
+ * s_waitcnt vmcnt(0) before it, which drains the prefetch ring.  The kernels count
+ * these loads themselves (wait_vm<N>, barriers); to the compiler they are unknown
+ * VMEM ops, which only makes its own vmcnt waits stricter (never unsafe). */
+__device__ __forceinline__ void glds16(const void *gsrc, char *lds_dst) {
+    const unsigned int m0 =
+        __builtin_amdgcn_readfirstlane((unsigned int)(uintptr_t)(__attribute__((address_space(3))) char *)lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0)
+                 : "memory", "m0");
+}
+
+/* 4-byte variant (global_load_lds_dword): lane i -> LDS byte lds_dst + 4 i */
+__device__ __forceinline__ void glds4(const void *gsrc, char *lds_dst) {
+    const unsigned int m0 =
+        __builtin_amdgcn_readfirstlane((unsigned int)(uintptr_t)(__attribute__((address_space(3))) char *)lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gsrc), "s"(m0)
+                 : "memory", "m0");
+}
+
 /* LDS-DMA: one 1 KiB piece = 16 rows x 32 cols of sub-tile `sub` of a T32 image with
  * R rows, from a row-major global matrix (ld_bytes per row); lane i fills bytes
  * [16i, 16i+16) of the piece, fetching the logical columns the half-swap puts there */
@@ -72,7 +95,35 @@ __device__ __forceinline__ void glds_t32_piece(const char *gbase, size_t ld_byte
     const int r = rp + (lane >> 2), cp = lane & 3;
     const int col = sub * 32 + ((cp ^ t32_g(r)) & 3) * 8;
     const char *src = gbase + (size_t)r * ld_bytes + (size_t)col * 2;
-    __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(img + sub * (R * 64) + rp * 64), 16, 0, 0);
+    glds16(src, img + sub * (R * 64) + rp * 64);
+}
+
+/* X image: K/64 sub-tiles of [R][64] bf16 (128-byte rows, 16-byte chunk c of row r at
+ * c ^ ((r >> 1) & 7): conflict-free ds_read_b128 row reads, bank-simulated) and, when
+ * K % 64 == 32, one T32 tail sub-tile.  128-byte rows let every LDS-DMA piece fetch
+ * 8 rows x 128 B (whole cache lines) instead of 16 rows x 64 B. */
+__device__ __forceinline__ int w128_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int R, int S64>
+__device__ __forceinline__ void glds_x_piece(const char *g, size_t ld, char *img, int p, int lane) {
+    constexpr int PF = R / 8; /* pieces per full sub-tile */
+    if (p < S64 * PF) {
+        const int sub = p / PF, rp = (p % PF) * 8;
+        const int r = rp + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
+        const char *src = g + (size_t)r * ld + (size_t)(sub * 64 + lc * 8) * 2;
+        glds16(src, img + sub * (R * 128) + rp * 128);
+    } else {
+        glds_t32_piece<R>(g + (size_t)S64 * 128, ld, img + S64 * (R * 128), p - S64 * PF, lane);
+    }
+}
+
+template <int R, int S64>
+__device__ __forceinline__ bf16x8 x_frag(const char *img, int r0, int ks, int lane) {
+    if (ks < 2 * S64) {
+        const int r = r0 + (lane & 15), c = (ks & 1) * 4 + (lane >> 4);
+        return *(const bf16x8 *)(img + (ks >> 1) * (R * 128) + w128_off(r, c));
+    }
+    return frag_row<R>(img + S64 * (R * 128), r0, 0, lane);
 }
 
 template <int N>

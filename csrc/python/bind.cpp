@@ -88,6 +88,43 @@ PYBIND11_MODULE(_native, m) {
               "reduce_slabs2");
     });
     m.def("mlp3_slab_floats", []() { return hpnn_mlp3_slab_floats(); });
+    m.def("mlp3_fused", [](uptr X, int ldx, int K0, uptr W0f, uptr W1, uptr W2, uptr labels, uptr T, int ldt,
+                           float t_hi, float t_lo, uptr D1, uptr gslab, uptr loss, uptr correct, int Bp, int n_valid,
+                           int n_out, int type, int grid, uptr stream) {
+        const int rc = hpnn_mlp3_fused(P(X), ldx, K0, P(W0f), P(W1), P(W2), (const int *)P(labels),
+                                       (const float *)P(T), ldt, t_hi, t_lo, P(D1), (float *)P(gslab), (float *)P(loss),
+                                       (unsigned int *)P(correct), Bp, n_valid, n_out, type, grid, S(stream));
+        if (rc <= 0) check(rc ? rc : -1, "mlp3_fused");
+        return rc;
+    });
+    m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
+    m.def("reduce_groups", [](uptr slab, int Sn, long stride, long n, int groups, uptr out, uptr stream) {
+        check(hpnn_reduce_groups((const float *)P(slab), Sn, stride, n, groups, (float *)P(out), S(stream)),
+              "reduce_groups");
+    });
+    m.def(
+        "sgd_update_multi",
+        [](py::list layers, float lr, float alpha, float scale, int momentum, uptr stream) {
+            hpnn_upd_layer L[HPNN_UPD_MAX];
+            const int n = (int)py::len(layers);
+            if (n < 1 || n > HPNN_UPD_MAX) throw std::runtime_error("sgd_update_multi: 1..8 layers");
+            for (int i = 0; i < n; i++) {
+                py::tuple t = layers[i].cast<py::tuple>();
+                if (py::len(t) != 10) throw std::runtime_error("sgd_update_multi: layer tuple of 10");
+                L[i].W32 = (float *)P(t[0].cast<uptr>());
+                L[i].V32 = (float *)P(t[1].cast<uptr>());
+                L[i].G = (const float *)P(t[2].cast<uptr>());
+                L[i].gstride = t[3].cast<long>();
+                L[i].Wbf = P(t[4].cast<uptr>());
+                L[i].Wt = P(t[5].cast<uptr>());
+                L[i].Wf = P(t[6].cast<uptr>());
+                L[i].S = t[7].cast<int>();
+                L[i].N = t[8].cast<int>();
+                L[i].K = t[9].cast<int>();
+            }
+            check(hpnn_sgd_update_multi(L, n, lr, alpha, scale, momentum, S(stream)), "sgd_update_multi");
+        },
+        "layers: [(W32, V32, G, gstride, Wbf, Wt, Wf, S, N, K)] device addresses (0 = none)");
     m.def("device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

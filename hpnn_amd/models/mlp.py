@@ -98,16 +98,34 @@ class MLP:
         # loss / accuracy: 64 slots x 16 floats ([0] loss sum, [1] hits as uint32 bits),
         # see HPNN_STAT_SLOTS in csrc/gpu/kernels.h
         self.stats = torch.zeros(64, 16, dtype=torch.float32, device=dev)
-        # fused 3-layer path (csrc/gpu/kernels_mlp3.hip) for n_in-128-64-(<=32) nets
+        # fused 3-layer paths (csrc/gpu/kernels_mlp3.hip) for n_in-128-64-(<=32) nets:
+        #   "x"   : mlp3_fused (X -> delta1 in one kernel, W0 register-resident)
+        #   "mid" : gemm_nt layer 0 + mlp3_mid (H1 -> delta1)
         eligible = self.L == 3 and tuple(self.Np) == ops.MLP3_DIMS
-        self.fused = eligible if fused is None else (bool(fused) and eligible)
-        if fused and not eligible:
-            raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
-        if self.fused:
+        x_ok = eligible and self.Kp[0] in ops.MLP3F_K0
+        if fused is None or fused is True:
+            mode = "x" if x_ok else ("mid" if eligible else None)
+            if fused is True and mode is None:
+                raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
+        elif fused in ("x", "mid"):
+            if not (x_ok if fused == "x" else eligible):
+                raise ValueError(f"fused={fused!r} not available for dims {self.Kp[0]}-{self.Np}")
+            mode = fused
+        else:
+            mode = None
+        self.fused_mode = mode
+        self.fused = mode is not None
+        self.W0f = None
+        if mode == "mid":
             grid = max(1, min(mid_grid, self.Bp // 64))
-            self.midslab = torch.empty(grid, self.Np[1] * self.Kp[1] + self.Np[2] * self.Kp[2], dtype=torch.float32,
-                                       device=dev)
+            self.midslab = torch.empty(grid, ops.MLP3_SLAB, dtype=torch.float32, device=dev)
             self.midtmp = torch.empty(16 * self.midslab.shape[1], dtype=torch.float32, device=dev)
+        elif mode == "x":
+            grid = ops.mlp3_fused_grid(self.Bp, dev)
+            self.midslab = torch.empty(grid, ops.MLP3_SLAB, dtype=torch.float32, device=dev)
+            self.mid_groups = min(16, grid)
+            self.midtmp = torch.empty(16 * ops.MLP3_SLAB, dtype=torch.float32, device=dev)
+            self.W0f = torch.empty(self.Np[0] * self.Kp[0], dtype=torch.bfloat16, device=dev)
         self.refresh_bf16()
 
     # ------------------------------------------------------------------ helpers
@@ -125,7 +143,7 @@ class MLP:
 
     def refresh_bf16(self):
         for l in range(self.L):
-            ops.cast_weights(self.W32[l], self.Wb[l], self.Wt[l])
+            ops.cast_weights(self.W32[l], self.Wb[l], self.Wt[l], self.W0f if l == 0 else None)
 
     def host_weights(self):
         """FP64 [N, M] weights (unpadded), for kernel.opt dumps / parity checks."""
@@ -164,7 +182,24 @@ class MLP:
 
     def update_layer(self, l, lr, alpha, scale, from_G=False):
         G = self.G[l] if from_G else self.slab[l]
+        if l == 0 and self.W0f is not None:
+            ops.sgd_update_multi([(self.W32[0], self.V32[0], G, self.Wb[0], self.Wt[0], self.W0f)], lr, alpha,
+                                 scale, self.momentum)
+            return
         ops.sgd_update(self.W32[l], self.V32[l], G, self.Wb[l], self.Wt[l], lr, alpha, scale, self.momentum)
+
+    def update_all(self, lr, alpha, scale, grads):
+        """every layer's optimizer step in one launch; grads[l]: [S, N, K] (view) or [N, K]"""
+        ops.sgd_update_multi([(self.W32[l], self.V32[l], grads[l], self.Wb[l], self.Wt[l],
+                               self.W0f if l == 0 else None) for l in range(self.L)], lr, alpha, scale, self.momentum)
+
+    def _mid_group_views(self):
+        """[G1 | G2] partial sums in midtmp as [groups, N, K] views for update_all"""
+        g = self.mid_groups
+        t = self.midtmp[:g * ops.MLP3_SLAB].view(g, ops.MLP3_SLAB)
+        n1 = self.Np[1] * self.Kp[1]
+        return (t[:, :n1].view(g, self.Np[1], self.Kp[1]),
+                t[:, n1:n1 + self.Np[2] * self.Kp[2]].view(g, self.Np[2], self.Kp[2]))
 
     def _t_hilo(self):
         return (1.0, 0.0) if self.type == ops.TYPE_SNN else (1.0, -1.0)
@@ -176,11 +211,7 @@ class MLP:
         become ready from the last to the first)."""
         n_valid = self.Bp if n_valid is None else n_valid
         if self.fused:
-            t_hi, t_lo = self._t_hilo()
-            ops.gemm_nt(X, self.Wb[0], ops.EPI_ACT, out=self.H[0])
-            ops.mlp3_mid(self.H[0], self.Wb[1], self.Wt[1], self.Wb[2], self.Wt[2], self.D[0], self.midslab,
-                         self.n_out, self.type, labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid,
-                         loss_acc=self.stats[0, 0:1], correct=self.stats[0, 1:2])
+            self._fused_front(X, labels, T, n_valid)
             # G1 | G2 are contiguous in grad_flat, exactly the per-block slab layout
             g12 = self.grad_flat[self.G[1].data_ptr() // 4 - self.grad_flat.data_ptr() // 4:]
             ops.reduce_slabs2(self.midslab, g12[:self.midslab.shape[1]], self.midtmp)
@@ -200,10 +231,32 @@ class MLP:
             if on_ready:
                 on_ready(l)
 
+    def _fused_front(self, X, labels, T, n_valid):
+        """X -> delta1 (self.D[0]) + per-block [G1 | G2] slabs (self.midslab)"""
+        t_hi, t_lo = self._t_hilo()
+        kw = dict(labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid, loss_acc=self.stats[0, 0:1],
+                  correct=self.stats[0, 1:2])
+        if self.fused_mode == "x":
+            ops.mlp3_fused(X, self.Wb[0], self.W0f, self.Wb[1], self.Wb[2], self.D[0], self.midslab, self.n_out,
+                           self.type, **kw)
+        else:
+            ops.gemm_nt(X, self.Wb[0], ops.EPI_ACT, out=self.H[0])
+            ops.mlp3_mid(self.H[0], self.Wb[1], self.Wt[1], self.Wb[2], self.Wt[2], self.D[0], self.midslab,
+                         self.n_out, self.type, **kw)
+
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         """One minibatch fwd + bwd + update on the current stream (no host sync)."""
         n_valid = self.Bp if n_valid is None else n_valid
         scale = 1.0 / n_valid
+        if self.fused_mode == "x":
+            # 4 launches: fused front, G0 GEMM, first [G1|G2] reduction pass, all updates
+            self._fused_front(X, labels, T, n_valid)
+            ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
+            ops.reduce_groups(self.midslab, self.mid_groups,
+                              self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB))
+            g1, g2 = self._mid_group_views()
+            self.update_all(lr, alpha, scale, [self.slab[0], g1, g2])
+            return
         if self.fused:
             self.backward_grads(X, labels=labels, T=T, n_valid=n_valid)
             self.update_layer(0, lr, alpha, scale)

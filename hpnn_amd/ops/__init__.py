@@ -123,6 +123,79 @@ def mlp3_mid(H1, W1, W1t, W2, W2t, D1, gslab, n_out, net_type, labels=None, T=No
     return D1
 
 
+MLP3F_K0 = (256, 512, 800, 832, 896)  # first-layer input widths of hpnn_mlp3_fused
+MLP3_SLAB = 128 * 64 + 64 * 32
+
+
+def mlp3_fused_grid(Bp, device=None):
+    """workgroups (= gradient slab rows) hpnn_mlp3_fused uses for Bp samples."""
+    if device is not None and torch.device(device).type == "cpu":
+        return 1
+    g = native().mlp3_fused_grid(int(Bp), 0)
+    if g <= 0:
+        raise ValueError(f"mlp3_fused: batch {Bp} not a multiple of 32")
+    return g
+
+
+def mlp3_fused(X, W0, W0f, W1, W2, D1, gslab, n_out, net_type, labels=None, T=None, t_hi=1.0, t_lo=0.0,
+               n_valid=None, loss_acc=None, correct=None):
+    """Whole n_in-128-64-(<=32) step up to delta1 in one persistent kernel
+    (csrc/gpu/kernels_mlp3.hip, mlp3_fused_kernel): X [Bp, K0] -> delta1 into D1
+    [Bp, 128], per-block [G1 | G2] slabs into gslab [grid, MLP3_SLAB], loss/hits.
+    W0f: fragment-major BF16 copy of W0 (frag_major); W0 (row-major) is only used by
+    the CPU emulation."""
+    Bp, K0 = X.shape[0], W0.shape[1]
+    n_valid = Bp if n_valid is None else int(n_valid)
+    if _cpu(X):
+        H1 = bipolar(X[:, :K0].float() @ W0.float().t()).bfloat16()
+        return _cpu_mlp3_mid(H1, W1, None, W2, None, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid,
+                             loss_acc, correct)
+    native().mlp3_fused(X.data_ptr(), X.stride(0), K0, W0f.data_ptr(), W1.data_ptr(), W2.data_ptr(), _ptr(labels),
+                        _ptr(T), T.stride(0) if T is not None else 0, float(t_hi), float(t_lo), D1.data_ptr(),
+                        gslab.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid, n_out, net_type,
+                        gslab.shape[0], _stream())
+    return D1
+
+
+def frag_major(W):
+    """[N, K] -> flat MFMA-fragment-major copy (layout of hpnn_sgd_update_multi's Wf):
+    element (n, k) at (((n//16)*(K//32) + k//32)*64 + n%16 + 16*((k//8)%4))*8 + k%8."""
+    N, K = W.shape
+    return W.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1)
+
+
+def reduce_groups(slab, groups, out):
+    """out[g, :] = sum of slab rows [g*ceil(S/groups), ...) (first reduction pass)."""
+    S = slab.shape[0]
+    n = slab[0].numel()
+    if _cpu(slab):
+        sg = -(-S // groups)
+        for g in range(groups):
+            out[g].copy_(slab[g * sg:min(S, (g + 1) * sg)].reshape(-1, n).sum(0).view_as(out[g]))
+        return out
+    native().reduce_groups(slab.data_ptr(), S, slab.stride(0), n, groups, out.data_ptr(), _stream())
+    return out
+
+
+def sgd_update_multi(layers, lr, alpha=0.0, scale=1.0, momentum=False):
+    """All layers' optimizer steps in one launch.  layers: list of
+    (W32, V32, G, Wbf, Wt, Wf) with G [S, N, K] (or a strided view) or [N, K]; Wf may be None."""
+    if _cpu(layers[0][0]):
+        for W32, V32, G, Wbf, Wt, Wf in layers:
+            sgd_update(W32, V32, G, Wbf, Wt, lr, alpha, scale, momentum)
+            if Wf is not None:
+                Wf.copy_(frag_major(W32.bfloat16()))
+        return
+    desc = []
+    for W32, V32, G, Wbf, Wt, Wf in layers:
+        N, K = W32.shape
+        S = G.shape[0] if G.dim() == 3 else 1
+        gstride = G.stride(0) if G.dim() == 3 else 0
+        desc.append((W32.data_ptr(), _ptr(V32), G.data_ptr(), gstride, Wbf.data_ptr(), Wt.data_ptr(), _ptr(Wf), S,
+                     N, K))
+    native().sgd_update_multi(desc, float(lr), float(alpha), float(scale), int(momentum), _stream())
+
+
 def sgd_update(W32, V32, G, Wbf, Wt, lr, alpha=0.0, scale=1.0, momentum=False):
     """W32[N,K] FP32 master; G: [S,N,K] or [N,K] FP32 gradient sum(s)."""
     N, K = W32.shape
@@ -143,11 +216,16 @@ def sgd_update(W32, V32, G, Wbf, Wt, lr, alpha=0.0, scale=1.0, momentum=False):
                         float(lr), float(alpha), float(scale), int(momentum), _stream())
 
 
-def cast_weights(W32, Wbf, Wt):
+def cast_weights(W32, Wbf, Wt, Wf=None):
     N, K = W32.shape
     if _cpu(W32):
         Wbf.copy_(W32.bfloat16())
         Wt.copy_(W32.bfloat16().t())
+        if Wf is not None:
+            Wf.copy_(frag_major(Wbf))
+        return
+    if Wf is not None:  # an lr = 0 update is exactly a cast (same kernel writes Wf)
+        sgd_update_multi([(W32, None, W32, Wbf, Wt, Wf)], 0.0, 0.0, 0.0, False)
         return
     native().cast_weights(W32.data_ptr(), Wbf.data_ptr(), Wt.data_ptr(), N, K, _stream())
 
@@ -231,6 +309,7 @@ def _cpu_mlp3_mid(H1, W1, W1t, W2, W2t, D1, gslab, n_out, net_type, labels, T, t
     """PyTorch emulation with the kernel's rounding points (bf16 H2 / deltas)."""
     Bp = H1.shape[0]
     H2 = bipolar(H1.float() @ W1.float().t()).bfloat16()
+    D1 = D1 if D1 is not None else torch.empty_like(H1)
     Z = (H2.float() @ W2.float().t())
     D3 = torch.zeros(Bp, W2.shape[0], dtype=torch.bfloat16)
     _cpu_output_delta(Z, n_out, net_type, D3, labels, T, t_hi, t_lo, n_valid, None, loss_acc, correct)

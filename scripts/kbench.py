@@ -34,35 +34,35 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--mid-grid", default="256,512")
+    ap.add_argument("--mid-grid", default="512")
+    ap.add_argument("--modes", default="x,mid")
     args = ap.parse_args()
     dev = torch.device("cuda")
-    for mg in [int(x) for x in args.mid_grid.split(",")]:
-        m = MLP([784, 128, 64, 10], "SNN", batch=args.batch, momentum=True, mid_grid=mg)
+    for mode in args.modes.split(","):
+        m = MLP([784, 128, 64, 10], "SNN", batch=args.batch, momentum=True, fused=mode,
+                mid_grid=int(args.mid_grid.split(",")[0]))
         X = m.prepare_input(torch.rand(m.Bp, 784, device=dev))
         lab = torch.randint(0, 10, (m.Bp,), device=dev, dtype=torch.int32)
         bytes_x = X.numel() * 2
-        red_out = torch.empty(m.midslab.shape[1], device=dev)
-        phases = {
-            "fwd_l0 (gemm_nt X.W0^T)": lambda: ops.gemm_nt(X, m.Wb[0], ops.EPI_ACT, out=m.H[0]),
-            "mlp3_mid": lambda: ops.mlp3_mid(m.H[0], m.Wb[1], m.Wt[1], m.Wb[2], m.Wt[2], m.D[0], m.midslab, 10,
-                                             ops.TYPE_SNN, labels=lab, loss_acc=m.stats[0, 0:1],
-                                             correct=m.stats[0, 1:2]),
-            "grad_l0 (gemm_tn D1^T.X)": lambda: ops.gemm_tn(m.D[0], X, splits=m.S[0], out=m.slab[0]),
-            "reduce_mid_slabs": lambda: ops.reduce_slabs2(m.midslab, red_out, m.midtmp),
-            "update_l0": lambda: m.update_layer(0, 0.01, 0.2, 1.0 / m.Bp),
-            "update_l1": lambda: m.update_layer(1, 0.01, 0.2, 1.0 / m.Bp, from_G=True),
-            "update_l2": lambda: m.update_layer(2, 0.01, 0.2, 1.0 / m.Bp, from_G=True),
-            "full train_step": lambda: m.train_step(X, labels=lab),
-        }
+        kw = dict(labels=lab, T=None, n_valid=m.Bp)
+        phases = {"fused front (" + mode + ")": lambda: m._fused_front(X, **kw)}
+        if mode == "mid":
+            phases["  fwd_l0 (gemm_nt X.W0^T)"] = lambda: ops.gemm_nt(X, m.Wb[0], ops.EPI_ACT, out=m.H[0])
+        phases["grad_l0 (gemm_tn D1^T.X)"] = lambda: ops.gemm_tn(m.D[0], X, splits=m.S[0], out=m.slab[0])
+        if mode == "x":
+            gv = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
+            g1, g2 = m._mid_group_views()
+            phases["reduce_groups (mid slabs)"] = lambda: ops.reduce_groups(m.midslab, m.mid_groups, gv)
+            phases["update_all (3 layers)"] = lambda: m.update_all(0.01, 0.2, 1.0 / m.Bp, [m.slab[0], g1, g2])
+        phases["full train_step"] = lambda: m.train_step(X, labels=lab)
         for f in phases.values():
             f()
         torch.cuda.synchronize()
-        print(f"--- batch {m.Bp} mid_grid {m.midslab.shape[0]} splits {m.S}")
+        print(f"--- batch {m.Bp} mode {mode} mid slabs {m.midslab.shape[0]} splits {m.S}")
         for name, f in phases.items():
             med, mn = timeit(f, args.reps)
             extra = ""
-            if name.startswith("fwd_l0") or name.startswith("grad_l0"):
+            if "X" in name:
                 extra = f"  X stream {bytes_x / med / 1e6:.2f} TB/s"
             print(f"{name:32s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
 

@@ -29,6 +29,25 @@ def test_gemm_nt(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 128, 800), (16416, 64, 800), (32768, 128, 512), (16384, 128, 1024),
+                                   (65536, 128, 800)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT])
+def test_gemm_nt_weight_stationary(gpu, M, N, K, epi):
+    """large-batch shapes that take the weight-stationary kernel (kernels_ws.hip); M=16416
+    leaves a ragged tile count over the persistent grid; X has a padded row stride."""
+    torch.manual_seed(M + N + K)
+    Xs = _rand(M, K + 64).bfloat16()
+    A = Xs[:, :K]
+    B = (_rand(N, K) + torch.arange(N, device="cuda")[:, None] * 0.01).bfloat16()
+    for f32 in (False, True):
+        C = ops.gemm_nt(A, B, epi, out_f32=f32)
+        R = ops.ref_gemm_nt(A, B, epi, None)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (C.float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+
+
 def test_gemm_nt_identity(gpu):
     """A = I checks the C layout with an asymmetric B (cdna guide section 3)."""
     M, N, K = 128, 64, 128

@@ -56,15 +56,17 @@ def test_predict_matches_forward(gpu):
 
 
 @pytest.mark.parametrize("net_type", ["SNN", "ANN", "LNN"])
-@pytest.mark.parametrize("B,n_valid", [(1024, 1024), (640, 600)])
-def test_fused_matches_layerwise(gpu, net_type, B, n_valid):
-    """fused mlp3 path == per-layer path (same math, different summation order)."""
+@pytest.mark.parametrize("B,n_valid", [(1024, 1024), (640, 600), (16384, 16000), (40960, 40000)])
+@pytest.mark.parametrize("mode,n_in", [("x", 784), ("mid", 784), ("x", 250)])
+def test_fused_matches_layerwise(gpu, net_type, B, n_valid, mode, n_in):
+    """fused mlp3 paths == per-layer path (same math, different summation order)."""
     torch.manual_seed(1)
-    sizes = [784, 128, 64, 10]
-    mf = MLP(sizes, net_type, batch=B, momentum=True, seed=5, fused=True, mid_grid=3)
+    sizes = [n_in, 128, 64, 10]
+    mf = MLP(sizes, net_type, batch=B, momentum=True, seed=5, fused=mode, mid_grid=3)
+    assert mf.fused_mode == mode
     ml = MLP(sizes, net_type, batch=B, momentum=True, seed=5, fused=False)
     assert mf.fused and not ml.fused
-    X = torch.rand(mf.Bp, 784)
+    X = torch.rand(mf.Bp, n_in)
     labels = torch.randint(0, 10, (mf.Bp,), dtype=torch.int32).cuda()
     Xd = mf.prepare_input(X)
     for _ in range(2):
@@ -78,3 +80,78 @@ def test_fused_matches_layerwise(gpu, net_type, B, n_valid):
     assert la == pytest.approx(lb, rel=2e-2)
     assert abs(ca - cb) <= max(2, 0.01 * n_valid)
     assert torch.equal(mf.D[0][n_valid:], torch.zeros_like(mf.D[0][n_valid:]))
+
+
+@pytest.mark.parametrize("net_type", ["SNN", "ANN"])
+def test_fused_x_dense_targets(gpu, net_type):
+    """mlp3_fused with dense targets T (no labels) == the per-layer path with T."""
+    torch.manual_seed(2)
+    sizes, B = [784, 128, 64, 20], 2048
+    mf = MLP(sizes, net_type, batch=B, momentum=False, seed=9, fused="x")
+    ml = MLP(sizes, net_type, batch=B, momentum=False, seed=9, fused=False)
+    X = mf.prepare_input(torch.rand(B, 784))
+    lo = 0.0 if net_type == "SNN" else -1.0
+    T = torch.full((B, 20), lo, device="cuda")
+    T[torch.arange(B), torch.randint(0, 20, (B,))] = 1.0
+    for m in (mf, ml):
+        m.train_step(X, T=T, lr=0.05)
+    torch.cuda.synchronize()
+    for a, b in zip(mf.host_weights(), ml.host_weights()):
+        assert (a - b).abs().max().item() < 2e-3 * (b.abs().max().item() + 1e-3)
+    assert mf.read_stats()[0] == pytest.approx(ml.read_stats()[0], rel=2e-2)
+    assert abs(mf.read_stats()[1] - ml.read_stats()[1]) <= 20
+
+
+def test_fused_x_kernel_vs_emulation(gpu):
+    """kernel outputs (delta1, [G1|G2] slab sum, loss, hits) vs the PyTorch emulation
+    with the same rounding points; W0f is the fragment-major copy the update writes."""
+    from hpnn_amd import ops
+    torch.manual_seed(3)
+    sizes, B = [784, 128, 64, 10], 8192
+    m = MLP(sizes, "SNN", batch=B, seed=4, fused="x")
+    assert torch.equal(m.W0f, ops.frag_major(m.Wb[0]))
+    X = m.prepare_input(torch.rand(B, 784))
+    lab = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
+    m.reset_stats()
+    m._fused_front(X, lab, None, B - 5)
+    torch.cuda.synchronize()
+    slab = torch.zeros(1, ops.MLP3_SLAB)
+    D1 = torch.empty(B, 128, dtype=torch.bfloat16)
+    st = torch.zeros(64, 16)
+    ops.mlp3_fused(X.cpu(), m.Wb[0].cpu(), None, m.Wb[1].cpu(), m.Wb[2].cpu(), D1, slab, 10, ops.TYPE_SNN,
+                   labels=lab.cpu(), n_valid=B - 5, loss_acc=st[0, 0:1], correct=st[0, 1:2])
+    d = (m.D[0].cpu().float() - D1.float()).abs().max().item()
+    assert d < 2e-2 * (D1.float().abs().max().item() + 1e-6), d
+    got = m.midslab.sum(0).cpu()
+    ref_ = slab[0]
+    assert (got - ref_).abs().max().item() < 2e-2 * (ref_.abs().max().item() + 1e-6)
+    loss, hits = m.read_stats()
+    assert loss == pytest.approx(st[0, 0].item(), rel=1e-2)
+    assert abs(hits - ops_hits(st)) <= 40
+
+
+def ops_hits(st):
+    return int(st[:, 1].contiguous().view(torch.int32).long().sum())
+
+
+def test_update_multi_writes_fragment_major(gpu):
+    from hpnn_amd import ops
+    torch.manual_seed(5)
+    W = torch.randn(128, 800, device="cuda")
+    V = torch.zeros_like(W)
+    G = torch.randn(4, 128, 800, device="cuda")
+    Wb = torch.empty(128, 800, dtype=torch.bfloat16, device="cuda")
+    Wt = torch.empty(800, 128, dtype=torch.bfloat16, device="cuda")
+    Wf = torch.empty(128 * 800, dtype=torch.bfloat16, device="cuda")
+    W2 = torch.randn(64, 128, device="cuda")
+    G2 = torch.randn(128 * 64 * 3, device="cuda")[:64 * 128 * 3].view(3, 64, 128)
+    W2b = torch.empty(64, 128, dtype=torch.bfloat16, device="cuda")
+    W2t = torch.empty(128, 64, dtype=torch.bfloat16, device="cuda")
+    Wr, W2r = W.clone(), W2.clone()
+    ops.sgd_update_multi([(W, V, G, Wb, Wt, Wf), (W2, None, G2, W2b, W2t, None)], 0.1, 0.0, 0.5, False)
+    torch.cuda.synchronize()
+    assert torch.allclose(W, Wr + 0.1 * 0.5 * G.sum(0), atol=1e-5)
+    assert torch.allclose(W2, W2r + 0.1 * 0.5 * G2.sum(0), atol=1e-5)
+    assert torch.equal(Wb, W.bfloat16()) and torch.equal(Wt, W.bfloat16().t())
+    assert torch.equal(Wf, ops.frag_major(Wb))
+    assert torch.equal(W2t, W2.bfloat16().t())
