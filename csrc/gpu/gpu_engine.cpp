@@ -275,10 +275,12 @@ struct Batched {
     /* loss / accuracy slots: HPNN_STAT_SLOTS x HPNN_STAT_STRIDE floats ([0] loss, [1] hits) */
     float *acc = nullptr;
     static constexpr size_t ACC_BYTES = HPNN_STAT_SLOTS * HPNN_STAT_STRIDE * 4;
-    /* fused n_in-128-64-(<=32) path (kernels_mlp3.hip) */
-    bool fused = false;
-    int mid_grid = 0;
+    /* fused n_in-128-64-(<=32) paths: fused_x = hpnn_mlp3_fused (X -> delta1 in one
+     * kernel, kernels_mlp3x.hip), else gemm_nt + hpnn_mlp3_mid (kernels_mlp3.hip) */
+    bool fused = false, fused_x = false;
+    int mid_grid = 0, mid_groups = 1;
     float *midslab = nullptr, *midtmp = nullptr, *G12 = nullptr;
+    void *W0f = nullptr; /* fragment-major BF16 W0 (fused_x) */
     hipStream_t s = nullptr;
 
     ~Batched() {
@@ -296,6 +298,7 @@ struct Batched {
         hipFree(midslab);
         hipFree(midtmp);
         hipFree(G12);
+        hipFree(W0f);
     }
 
     /* sum the stat slots: returns (loss sum, hits) */
@@ -352,12 +355,20 @@ struct Batched {
         HIPCHK(hipMalloc(&acc, ACC_BYTES));
         HIPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
         fused = (L == 3 && Np[0] == 128 && Np[1] == 64 && Np[2] == 32);
+        fused_x = fused && (Kp[0] == 256 || Kp[0] == 512 || Kp[0] == 800 || Kp[0] == 832 || Kp[0] == 896);
         if (fused) {
             const int slab_f = hpnn_mlp3_slab_floats();
-            mid_grid = Bp / 64 < 512 ? Bp / 64 : 512;
+            mid_grid = fused_x ? hpnn_mlp3_fused_grid(Bp, 0) : (Bp / 64 < 512 ? Bp / 64 : 512);
+            if (mid_grid <= 0) return FALSE;
+            mid_groups = mid_grid < 16 ? mid_grid : 16;
             HIPCHK(hipMalloc(&midslab, (size_t)mid_grid * slab_f * 4));
             HIPCHK(hipMalloc(&midtmp, (size_t)16 * slab_f * 4));
             HIPCHK(hipMalloc(&G12, (size_t)slab_f * 4));
+            if (fused_x) {
+                HIPCHK(hipMalloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
+                hpnn_upd_layer c0 = {W32[0], nullptr, W32[0], 0, Wb[0], Wt[0], W0f, 1, Np[0], Kp[0]};
+                if (hpnn_sgd_update_multi(&c0, 1, 0.f, 0.f, 0.f, 0, s)) return FALSE; /* lr 0: a cast */
+            }
         }
         return TRUE;
     }
@@ -379,21 +390,31 @@ struct Batched {
     BOOL step_fused(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
         const float scale = 1.0f / (float)n_valid;
         const float t_lo = type == 2 ? 0.f : -1.f;
-        (void)t_lo;
-        int r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0], HPNN_EPI_ACT, 0, s);
-        if (!r)
-            r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, 0.f, D[0], midslab, acc,
-                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid, s);
+        const int slab_f = hpnn_mlp3_slab_floats();
+        int r;
+        if (fused_x) {
+            r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab, acc,
+                                (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, s);
+            r = r > 0 ? 0 : (r ? r : -1);
+        } else {
+            r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0], HPNN_EPI_ACT, 0,
+                                  s);
+            if (!r)
+                r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab, acc,
+                                  (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid,
+                                  s);
+        }
         if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
-        if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, hpnn_mlp3_slab_floats(), hpnn_mlp3_slab_floats(), midtmp, G12, s);
-        if (!r)
-            r = hpnn_sgd_update(W32[0], V32[0], slab[0], S[0], (long)Np[0] * Kp[0], Wb[0], Wt[0], Np[0], Kp[0], lr,
-                                alpha, scale, mom ? 1 : 0, s);
-        if (!r)
-            r = hpnn_sgd_update(W32[1], V32[1], G12, 1, 0, Wb[1], Wt[1], Np[1], Kp[1], lr, alpha, scale, mom ? 1 : 0, s);
-        if (!r)
-            r = hpnn_sgd_update(W32[2], V32[2], G12 + (size_t)Np[1] * Kp[1], 1, 0, Wb[2], Wt[2], Np[2], Kp[2], lr,
-                                alpha, scale, mom ? 1 : 0, s);
+        /* first reduction pass of the [G1 | G2] block slabs; the optimizer sums the groups */
+        if (!r) r = hpnn_reduce_groups(midslab, mid_grid, slab_f, slab_f, mid_groups, midtmp, s);
+        if (!r) {
+            const long n1 = (long)Np[1] * Kp[1];
+            hpnn_upd_layer u[3] = {
+                {W32[0], V32[0], slab[0], (long)Np[0] * Kp[0], Wb[0], Wt[0], W0f, S[0], Np[0], Kp[0]},
+                {W32[1], V32[1], midtmp, slab_f, Wb[1], Wt[1], nullptr, mid_groups, Np[1], Kp[1]},
+                {W32[2], V32[2], midtmp + n1, slab_f, Wb[2], Wt[2], nullptr, mid_groups, Np[2], Kp[2]}};
+            r = hpnn_sgd_update_multi(u, 3, lr, alpha, scale, mom ? 1 : 0, s);
+        }
         if (r) NN_ERROR(stderr, "fused step failed: %d\n", r);
         return r == 0;
     }
@@ -413,6 +434,8 @@ struct Batched {
                 return FALSE;
             }
         }
+        /* every delta above used the pre-update weights: all gradients, then ONE update launch */
+        hpnn_upd_layer u[HPNN_UPD_MAX];
         for (int l = 0; l < L; l++) {
             const void *Hin = l ? H[l - 1] : X;
             int r = hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s);
@@ -420,10 +443,14 @@ struct Batched {
                 NN_ERROR(stderr, "gemm_tn (layer %d) failed: %d\n", l, r);
                 return FALSE;
             }
-            r = hpnn_sgd_update(W32[l], V32[l], slab[l], S[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], Np[l], Kp[l], lr,
-                                alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s);
-            if (r) return FALSE;
+            if (L <= HPNN_UPD_MAX)
+                u[l] = {W32[l], V32[l], slab[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], nullptr, S[l], Np[l], Kp[l]};
+            else if (hpnn_sgd_update(W32[l], V32[l], slab[l], S[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], Np[l], Kp[l],
+                                     lr, alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s))
+                return FALSE;
         }
+        if (L <= HPNN_UPD_MAX && hpnn_sgd_update_multi(u, L, lr, alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s))
+            return FALSE;
         return TRUE;
     }
 

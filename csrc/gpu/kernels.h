@@ -124,6 +124,8 @@ int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void 
                     const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                     float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
                     hipStream_t stream);
+/* profiling: s_memtime timeline of block 0 (HPNN_FZ_MODE=9), [8 waves][8 stages][8 marks] */
+int hpnn_mlp3_fused_trace(unsigned long long *out);
 /* grid hpnn_mlp3_fused will use for Bp samples (slab rows to allocate) */
 int hpnn_mlp3_fused_grid(int Bp, int grid);
 /* floats per block slab written by hpnn_mlp3_mid */

@@ -77,6 +77,34 @@ __device__ __forceinline__ void glds16(const void *gsrc, char *lds_dst) {
                  : "memory", "m0");
 }
 
+/* wave-uniform copy of a 64-bit value (readfirstlane returns int: widen through
+ * unsigned int, or a low half with bit 31 set sign-extends into the high half) */
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
+    const unsigned int lo = (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)v);
+    const unsigned int hi = (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)(v >> 32));
+    return ((unsigned long long)hi << 32) | (unsigned long long)lo;
+}
+
+/* Same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset
+ * (global_load_lds_dwordx4 voff, s[base]): one VGPR of addressing per lane instead of
+ * two, and the base is not replicated per lane. */
+__device__ __forceinline__ void glds16_sv(const void *gbase, unsigned int voff, char *lds_dst) {
+    const unsigned int m0 =
+        __builtin_amdgcn_readfirstlane((unsigned int)(uintptr_t)(__attribute__((address_space(3))) char *)lds_dst);
+    const unsigned long long b = (unsigned long long)(uintptr_t)gbase;
+    const unsigned long long bs = uniform_u64(b);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bs), "s"(m0)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void glds4_sv(const void *gbase, unsigned int voff, char *lds_dst) {
+    const unsigned int m0 =
+        __builtin_amdgcn_readfirstlane((unsigned int)(uintptr_t)(__attribute__((address_space(3))) char *)lds_dst);
+    const unsigned long long b = (unsigned long long)(uintptr_t)gbase;
+    const unsigned long long bs = uniform_u64(b);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(bs), "s"(m0)
+                 : "memory", "m0");
+}
+
 /* 4-byte variant (global_load_lds_dword): lane i -> LDS byte lds_dst + 4 i */
 __device__ __forceinline__ void glds4(const void *gsrc, char *lds_dst) {
     const unsigned int m0 =
@@ -117,6 +145,25 @@ __device__ __forceinline__ void glds_x_piece(const char *g, size_t ld, char *img
     }
 }
 
+/* glds_x_piece with a uniform base (SGPRs) and 32-bit lane offsets (ld_bytes * R < 4 GiB) */
+template <int R, int S64>
+__device__ __forceinline__ void glds_x_piece_sv(const char *g, unsigned int ld, char *img, int p, int lane) {
+    constexpr int PF = R / 8;
+    if (p < S64 * PF) {
+        const int sub = p / PF, rp = (p % PF) * 8;
+        const int r = rp + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
+        glds16_sv(g, (unsigned int)r * ld + (unsigned int)(sub * 64 + lc * 8) * 2u, img + sub * (R * 128) + rp * 128);
+    } else {
+        constexpr int PPS = R / 16;
+        const int pt = p - S64 * PF;
+        const int rp = pt * 16; /* one 32-col tail sub-tile: PPS pieces of 16 rows */
+        const int r = rp + (lane >> 2), cp = lane & 3;
+        const int col = S64 * 64 + ((cp ^ t32_g(r)) & 3) * 8;
+        (void)PPS;
+        glds16_sv(g, (unsigned int)r * ld + (unsigned int)col * 2u, img + S64 * (R * 128) + rp * 64);
+    }
+}
+
 template <int R, int S64>
 __device__ __forceinline__ bf16x8 x_frag(const char *img, int r0, int ks, int lane) {
     if (ks < 2 * S64) {
@@ -137,10 +184,42 @@ __device__ __forceinline__ void wait_vm() {
  * would emit vmcnt(0) and drain it) */
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+/* value of lane l ^ 16 / l ^ 32: gfx950 v_permlane16_swap / v_permlane32_swap (VALU, no
+ * LDS crossbar round trip like the ds_bpermute __shfl_xor compiles to).  With both
+ * operands = v, permlane16_swap yields {row-pair even value, odd value} in every lane
+ * (rows of 16 lanes), permlane32_swap {lower-half value, upper-half value}. */
+__device__ __forceinline__ float shfl_xor16(float v, int lane) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(((lane >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float shfl_xor32(float v, int lane) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float((lane >> 5) ? r[0] : r[1]);
+}
+__device__ __forceinline__ int shfl_xor16(int v, int lane) {
+    return __float_as_int(shfl_xor16(__int_as_float(v), lane));
+}
+__device__ __forceinline__ int shfl_xor32(int v, int lane) {
+    return __float_as_int(shfl_xor32(__int_as_float(v), lane));
+}
+/* reductions over the 4 rows of 16 lanes (lane>>4): every lane gets the result */
+__device__ __forceinline__ float rows_sum(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float rows_max(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return rows_sum(v);
 }
 
 }  // namespace hpnn

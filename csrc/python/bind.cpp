@@ -12,6 +12,8 @@
 #include <libhpnn.h>
 #include <stdexcept>
 #include <string>
+#include <vector>
+#include <pybind11/stl.h>
 
 #include "../gpu/kernels.h"
 
@@ -96,6 +98,11 @@ PYBIND11_MODULE(_native, m) {
                                        (unsigned int *)P(correct), Bp, n_valid, n_out, type, grid, S(stream));
         if (rc <= 0) check(rc ? rc : -1, "mlp3_fused");
         return rc;
+    });
+    m.def("mlp3_fused_trace", []() {
+        std::vector<unsigned long long> v(8 * 8 * 8);
+        check(hpnn_mlp3_fused_trace(v.data()), "mlp3_fused_trace");
+        return v;
     });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
     m.def("reduce_groups", [](uptr slab, int Sn, long stride, long n, int groups, uptr out, uptr stream) {
