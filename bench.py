@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--datasets", type=int, default=4, help="distinct synthetic minibatches cycled per GPU")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--alpha", type=float, default=0.2)
-    ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph (1 GPU)")
+    ap.add_argument("--graph", type=int, default=1, help="capture the steps in a HIP graph (1 GPU)")
+    ap.add_argument("--graph-steps", type=int, default=20, help="training steps per graph replay")
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
@@ -65,38 +66,50 @@ def main():
         dp.train_step(Xs[i % args.datasets], labels=Ls[i % args.datasets], lr=args.lr, alpha=args.alpha)
 
     use_graph = args.graph and world == 1
-    graphs = None
+    gsteps = max(1, args.graph_steps)
+    graphs = {}
+
+    def capture(n):
+        """one HIP graph holding n consecutive training steps (cycling over the synthetic
+        batches, whose input pointers are baked in): a replay launches n full steps, so the
+        host-side replay gap is paid once per n steps"""
+        if n not in graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(n):
+                    step(i)
+            graphs[n] = g
+        return graphs[n]
+
     if use_graph:
-        # one graph per synthetic batch (the input pointer is baked into the graph)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for i in range(3):
                 step(i)
         torch.cuda.current_stream().wait_stream(s)
-        graphs = []
-        for i in range(args.datasets):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                step(i)
-            graphs.append(gr)
+        # capture every graph the run will replay before anything is timed
+        for n in {gsteps, args.steps % gsteps, args.warmup % gsteps} - {0}:
+            capture(n)
 
-    def run(i):
-        if graphs is not None:
-            graphs[i % args.datasets].replay()
+    def run_steps(first, n):
+        if use_graph:
+            for _ in range(n // gsteps):
+                graphs[gsteps].replay()
+            if n % gsteps:
+                graphs[n % gsteps].replay()
         else:
-            step(i)
+            for i in range(first, first + n):
+                step(i)
 
-    for i in range(args.warmup):
-        run(i)
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     m.reset_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        run(i)
+    run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -129,6 +142,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "hip_graph": bool(use_graph),
+                "steps_per_graph": min(gsteps, args.steps) if use_graph else 0,
             },
             "train_loss_mean": loss_sum / max(1, samples // world),
         }

@@ -16,6 +16,7 @@ FP32 master weights and momentum; FP32 split-K gradient slabs.
 import ctypes
 import ctypes.util
 import math
+import os
 
 import torch
 
@@ -135,8 +136,9 @@ class MLP:
         tn = 128 if N % 128 == 0 else (64 if N % 64 == 0 else 32)
         tm = next(t for t in (128, 160, 96, 64, 32) if K % t == 0)
         tiles = (N // tn) * (K // tm)
+        rows = int(os.environ.get("HPNN_TN_ROWS", "1024"))  # minimum batch rows per split
         s = -(-512 // max(tiles, 1))
-        s = max(1, min(s, max(1, Bp // 1024)))
+        s = max(1, min(s, max(1, Bp // rows)))
         while s > 1 and Bp % (64 * s):
             s -= 1
         return s
