@@ -28,11 +28,14 @@ extern "C" DOUBLE ann_act(DOUBLE x) { return 2.0 / (1.0 + exp(-1.0 * x)) - 1.0; 
 extern "C" DOUBLE ann_dact(DOUBLE y) { return -0.5 * (y * y - 1.0); }
 
 static inline int nthreads(void) { return _NN(return, omp_threads)(); }
+/* fork/join costs microseconds: small layers (the online loop runs up to 10^5
+ * iterations per sample) stay on one thread; per-row results are identical either way */
+static inline bool par(unsigned long work) { return work >= 16384UL; }
 
 /* y[N] = W[N x M] x[M] (+ optional activation) */
 static void gemv_rows(const layer_ann *l, const DOUBLE *x, DOUBLE *y, bool act) {
     const UINT N = l->n_neurons, M = l->n_inputs;
-#pragma omp parallel for num_threads(nthreads()) schedule(static)
+#pragma omp parallel for if (par((unsigned long)N * M)) num_threads(nthreads()) schedule(static)
     for (long j = 0; j < (long)N; j++) {
         const DOUBLE *w = l->weights + _2D_IDX(M, j, 0);
         DOUBLE s = 0.0;
@@ -96,7 +99,7 @@ static void compute_deltas(const kernel_ann *k, nn_type type, const DOUBLE *t, D
         const UINT N = up->n_neurons, M = up->n_inputs;
         const DOUBLE *dn = d[l + 1];
         const DOUBLE *h = k->hiddens[l].vec;
-#pragma omp parallel for num_threads(nthreads()) schedule(static)
+#pragma omp parallel for if (par((unsigned long)N * M)) num_threads(nthreads()) schedule(static)
         for (long m = 0; m < (long)M; m++) {
             DOUBLE s = 0.0;
             for (UINT n = 0; n < N; n++) s += up->weights[_2D_IDX(M, n, m)] * dn[n];
@@ -108,7 +111,7 @@ static void compute_deltas(const kernel_ann *k, nn_type type, const DOUBLE *t, D
 static void update_layer(layer_ann *l, const DOUBLE *d, const DOUBLE *h, DOUBLE lr, DOUBLE *dw,
                          DOUBLE alpha) {
     const UINT N = l->n_neurons, M = l->n_inputs;
-#pragma omp parallel for num_threads(nthreads()) schedule(static)
+#pragma omp parallel for if (par((unsigned long)N * M)) num_threads(nthreads()) schedule(static)
     for (long j = 0; j < (long)N; j++) {
         DOUBLE *w = l->weights + _2D_IDX(M, j, 0);
         if (dw) {
