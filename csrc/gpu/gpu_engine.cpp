@@ -15,8 +15,12 @@
  */
 #include <hip/hip_runtime_api.h>
 #include <libhpnn/ann.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <vector>
@@ -299,6 +303,7 @@ struct Batched {
         hipFree(midtmp);
         hipFree(G12);
         hipFree(W0f);
+        if (own_flat) hipFree(gflat);
     }
 
     /* sum the stat slots: returns (loss sum, hits) */
@@ -454,6 +459,83 @@ struct Batched {
         return TRUE;
     }
 
+    /* ---- data-parallel split of a step: gradients into one flat FP32 buffer (the
+     * all-reduce payload), then the update from it ---- */
+    float *gflat = nullptr; /* sum over this replica's samples, [layer 0 | layer 1 | ...] */
+    size_t goff[17] = {0};
+    BOOL alloc_flat(float *external = nullptr) {
+        goff[0] = 0;
+        for (int l = 0; l < L; l++) goff[l + 1] = goff[l] + (size_t)Np[l] * Kp[l];
+        if (external) {
+            gflat = external;
+            own_flat = false;
+            return TRUE;
+        }
+        HIPCHK(hipMalloc(&gflat, goff[L] * 4));
+        own_flat = true;
+        return TRUE;
+    }
+    bool own_flat = false;
+    size_t flat_count() const { return goff[L]; }
+
+    BOOL grads(const void *X, const float *T, int ldt, int n_valid) {
+        const float t_lo = type == 2 ? 0.f : -1.f;
+        int r = 0;
+        if (fused) {
+            const int slab_f = hpnn_mlp3_slab_floats();
+            if (fused_x) {
+                r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab,
+                                    acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, s);
+                r = r > 0 ? 0 : (r ? r : -1);
+            } else {
+                r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0],
+                                      HPNN_EPI_ACT, 0, s);
+                if (!r)
+                    r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab,
+                                      acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2],
+                                      mid_grid, s);
+            }
+            if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
+            if (!r) r = hpnn_reduce_slabs(slab[0], S[0], (long)Np[0] * Kp[0], (long)Np[0] * Kp[0], gflat, s);
+            /* [G1 | G2] slab rows are exactly layers 1, 2 of the flat buffer */
+            if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, slab_f, slab_f, midtmp, gflat + goff[1], s);
+            if (r) NN_ERROR(stderr, "fused gradients failed: %d\n", r);
+            return r == 0;
+        }
+        if (!forward(X)) return FALSE;
+        if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
+                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
+            return FALSE;
+        for (int l = L - 1; l >= 1; l--)
+            if (hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp, Np[l - 1],
+                                  Np[l], HPNN_EPI_DACT, 0, s))
+                return FALSE;
+        for (int l = 0; l < L; l++) {
+            const void *Hin = l ? H[l - 1] : X;
+            if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s)) return FALSE;
+            if (hpnn_reduce_slabs(slab[l], S[l], (long)Np[l] * Kp[l], (long)Np[l] * Kp[l], gflat + goff[l], s))
+                return FALSE;
+        }
+        return TRUE;
+    }
+
+    /* update every layer from a flat gradient buffer G (this replica's gflat after the
+     * all-reduce, or the loopback sum) with scale = 1 / (samples of all replicas) */
+    BOOL update_flat(const float *G, float lr, float alpha, float scale, bool mom) {
+        hpnn_upd_layer u[HPNN_UPD_MAX];
+        if (L > HPNN_UPD_MAX) {
+            for (int l = 0; l < L; l++)
+                if (hpnn_sgd_update(W32[l], V32[l], G + goff[l], 1, 0, Wb[l], Wt[l], Np[l], Kp[l], lr, alpha, scale,
+                                    mom ? 1 : 0, s))
+                    return FALSE;
+            return TRUE;
+        }
+        for (int l = 0; l < L; l++)
+            u[l] = {W32[l], V32[l], G + goff[l], 0, Wb[l], Wt[l], (l == 0 && fused_x) ? W0f : nullptr, 1, Np[l],
+                    Kp[l]};
+        return hpnn_sgd_update_multi(u, L, lr, alpha, scale, mom ? 1 : 0, s) == 0;
+    }
+
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
         for (int l = 0; l < L; l++) {
@@ -481,8 +563,76 @@ BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, 
 
 }  // namespace
 
+namespace {
+
+/* RCCL, resolved at run time: the Python side (torch) may already have its own
+ * librccl.so.1 loaded in the process; dlopen by soname then reuses that copy instead
+ * of dragging in a second one through a link-time dependency. */
+struct Rccl {
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+    decltype(&ncclCommGetAsyncError) async_err = nullptr;
+    bool ok = false;
+    bool load() {
+        if (ok) return true;
+        const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+        void *h = nullptr;
+        for (const char *n : names)
+            if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            NN_ERROR(stderr, "RCCL not found (%s)\n", dlerror());
+            return false;
+        }
+        init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
+        destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+        all_reduce = (decltype(all_reduce))dlsym(h, "ncclAllReduce");
+        group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
+        group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
+        err = (decltype(err))dlsym(h, "ncclGetErrorString");
+        async_err = (decltype(async_err))dlsym(h, "ncclCommGetAsyncError");
+        ok = init_all && destroy && all_reduce && group_start && group_end && err && async_err;
+        if (!ok) NN_ERROR(stderr, "RCCL: missing symbols\n");
+        return ok;
+    }
+};
+Rccl g_rccl;
+
+#define RCCLCHK(call)                                                                  \
+    do {                                                                               \
+        ncclResult_t _r = (call);                                                      \
+        if (_r != ncclSuccess) {                                                       \
+            NN_ERROR(stderr, "RCCL error %s at %s:%d\n", g_rccl.err(_r), __FILE__, __LINE__); \
+            return FALSE;                                                              \
+        }                                                                              \
+    } while (0)
+
+/* Data-parallel batched training driven by ONE process over G replicas (the reference's
+ * single-process multi-GPU design, libhpnn.c:201-305, with its hub copies replaced by an
+ * RCCL all-reduce over xGMI): every global minibatch of B samples is split into G shards
+ * of ceil(B/G); each replica computes the gradient sum of its shard into a flat FP32
+ * buffer; one grouped ncclAllReduce sums them; every replica applies the identical update
+ * with scale 1/(samples of the minibatch), so the weights stay replicated and the result
+ * equals the single-GPU step up to summation order.
+ * loopback: G virtual replicas on ONE device (CI without a multi-GPU node): the buffers
+ * live in one allocation and the all-reduce is a deterministic slab sum. */
+BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+              hpnn_batched_stats *st, int G, bool loopback);
+
+}  // namespace
+
 extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
                                        const hpnn_batched_opts *o, hpnn_batched_stats *st) {
+    {
+        const char *lb = getenv("HPNN_LOOPBACK_RANKS");
+        const int lbr = lb ? atoi(lb) : 0;
+        const char *fr = getenv("HPNN_FORCE_RCCL");
+        if (lbr >= 2) return train_dp(k, X, T, n, o, st, lbr, true);
+        if (o->n_gpu > 1 || (fr && fr[0] == '1')) return train_dp(k, X, T, n, o, st, (int)(o->n_gpu ? o->n_gpu : 1), false);
+    }
     if (o->dtype != NN_DTYPE_BF16) {
         NN_WARN(stderr, "GPU batched engine runs BF16 MFMA; requested dtype promoted to bf16\n");
     }
@@ -537,6 +687,176 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     if (k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
     return TRUE;
 }
+
+namespace {
+
+BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+              hpnn_batched_stats *st, int G, bool loopback) {
+    if (k->n_hiddens + 1 > 16 || G < 1) return FALSE;
+    if (!loopback && !g_rccl.load()) return FALSE;
+    hpnn_gpu_sync_host(k);
+    const int B = (int)(o->batch ? o->batch : 256);
+    const int Bg = (B + G - 1) / G;
+    const bool mom = o->train == NN_TRAIN_BPM;
+    const int n_out = (int)k->n_outputs;
+    std::vector<int> dev(G);
+    std::vector<hipStream_t> str(G);
+    std::vector<std::unique_ptr<Batched>> nets(G);
+    float *lb_flat = nullptr; /* loopback: [G][count] in one allocation */
+    std::vector<void *> Xd(G, nullptr);
+    std::vector<float *> Td(G, nullptr);
+    std::vector<ncclComm_t> comms(G, nullptr);
+    BOOL ok = TRUE;
+    const int n_batches = (int)((n + B - 1) / B);
+    auto cleanup = [&]() {
+        for (int g = 0; g < G; g++) {
+            hipSetDevice(dev[g]);
+            if (!loopback || g == 0) {
+                hipFree(Xd[g]);
+                hipFree(Td[g]);
+            }
+            nets[g].reset();
+            if (comms[g]) g_rccl.destroy(comms[g]);
+        }
+        if (lb_flat) hipFree(lb_flat);
+        hipSetDevice(hpnn_rt_device(0));
+    };
+    for (int g = 0; g < G; g++) {
+        dev[g] = loopback ? hpnn_rt_device(0) : hpnn_rt_device((UINT)g);
+        str[g] = loopback ? hpnn_rt_stream(0, 0) : hpnn_rt_stream((UINT)g, 0);
+        if (!str[g]) return FALSE;
+    }
+    /* replicas + data (rows padded so every shard of the last minibatch reads Bp rows) */
+    const int rows_p = n_batches * B + Bg + 128;
+    for (int g = 0; g < G && ok; g++) {
+        if (hipSetDevice(dev[g]) != hipSuccess) return FALSE;
+        nets[g].reset(new Batched());
+        ok = nets[g]->init(k, Bg, o->type, mom, str[g]);
+        if (!ok) break;
+        if (loopback) {
+            if (g == 0) {
+                size_t tot = 0;
+                for (int l = 0; l < nets[0]->L; l++) tot += (size_t)nets[0]->Np[l] * nets[0]->Kp[l];
+                if (hipMalloc(&lb_flat, tot * 4 * G) != hipSuccess) ok = FALSE;
+            }
+            if (ok) {
+                size_t tot = 0;
+                for (int l = 0; l < nets[g]->L; l++) tot += (size_t)nets[g]->Np[l] * nets[g]->Kp[l];
+                ok = nets[g]->alloc_flat(lb_flat + tot * g);
+            }
+        } else {
+            ok = nets[g]->alloc_flat();
+        }
+        if (!ok) break;
+        if (!loopback || g == 0) {
+            ok = upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, nets[g]->Kp[0], &Xd[g], str[g]);
+            if (ok) {
+                std::vector<float> tf((size_t)rows_p * n_out, 0.f);
+                for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (float)T[i];
+                ok = hipMalloc(&Td[g], tf.size() * 4) == hipSuccess &&
+                     hipMemcpy(Td[g], tf.data(), tf.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+            }
+        } else {
+            Xd[g] = Xd[0];
+            Td[g] = Td[0];
+        }
+    }
+    if (ok && !loopback) {
+        if (g_rccl.init_all(comms.data(), G, dev.data()) != ncclSuccess) {
+            NN_ERROR(stderr, "ncclCommInitAll(%d GPUs) failed\n", G);
+            ok = FALSE;
+        }
+    }
+    if (!ok) {
+        cleanup();
+        return FALSE;
+    }
+    const size_t count = nets[0]->flat_count();
+    NN_OUT(stdout, "data-parallel batched training: %d replicas (%s), %d samples per replica per step\n", G,
+           loopback ? "loopback on one GPU" : "RCCL all-reduce", Bg);
+    auto t0 = std::chrono::steady_clock::now();
+    double ep_loss = 0.0;
+    unsigned int ep_hits = 0;
+    for (UINT e = 0; e < o->epochs && ok; e++) {
+        for (int g = 0; g < G; g++) {
+            hipSetDevice(dev[g]);
+            hipMemsetAsync(nets[g]->acc, 0, Batched::ACC_BYTES, str[g]);
+        }
+        for (int b = 0; b < n_batches && ok; b++) {
+            const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
+            int total = 0;
+            for (int g = 0; g < G && ok; g++) {
+                const int start = b * B + g * Bg;
+                int nv = end - start;
+                nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
+                total += nv;
+                hipSetDevice(dev[g]);
+                const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * 2;
+                const float *tb = Td[g] + (size_t)start * n_out;
+                ok = nets[g]->grads(xb, tb, n_out, nv);
+            }
+            if (!ok) break;
+            if (loopback) {
+                /* virtual replicas share one stream: sum the G buffers into replica 0's */
+                ok = hpnn_reduce_slabs(lb_flat, G, (long)count, (long)count, lb_flat, str[0]) == 0;
+            } else {
+                ncclResult_t r = g_rccl.group_start();
+                for (int g = 0; g < G && r == ncclSuccess; g++)
+                    r = g_rccl.all_reduce(nets[g]->gflat, nets[g]->gflat, count, ncclFloat32, ncclSum, comms[g],
+                                          str[g]);
+                ncclResult_t r2 = g_rccl.group_end();
+                if (r != ncclSuccess || r2 != ncclSuccess) {
+                    NN_ERROR(stderr, "ncclAllReduce failed: %s\n", g_rccl.err(r != ncclSuccess ? r : r2));
+                    ok = FALSE;
+                }
+            }
+            const float scale = 1.0f / (float)(total > 0 ? total : 1);
+            for (int g = 0; g < G && ok; g++) {
+                hipSetDevice(dev[g]);
+                ok = nets[g]->update_flat(loopback ? lb_flat : nets[g]->gflat, (float)o->lr, (float)o->alpha, scale,
+                                          mom);
+            }
+        }
+        if (!ok) break;
+        ep_loss = 0.0;
+        ep_hits = 0;
+        for (int g = 0; g < G && ok; g++) {
+            hipSetDevice(dev[g]);
+            double l = 0.0;
+            unsigned int h = 0;
+            ok = nets[g]->read_stats(&l, &h);
+            ep_loss += l;
+            ep_hits += h;
+        }
+        if (!loopback && ok) {
+            /* surface asynchronous communicator failures (a peer died, link error) */
+            for (int g = 0; g < G; g++) {
+                ncclResult_t ar = ncclSuccess;
+                if (g_rccl.async_err(comms[g], &ar) != ncclSuccess || ar != ncclSuccess) {
+                    NN_ERROR(stderr, "RCCL async error on replica %d: %s\n", g, g_rccl.err(ar));
+                    ok = FALSE;
+                }
+            }
+        }
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (ok) {
+        hipSetDevice(dev[0]);
+        ok = nets[0]->download(k);
+    }
+    if (ok && st) {
+        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->samples = (UINT64)n * o->epochs;
+        st->epoch_loss = ep_loss / (double)n;
+        st->correct = ep_hits;
+        st->last_loss = st->epoch_loss;
+    }
+    cleanup();
+    if (ok && k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
+    return ok;
+}
+
+}  // namespace
 
 extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
                                        DOUBLE *Y) {

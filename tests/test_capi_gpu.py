@@ -12,8 +12,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bin")
 
 
-def _run(cmd, cwd, cpu=False):
+def _run(cmd, cwd, cpu=False, extra_env=None):
     env = dict(os.environ)
+    env.pop("HPNN_LOOPBACK_RANKS", None)
+    env.pop("HPNN_FORCE_RCCL", None)
+    env.update(extra_env or {})
     if cpu:
         env["HPNN_FORCE_CPU"] = "1"
     else:
@@ -75,3 +78,30 @@ def test_run_nn_gpu(tmp_path):
     out_g = _run([os.path.join(BIN, "run_nn"), "-vv", "nn.conf"], d)
     out_c = _run([os.path.join(BIN, "run_nn"), "-vv", "nn.conf"], d, cpu=True)
     assert out_g.count("[PASS]") == out_c.count("[PASS]")
+
+
+@pytest.mark.parametrize("shape", ["fused", "generic"])
+@pytest.mark.parametrize("dp_env", [{"HPNN_LOOPBACK_RANKS": "2"}, {"HPNN_LOOPBACK_RANKS": "3"},
+                                    {"HPNN_FORCE_RCCL": "1"}])
+def test_batched_data_parallel_matches_single(tmp_path, shape, dp_env):
+    """native data-parallel path (csrc/gpu/gpu_engine.cpp train_dp): replicas each take a
+    shard of every minibatch, gradients are summed (loopback: virtual replicas on one GPU;
+    HPNN_FORCE_RCCL: a real 1-GPU RCCL communicator) -> same training as one replica."""
+    if shape == "fused":
+        dims = dict(inputs=784, hiddens=[128, 64], outputs=10, type="SNN")
+    else:
+        dims = dict(inputs=100, hiddens=[48], outputs=7, type="ANN")
+    res = {}
+    for tag, env in (("single", {}), ("dp", dp_env)):
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 333, dims["inputs"], dims["outputs"], dims["type"] == "SNN")
+        formats.write_conf(os.path.join(d, "nn.conf"), name="m", seed=9, train="BPM", sample_dir="./samples",
+                           test_dir="./samples", mode="batched", batch=256, epochs=2, lr=0.05, **dims)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, extra_env=env)
+        assert ("data-parallel batched training" in out) == (tag == "dp"), out[-2000:]
+        res[tag] = (formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"],
+                    formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"])
+    for (w0, ws, wd) in zip(res["single"][0], res["single"][1], res["dp"][1]):
+        ds, dd = ws - w0, wd - w0
+        rel = np.linalg.norm(ds - dd) / (np.linalg.norm(ds) + 1e-30)
+        assert rel < 0.03, rel
