@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
   return 0
 }
 if [ "$what" = tests ] || [ "$what" = all ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${@:2}
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${@:2}
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$what" = bench ] || [ "$what" = all ]; then
