@@ -65,7 +65,8 @@ def main():
     def step(i):
         dp.train_step(Xs[i % args.datasets], labels=Ls[i % args.datasets], lr=args.lr, alpha=args.alpha)
 
-    use_graph = args.graph and world == 1
+    # DP steps run eagerly (RCCL calls from Python); --graph 2 also captures them
+    use_graph = (args.graph and not dp.active) or args.graph == 2
     gsteps = max(1, args.graph_steps)
     graphs = {}
 

@@ -16,7 +16,7 @@
 #include <hip/hip_runtime_api.h>
 #include <libhpnn/ann.h>
 #include <dlfcn.h>
-#include <rccl/rccl.h>
+#include <libhpnn/comm.h>
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
@@ -251,9 +251,10 @@ namespace {
 inline int pad32(int v) { return (v + 31) / 32 * 32; }
 inline int pad128(int v) { return (v + 127) / 128 * 128; }
 
-/* split-K factor for the weight-gradient GEMM: ~512 workgroups, >= 1024 rows per
- * split (fewer slabs keep the optimizer's slab reduction cheap). Mirrors
- * hpnn_amd/models/mlp.py:MLP.pick_splits. */
+/* split-K factor of the weight-gradient GEMM: about one workgroup per CU (256 on
+ * MI355X; 48 splits measured fastest for MNIST's G0) so every CU streams the same share (gemm_tn takes uneven 64-row units per
+ * split), >= 512 batch rows per split, a multiple of 8 for the XCD-aware block order.
+ * Mirrors hpnn_amd/models/mlp.py:MLP._pick_splits (HPNN_TN_SPLITS forces a value). */
 int tn_tile_m(int K) {
     return K % 128 == 0 ? 128 : (K % 160 == 0 ? 160 : (K % 96 == 0 ? 96 : (K % 64 == 0 ? 64 : 32)));
 }
@@ -261,13 +262,16 @@ int pick_splits(int Np, int Kp, int Bp) {
     const int tn = (Np % 128 == 0) ? 128 : (Np % 64 == 0 ? 64 : 32);
     const int tm = tn_tile_m(Kp);
     const int tiles = (Np / tn) * (Kp / tm);
-    int s = (512 + tiles - 1) / (tiles > 0 ? tiles : 1);
-    int maxs = Bp / 1024;
-    if (maxs < 1) maxs = 1;
+    static const int forced = [] { const char *e = getenv("HPNN_TN_SPLITS"); return e ? atoi(e) : 0; }();
+    if (forced > 0) {
+        const int m = Bp / 64;
+        return forced < m ? forced : (m > 0 ? m : 1);
+    }
+    int s = (256 + tiles / 2) / (tiles > 0 ? tiles : 1);
+    const int maxs = Bp / 512;
     if (s > maxs) s = maxs;
-    if (s < 1) s = 1;
-    while (s > 1 && (Bp % (64 * s))) s--;
-    return s;
+    if (s >= 8) s -= s % 8;
+    return s < 1 ? 1 : s;
 }
 
 struct Batched {
@@ -286,8 +290,15 @@ struct Batched {
     float *midslab = nullptr, *midtmp = nullptr, *G12 = nullptr;
     void *W0f = nullptr; /* fragment-major BF16 W0 (fused_x) */
     hipStream_t s = nullptr;
+    /* fused_x: the [G1|G2] reduction pass forks onto `side` next to the G0 GEMM */
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
     ~Batched() {
+        if (s) hipStreamSynchronize(s);
+        if (side) hipStreamDestroy(side);
+        if (ev_fork) hipEventDestroy(ev_fork);
+        if (ev_join) hipEventDestroy(ev_join);
         for (int l = 0; l < 16; l++) {
             hipFree(W32[l]);
             hipFree(V32[l]);
@@ -370,6 +381,9 @@ struct Batched {
             HIPCHK(hipMalloc(&midtmp, (size_t)16 * slab_f * 4));
             HIPCHK(hipMalloc(&G12, (size_t)slab_f * 4));
             if (fused_x) {
+                HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+                HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
                 HIPCHK(hipMalloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
                 hpnn_upd_layer c0 = {W32[0], nullptr, W32[0], 0, Wb[0], Wt[0], W0f, 1, Np[0], Kp[0]};
                 if (hpnn_sgd_update_multi(&c0, 1, 0.f, 0.f, 0.f, 0, s)) return FALSE; /* lr 0: a cast */
@@ -409,9 +423,15 @@ struct Batched {
                                   (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid,
                                   s);
         }
+        /* first reduction pass of the [G1 | G2] block slabs (the optimizer sums the groups)
+         * on the side stream, concurrently with the G0 GEMM */
+        hipStream_t rs = s;
+        if (!r && side && hipEventRecord(ev_fork, s) == hipSuccess && hipStreamWaitEvent(side, ev_fork, 0) == hipSuccess)
+            rs = side;
+        if (!r) r = hpnn_reduce_groups(midslab, mid_grid, slab_f, slab_f, mid_groups, midtmp, rs);
         if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
-        /* first reduction pass of the [G1 | G2] block slabs; the optimizer sums the groups */
-        if (!r) r = hpnn_reduce_groups(midslab, mid_grid, slab_f, slab_f, mid_groups, midtmp, s);
+        if (rs != s && (hipEventRecord(ev_join, rs) != hipSuccess || hipStreamWaitEvent(s, ev_join, 0) != hipSuccess))
+            r = r ? r : -9;
         if (!r) {
             const long n1 = (long)Np[1] * Kp[1];
             hpnn_upd_layer u[3] = {
@@ -565,51 +585,6 @@ BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, 
 
 namespace {
 
-/* RCCL, resolved at run time: the Python side (torch) may already have its own
- * librccl.so.1 loaded in the process; dlopen by soname then reuses that copy instead
- * of dragging in a second one through a link-time dependency. */
-struct Rccl {
-    decltype(&ncclCommInitAll) init_all = nullptr;
-    decltype(&ncclCommDestroy) destroy = nullptr;
-    decltype(&ncclAllReduce) all_reduce = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclGetErrorString) err = nullptr;
-    decltype(&ncclCommGetAsyncError) async_err = nullptr;
-    bool ok = false;
-    bool load() {
-        if (ok) return true;
-        const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
-        void *h = nullptr;
-        for (const char *n : names)
-            if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
-        if (!h) {
-            NN_ERROR(stderr, "RCCL not found (%s)\n", dlerror());
-            return false;
-        }
-        init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
-        destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
-        all_reduce = (decltype(all_reduce))dlsym(h, "ncclAllReduce");
-        group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
-        group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
-        err = (decltype(err))dlsym(h, "ncclGetErrorString");
-        async_err = (decltype(async_err))dlsym(h, "ncclCommGetAsyncError");
-        ok = init_all && destroy && all_reduce && group_start && group_end && err && async_err;
-        if (!ok) NN_ERROR(stderr, "RCCL: missing symbols\n");
-        return ok;
-    }
-};
-Rccl g_rccl;
-
-#define RCCLCHK(call)                                                                  \
-    do {                                                                               \
-        ncclResult_t _r = (call);                                                      \
-        if (_r != ncclSuccess) {                                                       \
-            NN_ERROR(stderr, "RCCL error %s at %s:%d\n", g_rccl.err(_r), __FILE__, __LINE__); \
-            return FALSE;                                                              \
-        }                                                                              \
-    } while (0)
-
 /* Data-parallel batched training driven by ONE process over G replicas (the reference's
  * single-process multi-GPU design, libhpnn.c:201-305, with its hub copies replaced by an
  * RCCL all-reduce over xGMI): every global minibatch of B samples is split into G shards
@@ -693,7 +668,7 @@ namespace {
 BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
               hpnn_batched_stats *st, int G, bool loopback) {
     if (k->n_hiddens + 1 > 16 || G < 1) return FALSE;
-    if (!loopback && !g_rccl.load()) return FALSE;
+    if (!loopback && !hpnn_comm_available()) return FALSE;
     hpnn_gpu_sync_host(k);
     const int B = (int)(o->batch ? o->batch : 256);
     const int Bg = (B + G - 1) / G;
@@ -705,7 +680,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     float *lb_flat = nullptr; /* loopback: [G][count] in one allocation */
     std::vector<void *> Xd(G, nullptr);
     std::vector<float *> Td(G, nullptr);
-    std::vector<ncclComm_t> comms(G, nullptr);
+    std::vector<hpnn_comm *> comms(G, nullptr);
     BOOL ok = TRUE;
     const int n_batches = (int)((n + B - 1) / B);
     auto cleanup = [&]() {
@@ -716,7 +691,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                 hipFree(Td[g]);
             }
             nets[g].reset();
-            if (comms[g]) g_rccl.destroy(comms[g]);
+            if (comms[g]) hpnn_comm_destroy(comms[g]);
         }
         if (lb_flat) hipFree(lb_flat);
         hipSetDevice(hpnn_rt_device(0));
@@ -762,10 +737,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         }
     }
     if (ok && !loopback) {
-        if (g_rccl.init_all(comms.data(), G, dev.data()) != ncclSuccess) {
-            NN_ERROR(stderr, "ncclCommInitAll(%d GPUs) failed\n", G);
-            ok = FALSE;
-        }
+        if (hpnn_comm_init_all(comms.data(), G, dev.data()) != 0) ok = FALSE;
     }
     if (!ok) {
         cleanup();
@@ -800,13 +772,15 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                 /* virtual replicas share one stream: sum the G buffers into replica 0's */
                 ok = hpnn_reduce_slabs(lb_flat, G, (long)count, (long)count, lb_flat, str[0]) == 0;
             } else {
-                ncclResult_t r = g_rccl.group_start();
-                for (int g = 0; g < G && r == ncclSuccess; g++)
-                    r = g_rccl.all_reduce(nets[g]->gflat, nets[g]->gflat, count, ncclFloat32, ncclSum, comms[g],
-                                          str[g]);
-                ncclResult_t r2 = g_rccl.group_end();
-                if (r != ncclSuccess || r2 != ncclSuccess) {
-                    NN_ERROR(stderr, "ncclAllReduce failed: %s\n", g_rccl.err(r != ncclSuccess ? r : r2));
+                /* one grouped launch: the per-device calls of a single-process communicator
+                 * clique must not block each other */
+                int r = hpnn_comm_group_start();
+                for (int g = 0; g < G && r == 0; g++)
+                    r = hpnn_comm_all_reduce(comms[g], nets[g]->gflat, nets[g]->gflat, (long)count, HPNN_DT_F32,
+                                             HPNN_OP_SUM, str[g]);
+                const int r2 = hpnn_comm_group_end();
+                if (r || r2) {
+                    NN_ERROR(stderr, "gradient all-reduce failed (%d)\n", r ? r : r2);
                     ok = FALSE;
                 }
             }
@@ -830,13 +804,8 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         }
         if (!loopback && ok) {
             /* surface asynchronous communicator failures (a peer died, link error) */
-            for (int g = 0; g < G; g++) {
-                ncclResult_t ar = ncclSuccess;
-                if (g_rccl.async_err(comms[g], &ar) != ncclSuccess || ar != ncclSuccess) {
-                    NN_ERROR(stderr, "RCCL async error on replica %d: %s\n", g, g_rccl.err(ar));
-                    ok = FALSE;
-                }
-            }
+            for (int g = 0; g < G; g++)
+                if (hpnn_comm_check(comms[g]) != 0) ok = FALSE;
         }
     }
     auto t1 = std::chrono::steady_clock::now();

@@ -46,7 +46,8 @@ int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C
                          int epi, int c_f32, hipStream_t stream);
 
 /* slab[s][N x M] = sum_{b in slice s} D[b][n] H[b][m] (FP32 out).
- * D: [Bt x N] BF16, H: [Bt x M] BF16. Bt % (64*splits) == 0, N,M % 32 == 0.
+ * D: [Bt x N] BF16, H: [Bt x M] BF16. Bt % 64 == 0, 1 <= splits <= Bt/64, N,M % 32 == 0.
+ * Slice s = rows [64*floor(s*U/S), 64*floor((s+1)*U/S)), U = Bt/64 (uneven splits allowed).
  * ldg: row stride of a slab row (>= M); slab stride = N*ldg. */
 int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N,
                       int M, int Bt, int splits, hipStream_t stream);

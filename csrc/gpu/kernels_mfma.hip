@@ -220,8 +220,8 @@ __device__ __forceinline__ bf16x8 tnp_frag(const char *tile, int kbase, int c0, 
 template <int TM, int TN, int BKR, int STAGES>
 __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
                                                            const __bf16 *__restrict__ H, int ldh,
-                                                           float *__restrict__ slab, int ldg, int N, int chunk,
-                                                           int tiles_n, int tiles, int xcd_map) {
+                                                           float *__restrict__ slab, int ldg, int N, int units,
+                                                           int splits, int tiles_n, int tiles, int xcd_map) {
     constexpr int WTM = TM / 2, WTN = TN / 2;
     constexpr int FM = WTM / 16, FN = WTN / 16;
     constexpr int H_PIECES = (TM / 32) * (BKR / 16), D_PIECES = (TN / 32) * (BKR / 16);
@@ -247,8 +247,12 @@ __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restr
     }
     const int tn = tile % tiles_n, tm = tile / tiles_n;
     const int m0 = tm * TM, n0 = tn * TN;
-    const int b0 = split * chunk;
-    const int KT = chunk / BKR;
+    /* uneven splits: split s covers the 64-row units [s*U/S, (s+1)*U/S) of the batch, so
+     * any split count gives every workgroup the same share to within one unit and the
+     * grid can be sized to fill the CUs evenly (2 workgroups per CU) */
+    const int u0 = (int)((long)split * units / splits), u1 = (int)((long)(split + 1) * units / splits);
+    const int b0 = u0 * 64;
+    const int KT = (u1 - u0) * (64 / BKR);
     const size_t ldh_b = (size_t)ldh * 2, ldd_b = (size_t)ldd * 2;
     const char *Hg = (const char *)(H + (size_t)b0 * ldh + m0);
     const char *Dg = (const char *)(D + (size_t)b0 * ldd + n0);
@@ -342,16 +346,16 @@ template <int TM, int TN>
 int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s) {
     const int tiles_n = N / TN, tiles_m = M / TM;
-    const int chunk = Bt / splits;
+    const int units = Bt / 64;
     /* 32-row stages, ring of ~72 KiB (2 workgroups per CU) */
     constexpr int BKR = 32;
     constexpr int STAGE = BKR * (TM + TN) * 2;
     constexpr int ST = (73728 / STAGE) < 2 ? 2 : ((73728 / STAGE) > 6 ? 6 : (73728 / STAGE));
-    if (chunk % BKR) return -2;
     const int tiles = tiles_m * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
     hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits), dim3(256), 0, s,
-                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, chunk, tiles_n, tiles, xcd_map);
+                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, tiles,
+                       xcd_map);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -389,7 +393,7 @@ extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb,
 extern "C" int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M,
                                  int Bt, int splits, hipStream_t stream) {
     if (N <= 0 || M <= 0 || Bt <= 0 || splits <= 0) return -1;
-    if (N % 32 || M % 32 || Bt % (64 * splits)) return -2;
+    if (N % 32 || M % 32 || Bt % 64 || splits > Bt / 64) return -2;
     if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
     if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
     if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);

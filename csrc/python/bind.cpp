@@ -16,6 +16,7 @@
 #include <pybind11/stl.h>
 
 #include "../gpu/kernels.h"
+#include <libhpnn/comm.h>
 
 namespace py = pybind11;
 using uptr = uintptr_t;
@@ -132,6 +133,55 @@ PYBIND11_MODULE(_native, m) {
             check(hpnn_sgd_update_multi(L, n, lr, alpha, scale, momentum, S(stream)), "sgd_update_multi");
         },
         "layers: [(W32, V32, G, gstride, Wbf, Wt, Wf, S, N, K)] device addresses (0 = none)");
+    /* ---- communication layer (include/libhpnn/comm.h) ---- */
+    m.def("comm_available", []() { return hpnn_comm_available(); });
+    m.def("comm_unique_id", []() {
+        unsigned char id[HPNN_COMM_ID_BYTES];
+        check(hpnn_comm_unique_id(id), "comm_unique_id");
+        return py::bytes((const char *)id, HPNN_COMM_ID_BYTES);
+    });
+    m.def(
+        "comm_init_rank",
+        [](py::bytes id, int nranks, int rank, int device) {
+            const std::string s = id;
+            if (s.size() != HPNN_COMM_ID_BYTES) throw std::runtime_error("comm id must be 128 bytes");
+            py::gil_scoped_release nogil; /* collective: blocks until every rank joined */
+            return (uptr)hpnn_comm_init_rank((const unsigned char *)s.data(), nranks, rank, device);
+        },
+        "RCCL communicator of this process' device (0 on failure)");
+    m.def("comm_destroy", [](uptr c) { hpnn_comm_destroy((hpnn_comm *)c); });
+    m.def("comm_rank", [](uptr c) { return hpnn_comm_rank((const hpnn_comm *)c); });
+    m.def("comm_size", [](uptr c) { return hpnn_comm_size((const hpnn_comm *)c); });
+    m.def("comm_all_reduce", [](uptr c, uptr send, uptr recv, long count, int dt, int op, uptr stream) {
+        check(hpnn_comm_all_reduce((hpnn_comm *)c, P(send), P(recv), count, (hpnn_comm_dtype)dt, (hpnn_comm_op)op,
+                                   S(stream)),
+              "comm_all_reduce");
+    });
+    m.def("comm_broadcast", [](uptr c, uptr send, uptr recv, long count, int dt, int root, uptr stream) {
+        check(hpnn_comm_broadcast((hpnn_comm *)c, P(send), P(recv), count, (hpnn_comm_dtype)dt, root, S(stream)),
+              "comm_broadcast");
+    });
+    m.def("comm_all_gather", [](uptr c, uptr send, uptr recv, long count, int dt, uptr stream) {
+        check(hpnn_comm_all_gather((hpnn_comm *)c, P(send), P(recv), count, (hpnn_comm_dtype)dt, S(stream)),
+              "comm_all_gather");
+    });
+    m.def("comm_reduce_scatter", [](uptr c, uptr send, uptr recv, long count, int dt, int op, uptr stream) {
+        check(hpnn_comm_reduce_scatter((hpnn_comm *)c, P(send), P(recv), count, (hpnn_comm_dtype)dt,
+                                       (hpnn_comm_op)op, S(stream)),
+              "comm_reduce_scatter");
+    });
+    m.def("comm_all_reduce_async", [](uptr c, uptr buf, long count, int dt, uptr stream) {
+        check(hpnn_comm_all_reduce_async((hpnn_comm *)c, P(buf), count, (hpnn_comm_dtype)dt, S(stream)),
+              "comm_all_reduce_async");
+    });
+    m.def("comm_join", [](uptr c, uptr stream) { check(hpnn_comm_join((hpnn_comm *)c, S(stream)), "comm_join"); });
+    m.def("comm_check", [](uptr c) { return hpnn_comm_check((hpnn_comm *)c); });
+    m.def("comm_abort", [](uptr c) { hpnn_comm_abort((hpnn_comm *)c); });
+    m.def("comm_all_ok", [](uptr c, int ok, uptr stream) {
+        py::gil_scoped_release nogil;
+        return hpnn_comm_all_ok((hpnn_comm *)c, ok, S(stream));
+    });
+    m.def("fault_hit", [](const std::string &site) { return hpnn_fault_hit(site.c_str()); });
     m.def("device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

@@ -22,6 +22,11 @@ import torch
 
 from .. import ops
 
+# HPNN_SIDE_REDUCE=1: run the first [G1|G2] reduction pass on a second stream next to the
+# G0 GEMM (fused path); off by default (cross-stream fork/join inside the graph measured
+# slower than back-to-back launches on MI355X)
+_SIDE_REDUCE = os.environ.get("HPNN_SIDE_REDUCE", "0") == "1"
+
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
 
@@ -132,16 +137,29 @@ class MLP:
     # ------------------------------------------------------------------ helpers
     @staticmethod
     def _pick_splits(N, K, Bp):
-        """split-K factor of the weight-gradient GEMM (mirrors csrc/gpu/gpu_engine.cpp)."""
+        """split-K factor of the weight-gradient GEMM (mirrors csrc/gpu/gpu_engine.cpp
+        pick_splits): about one workgroup per CU (256 on MI355X; measured 76.1 us/step
+        at 48 splits vs 79.7 us at 64 and 78.9 us at 96 for MNIST) so that every CU
+        streams the same share -- the kernel accepts uneven splits --, at least 512 batch
+        rows per split, and a multiple of 8 for the XCD-aware block order.
+        HPNN_TN_SPLITS forces a value (tuning)."""
         tn = 128 if N % 128 == 0 else (64 if N % 64 == 0 else 32)
         tm = next(t for t in (128, 160, 96, 64, 32) if K % t == 0)
         tiles = (N // tn) * (K // tm)
-        rows = int(os.environ.get("HPNN_TN_ROWS", "1024"))  # minimum batch rows per split
-        s = -(-512 // max(tiles, 1))
-        s = max(1, min(s, max(1, Bp // rows)))
-        while s > 1 and Bp % (64 * s):
-            s -= 1
-        return s
+        forced = int(os.environ.get("HPNN_TN_SPLITS", "0"))
+        if forced > 0:
+            return max(1, min(forced, Bp // 64)) if Bp % 64 == 0 else 1
+        rows = int(os.environ.get("HPNN_TN_ROWS", "512"))
+        s = (256 + tiles // 2) // max(tiles, 1)
+        s = min(s, Bp // rows)
+        if s >= 8:
+            s -= s % 8
+        return max(1, s)
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def refresh_bf16(self):
         for l in range(self.L):
@@ -251,11 +269,23 @@ class MLP:
         n_valid = self.Bp if n_valid is None else n_valid
         scale = 1.0 / n_valid
         if self.fused_mode == "x":
-            # 4 launches: fused front, G0 GEMM, first [G1|G2] reduction pass, all updates
+            # 4 launches: fused front, then the G0 GEMM and the first [G1|G2] reduction pass
+            # side by side (the reduction forks onto a second stream: it only needs the
+            # fused front's block slabs and fills CUs the memory-bound GEMM leaves idle),
+            # then every layer's update
             self._fused_front(X, labels, T, n_valid)
-            ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
-            ops.reduce_groups(self.midslab, self.mid_groups,
-                              self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB))
+            groups = self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB)
+            if self.device.type == "cuda" and _SIDE_REDUCE:
+                main = torch.cuda.current_stream(self.device)
+                side = self._side_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    ops.reduce_groups(self.midslab, self.mid_groups, groups)
+                ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
+                main.wait_stream(side)
+            else:
+                ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
+                ops.reduce_groups(self.midslab, self.mid_groups, groups)
             g1, g2 = self._mid_group_views()
             self.update_all(lr, alpha, scale, [self.slab[0], g1, g2])
             return

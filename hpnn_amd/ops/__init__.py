@@ -50,6 +50,16 @@ def gemm_nt(A, B, epi=EPI_NONE, aux=None, out_f32=False, out=None):
     return out
 
 
+def split_rows(Bt, splits):
+    """batch rows of each split-K slice of gemm_tn: 64-row units, uneven when S does not
+    divide them (csrc/gpu/kernels.h)"""
+    if Bt % 64 == 0:
+        U = Bt // 64
+        return [(s * U // splits * 64, (s + 1) * U // splits * 64) for s in range(splits)]
+    c = Bt // splits  # CPU emulation of tiny batches only
+    return [(s * c, (s + 1) * c) for s in range(splits)]
+
+
 def gemm_tn(D, H, splits=1, out=None):
     """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m]  (FP32)."""
     Bt, N = D.shape
@@ -57,9 +67,8 @@ def gemm_tn(D, H, splits=1, out=None):
     if out is None:
         out = torch.empty(splits, N, M, dtype=torch.float32, device=D.device)
     if _cpu(D):
-        c = Bt // splits
-        for s_ in range(splits):
-            out[s_].copy_(ref_gemm_tn(D[s_ * c:(s_ + 1) * c], H[s_ * c:(s_ + 1) * c]))
+        for s_, (a, b) in enumerate(split_rows(Bt, splits)):
+            out[s_].copy_(ref_gemm_tn(D[a:b], H[a:b]))
         return out
     native().gemm_tn_bf16(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), out.data_ptr(), out.stride(1), N, M,
                           Bt, splits, _stream())
@@ -102,6 +111,7 @@ def reduce_slabs2(slab, out, tmp=None):
     return out
 
 
+UPD_MAX = 8  # HPNN_UPD_MAX (csrc/gpu/kernels.h): layers per sgd_update_multi launch
 MLP3_DIMS = (128, 64, 32)
 
 

@@ -1,0 +1,112 @@
+"""Native RCCL communicator for the data-parallel hot path (libhpnn comm layer).
+
+torch.distributed (backend "nccl" = RCCL on ROCm) owns the process group: rendezvous,
+rank / world size, barriers and the one-time bootstrap.  The per-step gradient
+all-reduce goes through libhpnn's own RCCL communicator instead
+(include/libhpnn/comm.h, csrc/dist/comm.cpp): one C call per bucket, issued on a
+high-priority side stream that forks from the compute stream with a hipEvent and joins
+back before the update.  Measured on one MI355X (single-rank group, MNIST step of
+84 us): the same bucketed step through ProcessGroupNCCL ran at 144 us per step, its
+per-collective host bookkeeping being of the order of a whole training step; the
+native path keeps the host cost of a step at a few microseconds and is capturable in
+a HIP graph.
+
+The reference's equivalent is MPI_Allreduce / MPI_Allgather inline in every compute
+function (src/ann.c, e.g. ann.c:1263, 1638).
+"""
+import torch
+import torch.distributed as dist
+
+from .._lib import native
+
+DT_F32, DT_F64, DT_BF16, DT_I32, DT_U8 = 0, 1, 2, 3, 4
+OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
+ID_BYTES = 128
+
+_DT = {torch.float32: DT_F32, torch.float64: DT_F64, torch.bfloat16: DT_BF16, torch.int32: DT_I32,
+       torch.uint8: DT_U8}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class NativeComm:
+    """One libhpnn RCCL communicator per process (this process' current GPU).
+
+    Bootstrap: rank 0 of `group` creates the RCCL unique id, torch.distributed
+    broadcasts it, every rank calls ncclCommInitRank through libhpnn."""
+
+    def __init__(self, group=None, device=None):
+        if not dist.is_initialized():
+            raise RuntimeError("NativeComm needs an initialised torch.distributed process group")
+        n = native()
+        self.h = 0
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        uid = torch.zeros(ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            uid = torch.tensor(list(n.comm_unique_id()), dtype=torch.uint8)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if dist.get_backend(group) == "nccl":
+            t = uid.to(torch.device("cuda", self.device))
+            dist.broadcast(t, src, group=group)
+            uid = t.cpu()
+        else:
+            dist.broadcast(uid, src, group=group)
+        self.h = n.comm_init_rank(bytes(uid.tolist()), self.world, self.rank, self.device)
+        if not self.h:
+            raise RuntimeError("ncclCommInitRank failed (see stderr)")
+
+    # -- collectives on the current stream ------------------------------------------
+    def all_reduce(self, t, op=OP_SUM):
+        native().comm_all_reduce(self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], op, _stream())
+        return t
+
+    def broadcast(self, t, root=0):
+        native().comm_broadcast(self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], root, _stream())
+        return t
+
+    def all_gather(self, out, inp):
+        """out: world * inp.numel() elements, rank r's block at r * inp.numel()"""
+        native().comm_all_gather(self.h, inp.data_ptr(), out.data_ptr(), inp.numel(), _DT[inp.dtype], _stream())
+        return out
+
+    def reduce_scatter(self, out, inp, op=OP_SUM):
+        native().comm_reduce_scatter(self.h, inp.data_ptr(), out.data_ptr(), out.numel(), _DT[inp.dtype], op,
+                                     _stream())
+        return out
+
+    # -- overlapped gradient buckets ------------------------------------------------
+    def all_reduce_async(self, t):
+        """sum all-reduce of t on the side stream, after the work already on the current
+        stream; overlaps whatever is enqueued next until join()"""
+        native().comm_all_reduce_async(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], _stream())
+
+    def join(self):
+        native().comm_join(self.h, _stream())
+
+    # -- failure detection ----------------------------------------------------------
+    def check(self):
+        """raise if the communicator saw an asynchronous error (peer died, link down)"""
+        if native().comm_check(self.h) != 0:
+            native().comm_abort(self.h)
+            raise RuntimeError(f"RCCL communicator failed on rank {self.rank}")
+
+    def all_ok(self, ok=True):
+        """MIN over ranks of ok (the collective replacement of the reference's MPI
+        bail-out after a failed kernel load, ann.c:237-249)"""
+        return bool(native().comm_all_ok(self.h, 1 if ok else 0, _stream()))
+
+    def close(self):
+        if self.h:
+            native().comm_destroy(self.h)
+            self.h = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -20,11 +20,20 @@ from .. import ops
 
 
 class DataParallel:
-    def __init__(self, model, group=None, bucket_bytes=256 * 1024):
+    """comm: "auto" (libhpnn's native RCCL communicator when the model is on a GPU and the
+    group runs on the nccl backend, else torch.distributed), "native" or "torch"."""
+
+    def __init__(self, model, group=None, bucket_bytes=256 * 1024, comm="auto"):
         self.m = model
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.active else 1
         self.buckets = self._plan(bucket_bytes)
+        self.native = None
+        on_gpu = getattr(model, "device", torch.device("cpu")).type == "cuda"
+        if self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
+            from .comm import NativeComm
+            self.native = NativeComm(group, device=model.device.index)
 
     def _plan(self, bucket_bytes):
         """Group layers (descending = production order) into contiguous buckets."""
@@ -33,7 +42,10 @@ class DataParallel:
         for l in range(m.L - 1, -1, -1):
             cur.append(l)
             cur_bytes += m.G[l].numel() * 4
-            if cur_bytes >= bucket_bytes or l == 0:
+            # the fused path produces [G1 | G2] long before G0 (whose GEMM is the last
+            # backward kernel): close the bucket there so its all-reduce overlaps that GEMM
+            fused_cut = getattr(m, "fused", False) and l == 1
+            if cur_bytes >= bucket_bytes or l == 0 or fused_cut:
                 buckets.append(cur)
                 cur, cur_bytes = [], 0
         return buckets
@@ -44,10 +56,30 @@ class DataParallel:
         if self.world == 1:
             return
         for l in range(self.m.L):
-            dist.broadcast(self.m.W32[l], src, group=self.group)
-            if self.m.V32[l] is not None:
-                dist.broadcast(self.m.V32[l], src, group=self.group)
+            for t in (self.m.W32[l], self.m.V32[l]):
+                if t is None:
+                    continue
+                if self.native is not None:
+                    self.native.broadcast(t, root=dist.get_group_rank(self.group, src) if self.group else src)
+                else:
+                    dist.broadcast(t, src, group=self.group)
         self.m.refresh_bf16()
+
+    def check(self):
+        """failure detection: raise if the communicator reported an asynchronous error"""
+        if self.native is not None:
+            self.native.check()
+
+    def all_ok(self, ok=True):
+        """every rank agrees on a status (replaces the reference's MPI bail-out)"""
+        if not self.active:
+            return bool(ok)
+        if self.native is not None:
+            return self.native.all_ok(ok)
+        dev = self.m.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
 
     def _bucket_view(self, layers):
         lo, hi = min(layers), max(layers)
@@ -59,7 +91,7 @@ class DataParallel:
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         m = self.m
         n_valid = m.Bp if n_valid is None else n_valid
-        if self.world == 1:
+        if not self.active:
             return m.train_step(X, labels=labels, T=T, n_valid=n_valid, lr=lr, alpha=alpha)
         works = []
         done = set()
@@ -68,14 +100,22 @@ class DataParallel:
             done.add(l)
             for b in self.buckets:
                 if b[-1] == l and all(x in done for x in b):
-                    works.append(dist.all_reduce(self._bucket_view(b), group=self.group, async_op=True))
+                    if self.native is not None:
+                        self.native.all_reduce_async(self._bucket_view(b))
+                    else:
+                        works.append(dist.all_reduce(self._bucket_view(b), group=self.group, async_op=True))
 
         m.backward_grads(X, labels=labels, T=T, n_valid=n_valid, reduce=True, on_ready=ready)
         scale = 1.0 / (n_valid * self.world)
+        if self.native is not None:
+            self.native.join()
         for w in works:
             w.wait()
-        for l in range(m.L):
-            m.update_layer(l, lr, alpha, scale, from_G=True)
+        if m.L <= ops.UPD_MAX:
+            m.update_all(lr, alpha, scale, m.G)  # one launch for every layer
+        else:
+            for l in range(m.L):
+                m.update_layer(l, lr, alpha, scale, from_G=True)
 
 
 def init_from_env(backend=None):
@@ -85,7 +125,10 @@ def init_from_env(backend=None):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1 and not dist.is_initialized():
+    # HPNN_DP_FORCE=1: build the process group even for one rank, so the bucketed
+    # all-reduce path (RCCL on a GPU) can be exercised on a single-GPU box
+    force = os.environ.get("HPNN_DP_FORCE", "0") == "1" and "MASTER_ADDR" in os.environ
+    if (ws > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":

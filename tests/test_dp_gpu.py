@@ -1,0 +1,79 @@
+"""Data-parallel step on a real GPU through RCCL (single-rank process group): the bucketed
+all-reduce path of hpnn_amd.parallel.DataParallel must give the same weights as the plain
+single-GPU step (an all-reduce over one rank is the identity)."""
+import pytest
+import torch
+import torch.distributed as dist
+
+from hpnn_amd.models import MLP
+from hpnn_amd.parallel import DataParallel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", ["native", "torch"])
+@pytest.mark.parametrize("sizes", [[784, 128, 64, 10], [300, 96, 40, 7]])
+def test_dp_rccl_single_rank_matches_plain(gpu, sizes, comm):
+    dev = torch.device("cuda", 0)
+    store = dist.HashStore()
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        g = torch.Generator(device=dev).manual_seed(7)
+        B = 4096
+        Xr = torch.rand(B, sizes[0], device=dev, generator=g)
+        L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
+        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3)
+        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3)
+        dp = DataParallel(a, comm=comm)
+        assert dp.active and dp.world == 1
+        assert (dp.native is not None) == (comm == "native")
+        Xa, Xb = a.prepare_input(Xr), b.prepare_input(Xr)
+        for _ in range(3):
+            dp.train_step(Xa, labels=L, lr=0.05, alpha=0.2)
+            b.train_step(Xb, labels=L, lr=0.05, alpha=0.2)
+        torch.cuda.synchronize()
+        for wa, wb in zip(a.host_weights(), b.host_weights()):
+            # same math; the fused single-GPU step sums the split-K slabs in a different order
+            assert (wa - wb).abs().max().item() < 1e-6
+        assert dp.all_ok(True)
+        dp.check()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_native_comm_primitives_single_rank(gpu):
+    """libhpnn's RCCL communicator (csrc/dist/comm.cpp) on a one-rank group: every
+    collective is the identity, async all-reduce + join are ordered on the stream, the
+    status agreement and the error check work, and an injected fault surfaces."""
+    from hpnn_amd._lib import native
+    from hpnn_amd.parallel import NativeComm
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        c = NativeComm()
+        assert (c.rank, c.world) == (0, 1)
+        x = torch.arange(1000, dtype=torch.float32, device=dev)
+        ref = x.clone()
+        c.all_reduce(x)
+        c.broadcast(x, root=0)
+        out = torch.empty_like(x)
+        c.all_gather(out, x)
+        rs = torch.empty_like(x)
+        c.reduce_scatter(rs, x)
+        y = torch.ones(4096, device=dev)
+        y.mul_(3.0)
+        c.all_reduce_async(y)
+        c.join()
+        y.add_(1.0)  # ordered after the joined all-reduce
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref) and torch.equal(out, ref) and torch.equal(rs, ref)
+        assert torch.equal(y, torch.full_like(y, 4.0))
+        for dt in (torch.float64, torch.bfloat16, torch.int32):
+            z = torch.arange(64, device=dev).to(dt)
+            c.all_reduce(z)
+            assert torch.equal(z.cpu(), torch.arange(64).to(dt))
+        assert c.all_ok(True) and not c.all_ok(False)
+        c.check()
+        c.close()
+    finally:
+        dist.destroy_process_group()

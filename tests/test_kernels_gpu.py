@@ -83,6 +83,64 @@ def test_gemm_tn(gpu, Bt, N, M, S):
     assert (slab[0] - R0).abs().max().item() <= 1e-3 * R0.abs().max().item() + 1e-4
 
 
+@pytest.mark.parametrize("Bt,S", [(640, 3), (65536 // 8, 12), (1024, 16)])
+def test_gemm_tn_uneven_splits(gpu, Bt, S):
+    """split s covers the 64-row units [s*U/S, (s+1)*U/S): slabs match the row ranges"""
+    torch.manual_seed(S)
+    N, M = 128, 800
+    D = _rand(Bt, N).bfloat16()
+    H = _rand(Bt, M).bfloat16()
+    slab = ops.gemm_tn(D, H, splits=S)
+    rows = ops.split_rows(Bt, S)
+    assert rows[0][0] == 0 and rows[-1][1] == Bt and len({b - a for a, b in rows}) <= 2
+    for s_ in (0, S // 2, S - 1):
+        a, b = rows[s_]
+        R = ops.ref_gemm_tn(D[a:b], H[a:b])
+        assert (slab[s_] - R).abs().max().item() <= 1e-3 * R.abs().max().item() + 1e-4
+    R = ops.ref_gemm_tn(D, H)
+    assert (slab.sum(0) - R).abs().max().item() <= 1e-3 * R.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("S", [1, 8, 96, 37])
+def test_reduce_slabs_many(gpu, S):
+    torch.manual_seed(S)
+    slab = torch.randn(S, 128, 800, device="cuda")
+    out = torch.empty(128, 800, device="cuda")
+    ops.reduce_slabs(slab, out)
+    assert torch.allclose(out, slab.double().sum(0).float(), atol=1e-4, rtol=1e-5)
+    ops.reduce_slabs(slab, out)
+    out2 = out.clone()
+    ops.reduce_slabs(slab, out)
+    assert torch.equal(out, out2)  # deterministic
+
+
+@pytest.mark.parametrize("momentum", [False, True])
+def test_sgd_update_multi_wide(gpu, momentum):
+    """many slabs (>= 8) take the 1024-thread kernel: same step as the FP64 reference"""
+    torch.manual_seed(11)
+    layers, refs = [], []
+    for (N, K, S) in [(128, 800, 96), (64, 128, 16), (32, 64, 9)]:
+        W = torch.randn(N, K, device="cuda")
+        V = torch.randn(N, K, device="cuda") * 0.1 if momentum else None
+        G = torch.randn(S, N, K, device="cuda")
+        Wb = torch.empty(N, K, dtype=torch.bfloat16, device="cuda")
+        Wt = torch.empty(K, N, dtype=torch.bfloat16, device="cuda")
+        refs.append((W.double().clone(), None if V is None else V.double().clone(), G.double().sum(0)))
+        layers.append((W, V, G, Wb, Wt, None))
+    lr, alpha, scale = 0.05, 0.2, 1.0 / 512
+    ops.sgd_update_multi(layers, lr, alpha, scale, momentum)
+    torch.cuda.synchronize()
+    for (W, V, G, Wb, Wt, _), (W0, V0, g) in zip(layers, refs):
+        if momentum:
+            v = V0 + lr * g * scale
+            w = W0 + v
+            assert torch.allclose(V.double(), v * alpha, atol=1e-5)
+        else:
+            w = W0 + lr * g * scale
+        assert torch.allclose(W.double(), w, atol=1e-5)
+        assert torch.equal(Wb, W.bfloat16()) and torch.equal(Wt, W.bfloat16().t())
+
+
 def test_gemm_tn_integer_exact(gpu):
     """small integers are exact in bf16/fp32: any index permutation shows up."""
     Bt, N, M = 128, 32, 64
