@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--datasets", type=int, default=4, help="distinct synthetic minibatches cycled per GPU")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--alpha", type=float, default=0.2)
-    ap.add_argument("--graph", type=int, default=1, help="capture the steps in a HIP graph (1 GPU)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="capture the steps in HIP graphs (0: eager, 2: also with torch.distributed collectives)")
     ap.add_argument("--graph-steps", type=int, default=20, help="training steps per graph replay")
     args = ap.parse_args()
 
@@ -65,8 +66,10 @@ def main():
     def step(i):
         dp.train_step(Xs[i % args.datasets], labels=Ls[i % args.datasets], lr=args.lr, alpha=args.alpha)
 
-    # DP steps run eagerly (RCCL calls from Python); --graph 2 also captures them
-    use_graph = (args.graph and not dp.active) or args.graph == 2
+    # HIP graphs: single GPU always; data parallel when the gradient all-reduce goes through
+    # libhpnn's native RCCL communicator (capturable: event fork/join of its side stream),
+    # --graph 2 forces capture with torch.distributed collectives too
+    use_graph = bool(args.graph) and (not dp.active or dp.native is not None or args.graph == 2)
     gsteps = max(1, args.graph_steps)
     graphs = {}
 
@@ -89,9 +92,22 @@ def main():
             for i in range(3):
                 step(i)
         torch.cuda.current_stream().wait_stream(s)
-        # capture every graph the run will replay before anything is timed
-        for n in {gsteps, args.steps % gsteps, args.warmup % gsteps} - {0}:
-            capture(n)
+        # capture every graph the run will replay before anything is timed; a capture
+        # failure on any rank sends every rank back to eager steps (captured collectives
+        # never ran, so the ranks stay in step)
+        ok = True
+        try:
+            for n in {gsteps, args.steps % gsteps, args.warmup % gsteps} - {0}:
+                capture(n)
+        except Exception as e:  # noqa: BLE001
+            ok = False
+            print(f"rank {rank}: HIP graph capture failed ({e}); running eager steps", file=sys.stderr)
+        torch.cuda.synchronize()
+        if dp.active and not dp.all_ok(ok):
+            ok = False
+        if not ok:
+            graphs.clear()
+            use_graph = False
 
     def run_steps(first, n):
         if use_graph:
