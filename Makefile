@@ -30,7 +30,7 @@ PYINC     := $(shell $(PYTHON) -c "import sysconfig,pybind11;print('-I'+sysconfi
 PYMOD     := hpnn_amd/_native$(PYEXT)
 
 LIB       := $(LIBDIR)/libhpnn.so
-BINS      := $(BINDIR)/train_nn $(BINDIR)/run_nn $(BINDIR)/pmnist $(BINDIR)/pdif
+BINS      := $(BINDIR)/train_nn $(BINDIR)/run_nn $(BINDIR)/pmnist $(BINDIR)/pdif $(BINDIR)/pack_nn
 
 all: $(LIB) $(BINS) $(PYMOD)
 

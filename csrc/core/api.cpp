@@ -32,6 +32,10 @@
 #include <string>
 #include <vector>
 
+#include <libhpnn/observe.h>
+#include <omp.h>
+
+#include "dataset.h"
 #include "runtime_internal.h"
 #include "../gpu/engine.h"
 
@@ -435,19 +439,6 @@ extern "C" BOOL _NN(read, sample)(CHAR *filename, DOUBLE **in, DOUBLE **out) {
 /* ------------------------------------------------------------------ */
 /* workflow helpers                                                    */
 /* ------------------------------------------------------------------ */
-static bool list_dir(const char *dir, std::vector<std::string> &files) {
-    DIR *d = opendir(dir);
-    if (!d) return false;
-    struct dirent *e;
-    while ((e = readdir(d)) != NULL) {
-        if (e->d_name[0] == '.') continue;
-        files.emplace_back(e->d_name);
-    }
-    closedir(d);
-    std::sort(files.begin(), files.end());
-    return true;
-}
-
 /* seeded permutation without replacement (reference libhpnn.c:1218-1229) */
 static std::vector<UINT> seeded_order(UINT n, UINT seed) {
     srandom(seed);
@@ -483,22 +474,6 @@ static DOUBLE default_lr(const nn_def *conf, bool gpu) {
 
 static DOUBLE default_alpha(const nn_def *conf) { return conf->momentum >= 0 ? conf->momentum : BPM_MOMENTUM; }
 
-static bool load_all_samples(const char *dir, const std::vector<std::string> &files, UINT n_in,
-                             UINT n_out, std::vector<DOUBLE> &X, std::vector<DOUBLE> &T) {
-    X.clear();
-    T.clear();
-    for (const auto &f : files) {
-        std::string path = std::string(dir) + "/" + f;
-        DOUBLE *in, *out;
-        if (!_NN(read, sample)((CHAR *)path.c_str(), &in, &out)) continue;
-        X.insert(X.end(), in, in + n_in);
-        T.insert(T.end(), out, out + n_out);
-        free(in);
-        free(out);
-    }
-    return !X.empty();
-}
-
 /* ------------------------------------------------------------------ */
 /* training                                                            */
 /* ------------------------------------------------------------------ */
@@ -509,8 +484,9 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
         NN_ERROR(stdout, "unimplemented training type!\n");
         return FALSE;
     }
-    std::vector<std::string> files;
-    if (!list_dir(conf->samples, files)) {
+    HpnnTraceRange tr("nn_train_kernel");
+    HpnnSamples src;
+    if (!src.open(conf->samples)) {
         NN_ERROR(stderr, "can't open sample directory: %s\n", conf->samples);
         return FALSE;
     }
@@ -520,13 +496,16 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
     const DOUBLE alpha = default_alpha(conf);
 
     if (conf->mode == NN_MODE_BATCHED) {
-        std::vector<UINT> order = seeded_order((UINT)files.size(), conf->seed);
-        std::vector<std::string> shuffled;
-        for (UINT i : order) shuffled.push_back(files[i]);
+        std::vector<UINT> order = seeded_order((UINT)src.size(), conf->seed);
         std::vector<DOUBLE> X, T;
-        if (!load_all_samples(conf->samples, shuffled, k->n_inputs, k->n_outputs, X, T)) return FALSE;
-        UINT n = (UINT)(X.size() / k->n_inputs);
+        UINT n;
+        {
+            HpnnTraceRange tl("load_samples");
+            n = (UINT)src.load(order, k->n_inputs, k->n_outputs, _NN(return, omp_threads)(), X, T);
+        }
+        if (n == 0) return FALSE;
         hpnn_batched_opts o;
+        memset(&o, 0, sizeof(o));
         o.type = conf->type;
         o.train = conf->train;
         o.dtype = conf->dtype;
@@ -535,27 +514,47 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
         o.lr = lr;
         o.alpha = conf->train == NN_TRAIN_BPM ? alpha : 0.0;
         o.seed = conf->seed;
+        o.resume = conf->resume && k->dw != NULL;
+        o.epoch0 = conf->epochs_done;
         UINT ng = 1;
         _NN(get, n_gpu)(&ng);
         o.n_gpu = ng ? ng : 1;
         hpnn_batched_stats st;
         memset(&st, 0, sizeof(st));
-        BOOL ok = gpu ? hpnn_gpu_train_batched(k, X.data(), T.data(), n, &o, &st)
-                      : hpnn_cpu_train_batched(k, X.data(), T.data(), n, &o, &st);
+        BOOL ok;
+        {
+            HpnnTraceRange tb(gpu ? "train_batched_gpu" : "train_batched_cpu");
+            ok = gpu ? hpnn_gpu_train_batched(k, X.data(), T.data(), n, &o, &st)
+                     : hpnn_cpu_train_batched(k, X.data(), T.data(), n, &o, &st);
+        }
+        if (ok) {
+            conf->epochs_done += conf->epochs;
+            conf->samples_seen += st.samples;
+        }
         NN_OUT(stdout, "BATCHED TRAINING: %llu samples in %.6f s (%.1f samples/s) loss=%.10f acc=%u/%u\n",
                (unsigned long long)st.samples, st.seconds, st.seconds > 0 ? st.samples / st.seconds : 0.0,
                st.epoch_loss, st.correct, n);
+        if (hpnn_metrics_active()) {
+            char buf[384];
+            snprintf(buf, sizeof buf,
+                     "\"engine\": \"%s\", \"ok\": %s, \"samples\": %llu, \"seconds\": %.6f, \"samples_per_s\": %.3f, "
+                     "\"loss\": %.10g, \"correct\": %u, \"n\": %u, \"epochs_done\": %u",
+                     gpu ? "gpu" : "cpu", ok ? "true" : "false", (unsigned long long)st.samples, st.seconds,
+                     st.seconds > 0 ? st.samples / st.seconds : 0.0, st.epoch_loss, st.correct, n, conf->epochs_done);
+            hpnn_metrics_emit("train_batched", buf);
+        }
         return ok;
     }
 
     /* online (reference) mode */
-    std::vector<UINT> order = seeded_order((UINT)files.size(), conf->seed);
+    std::vector<UINT> order = seeded_order((UINT)src.size(), conf->seed);
+    UINT n_ok = 0, n_done = 0;
     for (UINT idx : order) {
-        const std::string &f = files[idx];
+        const std::string &f = src.names[idx];
         NN_OUT(stdout, "TRAINING FILE: %16.16s\t", f.c_str());
-        std::string path = std::string(conf->samples) + "/" + f;
         DOUBLE *in = NULL, *out = NULL;
-        if (!_NN(read, sample)((CHAR *)path.c_str(), &in, &out)) continue;
+        if (!src.get(idx, &in, &out)) continue;
+        HpnnTraceRange ts("train_sample");
         UINT it = 0;
         BOOL ok = FALSE, first = FALSE;
         DOUBLE e0 = 0.0, r;
@@ -570,10 +569,26 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
         NN_COUT(stdout, ok ? " SUCCESS!\n" : " FAIL!\n");
         fflush(stdout);
         if (r > 0.1) NN_DBG(stdout, "bad optimization!\n");
+        if (hpnn_metrics_active()) {
+            char buf[384];
+            snprintf(buf, sizeof buf,
+                     "\"file\": \"%s\", \"init\": %.10g, \"first_ok\": %s, \"n_iter\": %u, \"final\": %.10g, "
+                     "\"success\": %s",
+                     f.c_str(), e0, first ? "true" : "false", it, r, ok ? "true" : "false");
+            hpnn_metrics_emit("train_sample", buf);
+        }
+        n_ok += ok ? 1 : 0;
+        n_done++;
+        conf->samples_seen++;
         free(in);
         free(out);
     }
     if (gpu) hpnn_gpu_sync_host(k);
+    if (hpnn_metrics_active()) {
+        char buf[128];
+        snprintf(buf, sizeof buf, "\"samples\": %u, \"success\": %u", n_done, n_ok);
+        hpnn_metrics_emit("train_online", buf);
+    }
     return TRUE;
 }
 
@@ -584,20 +599,20 @@ extern "C" void _NN(run, kernel)(nn_def *conf) {
     g_last_pass = g_last_total = 0;
     if (!conf || !conf->kernel || !conf->tests || conf->type == NN_TYPE_UKN) return;
     kernel_ann *k = KERN(conf);
-    std::vector<std::string> files;
-    if (!list_dir(conf->tests, files)) {
+    HpnnSamples src;
+    if (!src.open(conf->tests)) {
         NN_ERROR(stderr, "can't open test directory: %s\n", conf->tests);
         return;
     }
+    HpnnTraceRange tr("nn_run_kernel");
     if (conf->seed == 0) conf->seed = (UINT)time(NULL);
     const bool gpu = use_gpu(conf);
-    std::vector<UINT> order = seeded_order((UINT)files.size(), conf->seed);
+    std::vector<UINT> order = seeded_order((UINT)src.size(), conf->seed);
     for (UINT idx : order) {
-        const std::string &f = files[idx];
+        const std::string &f = src.names[idx];
         NN_OUT(stdout, "TESTING FILE: %16.16s\t", f.c_str());
-        std::string path = std::string(conf->tests) + "/" + f;
         DOUBLE *in = NULL, *out = NULL;
-        if (!_NN(read, sample)((CHAR *)path.c_str(), &in, &out)) continue;
+        if (!src.get(idx, &in, &out)) continue;
         if (gpu) {
             hpnn_gpu_forward(k, conf->type, in);
         } else {
@@ -644,5 +659,11 @@ extern "C" void _NN(run, kernel)(nn_def *conf) {
         fflush(stdout);
         free(in);
         free(out);
+    }
+    if (hpnn_metrics_active()) {
+        char buf[128];
+        snprintf(buf, sizeof buf, "\"pass\": %u, \"total\": %u, \"accuracy\": %.6f", g_last_pass, g_last_total,
+                 g_last_total ? (double)g_last_pass / g_last_total : 0.0);
+        hpnn_metrics_emit("run", buf);
     }
 }

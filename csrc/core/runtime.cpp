@@ -15,6 +15,7 @@
  *   - there is no BLAS tier: nn_init_BLAS succeeds and only records -B.
  */
 #include <libhpnn.h>
+#include <libhpnn/observe.h>
 #include <hip/hip_runtime_api.h>
 #include <omp.h>
 #include <stdarg.h>
@@ -114,6 +115,13 @@ extern "C" BOOL _NN(init, MPI)(void) {
 
 extern "C" BOOL _NN(init, CUDA)(void) {
     ensure_runtime();
+    /* HPNN_DEBUG=1: serialise and check every HIP launch / copy (takes effect when the
+     * HIP runtime starts here, i.e. before any other HIP call of the process) */
+    if (hpnn_debug_enabled()) {
+        setenv("AMD_SERIALIZE_KERNEL", "3", 0);
+        setenv("AMD_SERIALIZE_COPY", "3", 0);
+        NN_WARN(stdout, "debug mode: serialised HIP launches and copies.\n");
+    }
     int n = 0;
     const char *force_cpu = getenv("HPNN_FORCE_CPU");
     if (force_cpu && force_cpu[0] == '1') n = 0;

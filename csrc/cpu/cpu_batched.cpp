@@ -14,6 +14,7 @@
  * not depend on the OpenMP thread count.
  */
 #include <libhpnn/ann.h>
+#include <libhpnn/observe.h>
 #include <math.h>
 #include <string.h>
 #include <chrono>
@@ -129,8 +130,9 @@ extern "C" BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     if (!k || n == 0) return FALSE;
     const bool mom = o->train == NN_TRAIN_BPM;
     if (mom) {
+        const bool keep = o->resume && k->dw;
         ann_momentum_init(k);
-        ann_raz_momentum(k);
+        if (!keep) ann_raz_momentum(k);
     }
     const UINT B = o->batch ? o->batch : 1;
     auto t0 = std::chrono::steady_clock::now();
@@ -148,6 +150,9 @@ extern "C" BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
             samples += b;
         }
         if (st) st->epoch_loss = acc / (nb ? nb : 1);
+        if (hpnn_metrics_active())
+            hpnn_metrics_epoch("cpu", o->epoch0 + e + 1, acc / (nb ? nb : 1), 0, n,
+                               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), samples);
     }
     auto t1 = std::chrono::steady_clock::now();
     if (st) {
@@ -169,6 +174,6 @@ extern "C" BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         }
         st->correct = correct;
     }
-    if (mom) ann_momentum_free(k);
+    /* the momentum stays in k->dw: nn_dump_state saves it for an exact resume */
     return TRUE;
 }

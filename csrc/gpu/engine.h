@@ -43,6 +43,8 @@ typedef struct {
     DOUBLE alpha;
     UINT seed;
     UINT n_gpu;       /* data-parallel replicas driven by this process */
+    BOOL resume;      /* BPM: start from the momentum in k->dw (exact resume)  */
+    UINT epoch0;      /* epochs completed before this call (metrics numbering) */
 } hpnn_batched_opts;
 
 typedef struct {
@@ -54,7 +56,8 @@ typedef struct {
 } hpnn_batched_stats;
 
 /* X: n x n_in, T: n x n_out (host, row-major FP64). Weights are read from
- * and written back to the host kernel. */
+ * and written back to the host kernel; with BPM the final momentum is written to
+ * k->dw (allocated if needed) so that nn_dump_state can save it. */
 BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
                             const hpnn_batched_opts *o, hpnn_batched_stats *st);
 /* batched inference: Y = net(X), n x n_out (host) */

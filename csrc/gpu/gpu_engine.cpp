@@ -17,6 +17,7 @@
 #include <libhpnn/ann.h>
 #include <dlfcn.h>
 #include <libhpnn/comm.h>
+#include <libhpnn/observe.h>
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
@@ -445,6 +446,11 @@ struct Batched {
     }
 
     BOOL step(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
+        const BOOL ok = step_launch(X, T, ldt, n_valid, lr, alpha, mom);
+        return ok && hpnn_debug_check("batched training step") == 0;
+    }
+
+    BOOL step_launch(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
         if (fused) return step_fused(X, T, ldt, n_valid, lr, alpha, mom);
         if (!forward(X)) return FALSE;
         if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
@@ -556,14 +562,34 @@ struct Batched {
         return hpnn_sgd_update_multi(u, L, lr, alpha, scale, mom ? 1 : 0, s) == 0;
     }
 
+    /* FP32 master weights (and BPM momentum, into k->dw) -> host FP64 */
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
+        if (V32[0]) ann_momentum_init(k);
         for (int l = 0; l < L; l++) {
             layer_ann *ly = layer_of(k, l);
             std::vector<float> tmp((size_t)Np[l] * Kp[l]);
             HIPCHK(hipMemcpy(tmp.data(), W32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
             for (int n = 0; n < N[l]; n++)
                 for (int m = 0; m < M[l]; m++) ly->weights[(size_t)n * M[l] + m] = tmp[(size_t)n * Kp[l] + m];
+            if (!V32[l]) continue;
+            HIPCHK(hipMemcpy(tmp.data(), V32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N[l]; n++)
+                for (int m = 0; m < M[l]; m++) k->dw[l][(size_t)n * M[l] + m] = tmp[(size_t)n * Kp[l] + m];
+        }
+        return TRUE;
+    }
+
+    /* exact resume: BPM momentum k->dw (host FP64) -> padded FP32 V32 */
+    BOOL upload_momentum(const kernel_ann *k) {
+        if (!k->dw) return TRUE;
+        for (int l = 0; l < L; l++) {
+            if (!V32[l]) continue;
+            std::vector<float> tmp((size_t)Np[l] * Kp[l], 0.f);
+            for (int n = 0; n < N[l]; n++)
+                for (int m = 0; m < M[l]; m++) tmp[(size_t)n * Kp[l] + m] = (float)k->dw[l][(size_t)n * M[l] + m];
+            HIPCHK(hipMemcpyAsync(V32[l], tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
         }
         return TRUE;
     }
@@ -619,6 +645,7 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     const bool mom = o->train == NN_TRAIN_BPM;
     Batched net;
     if (!net.init(k, B, o->type, mom, s)) return FALSE;
+    if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = (n_batches - 1) * B + net.Bp; /* last batch reads Bp rows */
     void *Xd = nullptr;
@@ -646,6 +673,10 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
             }
         }
         if (!net.read_stats(&ep_loss, &ep_hits)) return FALSE;
+        if (hpnn_metrics_active())
+            hpnn_metrics_epoch("gpu", o->epoch0 + e + 1, ep_loss / (double)n, ep_hits, n,
+                               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
+                               (UINT64)n * (e + 1));
     }
     auto t1 = std::chrono::steady_clock::now();
     net.download(k);
@@ -707,6 +738,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         if (hipSetDevice(dev[g]) != hipSuccess) return FALSE;
         nets[g].reset(new Batched());
         ok = nets[g]->init(k, Bg, o->type, mom, str[g]);
+        if (ok && mom && o->resume) ok = nets[g]->upload_momentum(k);
         if (!ok) break;
         if (loopback) {
             if (g == 0) {
@@ -807,6 +839,10 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
             for (int g = 0; g < G; g++)
                 if (hpnn_comm_check(comms[g]) != 0) ok = FALSE;
         }
+        if (ok && hpnn_metrics_active())
+            hpnn_metrics_epoch(loopback ? "gpu-dp-loopback" : "gpu-dp", o->epoch0 + e + 1, ep_loss / (double)n,
+                               ep_hits, n, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
+                               (UINT64)n * (e + 1));
     }
     auto t1 = std::chrono::steady_clock::now();
     if (ok) {

@@ -48,6 +48,12 @@ def lib():
             "nn_set_seed": (None, [vp, u]), "nn_return_seed": (u, [vp]),
             "nn_return_last_pass": (u, []), "nn_return_last_total": (u, []),
             "nn_return_version": (cp, []), "nn_return_type": (i, [vp]), "nn_return_train": (i, [vp]),
+            "nn_dump_state": (i, [vp, cp]), "nn_load_state": (i, [vp, cp]), "nn_return_epochs_done": (u, [vp]),
+            "nn_pack_samples": (i, [cp, cp]),
+            "hpnn_trace_enable": (None, [i]), "hpnn_trace_enabled": (i, []), "hpnn_trace_push": (None, [cp]),
+            "hpnn_trace_pop": (None, []), "hpnn_trace_add": (None, [cp, d]), "hpnn_trace_reset": (None, []),
+            "hpnn_trace_calls": (ctypes.c_uint64, [cp]), "hpnn_trace_seconds": (d, [cp]),
+            "hpnn_metrics_open": (i, [cp]), "hpnn_metrics_emit": (None, [cp, cp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -139,6 +145,25 @@ class Network:
 
     def dump_conf(self, path):
         self._dump(self.L.nn_dump_conf, path)
+
+    # exact checkpoint / resume (csrc/core/state.cpp)
+    def dump_state(self, path):
+        if not self.L.nn_dump_state(self.ptr, path.encode()):
+            raise OSError(f"nn_dump_state({path}) failed")
+
+    def load_state(self, path):
+        if not self.L.nn_load_state(self.ptr, path.encode()):
+            raise OSError(f"nn_load_state({path}) failed (missing, corrupted or mismatched)")
+
+    @property
+    def epochs_done(self):
+        return self.L.nn_return_epochs_done(self.ptr)
+
+
+def pack_samples(sample_dir, out_path):
+    """pack a directory of sample files into one binary file (csrc/core/dataset.cpp)"""
+    if not lib().nn_pack_samples(sample_dir.encode(), out_path.encode()):
+        raise OSError(f"nn_pack_samples({sample_dir}) failed")
 
 
 def smoke_online():

@@ -107,6 +107,10 @@ typedef struct {
     UINT epochs;     /* passes over the sample directory (default 1) */
     DOUBLE lr;       /* <=0: reference default for the path          */
     DOUBLE momentum; /* <0 : reference default 0.2                   */
+    /* -- training progress (exact resume, nn_dump_state / nn_load_state) -- */
+    UINT epochs_done;    /* batched epochs completed on this kernel       */
+    UINT64 samples_seen; /* training samples processed on this kernel     */
+    BOOL resume;         /* start batched training from the saved momentum */
 } nn_def;
 
 #define _NN(a, b) nn_##a##_##b
@@ -248,6 +252,14 @@ UINT _NN(return, last_pass)(void);
 UINT _NN(return, last_total)(void);
 /* library version string */
 const char *_NN(return, version)(void);
+/* exact training state sidecar (bit-exact FP64 weights, momentum, seed, progress,
+ * checksum): kernel.opt stays the interchange format, the state file resumes exactly */
+BOOL _NN(dump, state)(nn_def *conf, const CHAR *filename);
+BOOL _NN(load, state)(nn_def *conf, const CHAR *filename);
+UINT _NN(return, epochs_done)(nn_def *conf);
+/* pack a directory of sample files into one binary file; train / run accept a pack
+ * file wherever a sample or test directory is expected */
+BOOL _NN(pack, samples)(const CHAR *dir, const CHAR *filename);
 
 #ifdef __cplusplus
 }

@@ -7,11 +7,15 @@
  *   BLAS here), -S N streams per GPU.  Numeric flags take "-O4" or "-O 4".
  * Extensions: -G N GPUs, -b N minibatch (implies batched mode), -e N epochs,
  *   -m online|batched, -d f64|f32|bf16, -c force the CPU engine,
- *   -l LR learning rate, -a ALPHA momentum.
+ *   -l LR learning rate, -a ALPHA momentum,
+ *   -r FILE exact-resume state (loaded when present, written after training),
+ *   -M FILE JSON-lines metrics (same as HPNN_METRICS=FILE),
+ *   -T trace ranges + timing table (same as HPNN_TRACE=1).
  */
 #ifndef HPNN_CLI_COMMON_H
 #define HPNN_CLI_COMMON_H
 #include <libhpnn.h>
+#include <libhpnn/observe.h>
 #include <ctype.h>
 #include <string.h>
 #include <stdlib.h>
@@ -24,6 +28,8 @@ typedef struct {
     int dtype; /* -1 = from conf */
     int force_cpu;
     double lr, alpha;
+    const char *state;   /* -r */
+    const char *metrics; /* -M */
     int help;
 } cli_opts;
 
@@ -62,7 +68,12 @@ static int cli_parse(int argc, char **argv, cli_opts *o, int allow_x) {
                 j++;
                 continue;
             }
-            if (strchr("OBSGbemdla", c)) {
+            if (c == 'T') {
+                hpnn_trace_enable(1);
+                j++;
+                continue;
+            }
+            if (strchr("OBSGbemdlarM", c)) {
                 const char *val = a[j + 1] ? &a[j + 1] : (i + 1 < argc ? argv[++i] : NULL);
                 if (!val) {
                     _OUT(stderr, "syntax error: missing -%c parameter!\n", c);
@@ -90,6 +101,10 @@ static int cli_parse(int argc, char **argv, cli_opts *o, int allow_x) {
                     o->lr = atof(val);
                 } else if (c == 'a') {
                     o->alpha = atof(val);
+                } else if (c == 'r') {
+                    o->state = val;
+                } else if (c == 'M') {
+                    o->metrics = val;
                 }
                 break; /* a value consumes the rest of the argument */
             }
@@ -106,6 +121,7 @@ static void cli_apply_runtime(const cli_opts *o) {
     if (o->gpus) _NN(set, n_gpu)(o->gpus);
     _NN(set, cuda_streams)(o->streams ? o->streams : 1);
     if (o->dry) _NN(toggle, dry)();
+    if (o->metrics) hpnn_metrics_open(o->metrics);
 }
 
 static void cli_apply_conf(const cli_opts *o, nn_def *conf) {

@@ -6,7 +6,10 @@
  *   -> dump kernel.tmp (weights before training) -> nn_train_kernel
  *   -> dump kernel.opt (weights after training) -> deinit.
  * With -x (dry run) the two dumps are skipped.
+ * Extension: -r STATE resumes exactly from STATE when it exists (weights bit-exact,
+ * momentum, progress; see csrc/core/state.cpp) and writes it after training.
  */
+#include <sys/stat.h>
 #include <libhpnn.h>
 #include "cli_common.h"
 
@@ -28,6 +31,8 @@ static void dump_help(void) {
     _OUT(stdout, "-d D\tdtype: f64 | f32 | bf16.\n");
     _OUT(stdout, "-l X\tlearning rate.  -a X momentum.\n");
     _OUT(stdout, "-c \tforce the CPU engine.\n");
+    _OUT(stdout, "-r F\texact-resume state file (read if present, written after training).\n");
+    _OUT(stdout, "-M F\tJSON-lines metrics file.  -T trace ranges + timing table.\n");
     _OUT(stdout, "***********************************\n");
     _OUT(stdout, "input: neural network conf file\n");
     _OUT(stdout, "(default ./nn.conf)\n");
@@ -55,6 +60,14 @@ int main(int argc, char *argv[]) {
         return -1;
     }
     cli_apply_conf(&o, neural);
+    struct stat st;
+    if (o.state && stat(o.state, &st) == 0 && !_NN(load, state)(neural, o.state)) {
+        _OUT(stderr, "FAILED to load state file %s! (ABORTING)\n", o.state);
+        _NN(deinit, conf)(neural);
+        free(neural);
+        _NN(deinit, all)();
+        return -1;
+    }
     if (_NN(return, verbose)() > 1) _NN(dump, conf)(neural, stdout);
     if (!_NN(return, dry)()) {
         FILE *f = fopen("./kernel.tmp", "w");
@@ -75,7 +88,9 @@ int main(int argc, char *argv[]) {
             _NN(dump, kernel)(neural, f);
             fclose(f);
         }
+        if (o.state && ok && !_NN(dump, state)(neural, o.state)) ok = FALSE;
     }
+    if (hpnn_trace_enabled()) hpnn_trace_report(stdout);
     _NN(deinit, conf)(neural);
     free(neural);
     _NN(deinit, all)();
