@@ -57,3 +57,22 @@ clean:
 	rm -rf $(BUILD) $(LIB) $(BINS) $(PYMOD)
 
 .PHONY: all clean
+
+# Host-side sanitizer build (AddressSanitizer + UBSan) of the C API, CPU engine, runtime,
+# comm layer and CLIs; device code objects are the regular ones (GPU sanitizers are not
+# available on this pool).  tests/test_sanitizers_cpu.py runs the CPU workflows under it.
+ASAN_DIR   := $(BUILD)/asan
+ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+ASAN_OBJ   := $(patsubst %.cpp,$(ASAN_DIR)/%.o,$(CORE_SRC))
+ASAN_BINS  := $(ASAN_DIR)/train_nn $(ASAN_DIR)/run_nn $(ASAN_DIR)/pack_nn
+
+$(ASAN_DIR)/%.o: %.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) -c $< -o $@
+
+$(ASAN_DIR)/%: tools/%.cpp $(ASAN_OBJ) $(HIP_OBJ) tools/cli_common.h
+	$(CXX) $(CXXFLAGS) $(ASAN_FLAGS) $< $(ASAN_OBJ) $(HIP_OBJ) -o $@ $(LDFLAGS) -ldl
+
+asan: $(ASAN_BINS)
+
+.PHONY: asan

@@ -105,3 +105,28 @@ def test_batched_data_parallel_matches_single(tmp_path, shape, dp_env):
         ds, dd = ws - w0, wd - w0
         rel = np.linalg.norm(ds - dd) / (np.linalg.norm(ds) + 1e-30)
         assert rel < 0.03, rel
+
+
+@pytest.mark.parametrize("dims", [(784, [128, 64], 10), (40, [48], 6)])
+def test_batched_gpu_exact_resume(tmp_path, dims):
+    """GPU batched BPM: 2 epochs in one run == 1 epoch + state + 1 resumed epoch, bit for
+    bit (FP32 master weights and momentum round-trip exactly through the FP64 state), with
+    the HPNN_DEBUG serialised-launch mode and JSON metrics on."""
+    n_in, hid, n_out = dims
+    a, b = tmp_path / "a", tmp_path / "b"
+    for d in (a, b):
+        _data(str(d / "s"), 300, n_in, n_out, True, seed=4)
+        formats.write_conf(str(d / "nn.conf"), name="r", type="SNN", seed=5, inputs=n_in, hiddens=hid,
+                           outputs=n_out, train="BPM", sample_dir="./s", test_dir="./s")
+    tn = os.path.join(BIN, "train_nn")
+    env = {"HPNN_DEBUG": "1", "HPNN_METRICS": "m.jsonl"}
+    _run([tn, "-b", "128", "-e", "2", "-r", "st.bin", "nn.conf"], str(a), extra_env=env)
+    _run([tn, "-b", "128", "-e", "1", "-r", "st.bin", "nn.conf"], str(b), extra_env=env)
+    out = _run([tn, "-vv", "-b", "128", "-e", "1", "-r", "st.bin", "nn.conf"], str(b), extra_env=env)
+    assert "momentum restored" in out
+    assert (a / "st.bin").read_bytes() == (b / "st.bin").read_bytes()
+    assert (a / "kernel.opt").read_bytes() == (b / "kernel.opt").read_bytes()
+    import json
+    ep = [json.loads(x) for x in open(b / "m.jsonl")]
+    assert [r["epoch"] for r in ep if r["event"] == "epoch"] == [1, 2]
+    assert all(r["engine"] == "gpu" for r in ep if r["event"] == "epoch")
