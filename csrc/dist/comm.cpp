@@ -16,6 +16,7 @@
  */
 #include <libhpnn.h>
 #include <libhpnn/comm.h>
+#include <libhpnn/xar.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
 #include <stdlib.h>
@@ -132,6 +133,9 @@ struct hpnn_comm {
     int pending = -1; /* ring index of the last async collective not joined yet */
     int *d_flag = nullptr;
     bool failed = false;
+    /* one-shot xGMI all-reduce for small float32 sum buckets (csrc/dist/xgmi_ar.hip) */
+    hpnn_xar *xar = nullptr;
+    size_t xar_max = 0;
 };
 
 extern "C" int hpnn_fault_hit(const char *site) {
@@ -308,7 +312,10 @@ extern "C" int hpnn_comm_all_reduce_async(hpnn_comm *c, void *buf, long count, h
     /* fork: the side stream starts after what the compute stream has enqueued so far */
     if (hipEventRecord(c->ev_in[i], compute) != hipSuccess) return -2;
     if (hipStreamWaitEvent(c->side, c->ev_in[i], 0) != hipSuccess) return -2;
-    const int rc = hpnn_comm_all_reduce(c, buf, buf, count, dt, HPNN_OP_SUM, c->side);
+    const bool one_shot = c->xar && dt == HPNN_DT_F32 && (count & 3) == 0 && (size_t)count * 4 <= c->xar_max &&
+                          ((uintptr_t)buf & 15) == 0;
+    const int rc = one_shot ? hpnn_xar_all_reduce_f32(c->xar, (const float *)buf, (float *)buf, count, c->side)
+                            : hpnn_comm_all_reduce(c, buf, buf, count, dt, HPNN_OP_SUM, c->side);
     if (rc) return rc;
     if (hipEventRecord(c->ev_out[i], c->side) != hipSuccess) return -2;
     c->pending = i;
@@ -324,8 +331,20 @@ extern "C" int hpnn_comm_join(hpnn_comm *c, hipStream_t compute) {
     return 0;
 }
 
+extern "C" int hpnn_comm_set_xar(hpnn_comm *c, hpnn_xar *x, size_t max_bytes) {
+    if (!c) return -1;
+    c->xar = x;
+    c->xar_max = x ? (max_bytes < hpnn_xar_max_bytes(x) ? max_bytes : hpnn_xar_max_bytes(x)) : 0;
+    return 0;
+}
+
 extern "C" int hpnn_comm_check(hpnn_comm *c) {
     if (!c) return -1;
+    if (c->xar && hpnn_xar_status(c->xar) != 0) {
+        NN_ERROR(stderr, "xgmi all-reduce barrier timed out on rank %d (a peer never arrived)\n", c->rank);
+        c->failed = true;
+        return -8;
+    }
     if (c->failed || !c->comm) return -7;
     ncclResult_t ar = ncclSuccess;
     if (R.async_err(c->comm, &ar) != ncclSuccess || ar != ncclSuccess) {

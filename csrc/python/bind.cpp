@@ -17,6 +17,7 @@
 
 #include "../gpu/kernels.h"
 #include <libhpnn/comm.h>
+#include <libhpnn/xar.h>
 
 namespace py = pybind11;
 using uptr = uintptr_t;
@@ -182,6 +183,29 @@ PYBIND11_MODULE(_native, m) {
         return hpnn_comm_all_ok((hpnn_comm *)c, ok, S(stream));
     });
     m.def("fault_hit", [](const std::string &site) { return hpnn_fault_hit(site.c_str()); });
+    /* one-shot xGMI all-reduce (include/libhpnn/xar.h) */
+    m.attr("XAR_HANDLE_BYTES") = (int)HPNN_XAR_HANDLE_BYTES;
+    m.def("xar_create", [](int rank, int world, size_t max_bytes) {
+        return (uptr)hpnn_xar_create(rank, world, max_bytes);
+    });
+    m.def("xar_handles", [](uptr c) {
+        std::string h(HPNN_XAR_HANDLE_BYTES, '\0');
+        check(hpnn_xar_handles((hpnn_xar *)c, &h[0]), "xar_handles");
+        return py::bytes(h);
+    });
+    m.def("xar_open", [](uptr c, py::bytes all) {
+        std::string s = all;
+        check(hpnn_xar_open((hpnn_xar *)c, s.data()), "xar_open");
+    });
+    m.def("xar_all_reduce_f32", [](uptr c, uptr in, uptr out, long count, uptr stream) {
+        check(hpnn_xar_all_reduce_f32((hpnn_xar *)c, (const float *)P(in), (float *)P(out), count, S(stream)),
+              "xar_all_reduce_f32");
+    });
+    m.def("xar_status", [](uptr c) { return hpnn_xar_status((hpnn_xar *)c); });
+    m.def("xar_destroy", [](uptr c) { hpnn_xar_destroy((hpnn_xar *)c); });
+    m.def("comm_set_xar", [](uptr c, uptr x, size_t max_bytes) {
+        check(hpnn_comm_set_xar((hpnn_comm *)c, (hpnn_xar *)x, max_bytes), "comm_set_xar");
+    });
     m.def("device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

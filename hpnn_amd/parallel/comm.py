@@ -14,6 +14,8 @@ a HIP graph.
 The reference's equivalent is MPI_Allreduce / MPI_Allgather inline in every compute
 function (src/ann.c, e.g. ann.c:1263, 1638).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -25,6 +27,14 @@ ID_BYTES = 128
 
 _DT = {torch.float32: DT_F32, torch.float64: DT_F64, torch.bfloat16: DT_BF16, torch.int32: DT_I32,
        torch.uint8: DT_U8}
+
+
+def _xar_wanted(world):
+    """one-shot xGMI all-reduce: all ranks on this node (torchrun's LOCAL_WORLD_SIZE), at
+    most 8, and not disabled with HPNN_XAR=0"""
+    if os.environ.get("HPNN_XAR", "1") == "0" or world > 8:
+        return False
+    return int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world
 
 
 def _stream():
@@ -59,6 +69,41 @@ class NativeComm:
         self.h = n.comm_init_rank(bytes(uid.tolist()), self.world, self.rank, self.device)
         if not self.h:
             raise RuntimeError("ncclCommInitRank failed (see stderr)")
+        self.xar = 0
+        if self.world > 1 and _xar_wanted(self.world):
+            self._attach_xar(int(os.environ.get("HPNN_XAR_MAX_BYTES", str(4 << 20))))
+
+    def _attach_xar(self, max_bytes):
+        """one-shot xGMI all-reduce for the small gradient buckets (include/libhpnn/xar.h):
+        every rank maps every peer's buffer (hipIpc handles exchanged over the process
+        group); all ranks agree before it is used, else every rank stays on RCCL"""
+        n = native()
+        x = n.xar_create(self.rank, self.world, max_bytes)
+        ok = bool(x)
+        nb = n.XAR_HANDLE_BYTES
+        h = torch.zeros(nb, dtype=torch.uint8)
+        if ok:
+            try:
+                h = torch.tensor(list(n.xar_handles(x)), dtype=torch.uint8)
+            except RuntimeError:
+                ok = False
+        dev = torch.device("cuda", self.device) if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        allh = torch.zeros(self.world * nb, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(allh, h.to(dev), group=self.group)
+        if ok:
+            try:
+                n.xar_open(x, bytes(allh.cpu().tolist()))
+            except RuntimeError:
+                ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) != 1:
+            if x:
+                n.xar_destroy(x)
+            return False
+        self.xar = x
+        n.comm_set_xar(self.h, x, max_bytes)
+        return True
 
     # -- collectives on the current stream ------------------------------------------
     def all_reduce(self, t, op=OP_SUM):
@@ -101,6 +146,10 @@ class NativeComm:
         return bool(native().comm_all_ok(self.h, 1 if ok else 0, _stream()))
 
     def close(self):
+        if getattr(self, "xar", 0):
+            native().comm_set_xar(self.h, 0, 0)
+            native().xar_destroy(self.xar)
+            self.xar = 0
         if self.h:
             native().comm_destroy(self.h)
             self.h = 0

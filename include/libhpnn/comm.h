@@ -80,6 +80,11 @@ int hpnn_comm_all_reduce_async(hpnn_comm *c, void *buf, long count, hpnn_comm_dt
 /* compute stream waits for every collective issued with *_async so far */
 int hpnn_comm_join(hpnn_comm *c, hipStream_t compute);
 
+/* route *_async float32 sum all-reduces of at most max_bytes through the one-shot xGMI
+ * all-reduce x (include/libhpnn/xar.h; NULL detaches); larger ones stay on RCCL */
+struct hpnn_xar;
+int hpnn_comm_set_xar(hpnn_comm *c, struct hpnn_xar *x, size_t max_bytes);
+
 /* failure detection: 0 healthy, < 0 the communicator reported an asynchronous error
  * (a peer died, a link failed) -- the caller should abort it */
 int hpnn_comm_check(hpnn_comm *c);

@@ -1,0 +1,55 @@
+/*
+ * libhpnn xGMI all-reduce: one-shot peer-to-peer sum all-reduce for small buffers
+ * between the GPUs of one node (csrc/dist/xgmi_ar.hip).
+ *
+ * Why: MNIST's whole gradient is 437 KB.  A ring all-reduce (RCCL) of that size over
+ * 8 MI355X is latency-bound -- 2(N-1) = 14 dependent hops -- while each GPU has a direct
+ * xGMI link to every other GPU.  Here every rank publishes its buffer in device memory
+ * that every peer maps (hipIpc handles), then one kernel per rank does, per workgroup
+ * slice: copy in -> signal all peers -> wait for all peers -> read the slice from all
+ * N buffers and sum them in rank order (identical bits on every rank, deterministic)
+ * -> signal/wait again (so a buffer is never overwritten while a peer still reads it).
+ * One launch, two flag barriers, 7 concurrent link reads instead of 14 ring hops.
+ *
+ * Graph capture: the barrier epochs live in device memory and are advanced by the
+ * kernel itself, so a captured launch replays correctly any number of times.
+ * Failure: every spin wait is bounded (HPNN_XAR_TIMEOUT_MS, default 5000); a peer that
+ * never arrives sets the error word instead of hanging the GPU, and
+ * hpnn_xar_status reports it.
+ *
+ * Usage (one process per GPU): c = hpnn_xar_create(rank, world, max_bytes);
+ * hpnn_xar_handles(c, h) -> exchange world * HPNN_XAR_HANDLE_BYTES bytes (any
+ * bootstrap, e.g. torch.distributed all_gather); hpnn_xar_open(c, all);
+ * hpnn_xar_all_reduce_f32(c, in, out, count, stream).
+ */
+#ifndef LIBHPNN_XAR_H
+#define LIBHPNN_XAR_H
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HPNN_XAR_MAX_RANKS 8
+#define HPNN_XAR_MAX_BLOCKS 80
+#define HPNN_XAR_HANDLE_BYTES 128
+
+typedef struct hpnn_xar hpnn_xar;
+
+hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes);
+/* this rank's IPC handles (HPNN_XAR_HANDLE_BYTES bytes) */
+int hpnn_xar_handles(hpnn_xar *c, void *out);
+/* all ranks' handles, rank r at r * HPNN_XAR_HANDLE_BYTES */
+int hpnn_xar_open(hpnn_xar *c, const void *all);
+size_t hpnn_xar_max_bytes(const hpnn_xar *c);
+/* out = sum over ranks of in (float32, count % 4 == 0, count * 4 <= max_bytes);
+ * in == out allowed */
+int hpnn_xar_all_reduce_f32(hpnn_xar *c, const float *in, float *out, long count, hipStream_t stream);
+/* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
+int hpnn_xar_status(hpnn_xar *c);
+void hpnn_xar_destroy(hpnn_xar *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
