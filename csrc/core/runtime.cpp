@@ -16,6 +16,7 @@
  */
 #include <libhpnn.h>
 #include <libhpnn/observe.h>
+#include <libhpnn/devmem.h>
 #include <hip/hip_runtime_api.h>
 #include <omp.h>
 #include <stdarg.h>
@@ -213,6 +214,7 @@ extern "C" BOOL _NN(deinit, CUDA)(void) {
     ensure_runtime();
     if (!(lib_runtime.capability & NN_CAP_CUDA)) return TRUE;
     hpnn_rt_release_device_state();
+    hpnn_dev_trim(); /* cached device blocks back to the driver */
     destroy_streams();
     return TRUE;
 }

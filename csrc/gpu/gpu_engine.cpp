@@ -18,6 +18,7 @@
 #include <dlfcn.h>
 #include <libhpnn/comm.h>
 #include <libhpnn/observe.h>
+#include <libhpnn/devmem.h>
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
@@ -62,14 +63,14 @@ void free_model(GpuModel *g) {
     if (!g) return;
     hipSetDevice(g->dev);
     for (int l = 0; l < 16; l++) {
-        if (g->W[l]) hipFree(g->W[l]);
-        if (g->dW[l]) hipFree(g->dW[l]);
+        if (g->W[l]) hpnn_dev_free(g->W[l]);
+        if (g->dW[l]) hpnn_dev_free(g->dW[l]);
     }
-    if (g->x) hipFree(g->x);
-    if (g->t) hipFree(g->t);
-    if (g->out) hipFree(g->out);
-    if (g->result) hipFree(g->result);
-    if (g->scratch) hipFree(g->scratch);
+    if (g->x) hpnn_dev_free(g->x);
+    if (g->t) hpnn_dev_free(g->t);
+    if (g->out) hpnn_dev_free(g->out);
+    if (g->result) hpnn_dev_free(g->result);
+    if (g->scratch) hpnn_dev_free(g->scratch);
     delete g;
 }
 
@@ -96,14 +97,14 @@ BOOL ensure_model(kernel_ann *k, UINT gpu) {
         size_t vec = k->n_inputs;
         for (int l = 0; l < L; l++) {
             layer_ann *ly = layer_of(k, l);
-            HIPCHK(hipMalloc(&g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs));
+            HIPCHK(hpnn_dev_malloc(&g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs));
             vec += 3 * (size_t)ly->n_neurons;
         }
-        HIPCHK(hipMalloc(&g->x, sizeof(double) * k->n_inputs));
-        HIPCHK(hipMalloc(&g->t, sizeof(double) * k->n_outputs));
-        HIPCHK(hipMalloc(&g->out, sizeof(double) * k->n_outputs));
-        HIPCHK(hipMalloc(&g->result, sizeof(double) * 8));
-        HIPCHK(hipMalloc(&g->scratch, sizeof(double) * vec));
+        HIPCHK(hpnn_dev_malloc(&g->x, sizeof(double) * k->n_inputs));
+        HIPCHK(hpnn_dev_malloc(&g->t, sizeof(double) * k->n_outputs));
+        HIPCHK(hpnn_dev_malloc(&g->out, sizeof(double) * k->n_outputs));
+        HIPCHK(hpnn_dev_malloc(&g->result, sizeof(double) * 8));
+        HIPCHK(hpnn_dev_malloc(&g->scratch, sizeof(double) * vec));
         k->gpu = g;
         std::lock_guard<std::mutex> lk(g_mu);
         g_models.insert(k);
@@ -126,7 +127,7 @@ BOOL ensure_momentum(kernel_ann *k) {
     for (int l = 0; l < g->L; l++) {
         layer_ann *ly = layer_of(k, l);
         size_t n = (size_t)ly->n_neurons * ly->n_inputs;
-        if (!g->dW[l]) HIPCHK(hipMalloc(&g->dW[l], sizeof(double) * n));
+        if (!g->dW[l]) HIPCHK(hpnn_dev_malloc(&g->dW[l], sizeof(double) * n));
         HIPCHK(hipMemsetAsync(g->dW[l], 0, sizeof(double) * n, hpnn_rt_stream(0, 0)));
     }
     return TRUE;
@@ -301,21 +302,21 @@ struct Batched {
         if (ev_fork) hipEventDestroy(ev_fork);
         if (ev_join) hipEventDestroy(ev_join);
         for (int l = 0; l < 16; l++) {
-            hipFree(W32[l]);
-            hipFree(V32[l]);
-            hipFree(slab[l]);
-            hipFree(Wb[l]);
-            hipFree(Wt[l]);
-            hipFree(H[l]);
-            hipFree(D[l]);
+            hpnn_dev_free(W32[l]);
+            hpnn_dev_free(V32[l]);
+            hpnn_dev_free(slab[l]);
+            hpnn_dev_free(Wb[l]);
+            hpnn_dev_free(Wt[l]);
+            hpnn_dev_free(H[l]);
+            hpnn_dev_free(D[l]);
         }
-        hipFree(Z);
-        hipFree(acc);
-        hipFree(midslab);
-        hipFree(midtmp);
-        hipFree(G12);
-        hipFree(W0f);
-        if (own_flat) hipFree(gflat);
+        hpnn_dev_free(Z);
+        hpnn_dev_free(acc);
+        hpnn_dev_free(midslab);
+        hpnn_dev_free(midtmp);
+        hpnn_dev_free(G12);
+        hpnn_dev_free(W0f);
+        if (own_flat) hpnn_dev_free(gflat);
     }
 
     /* sum the stat slots: returns (loss sum, hits) */
@@ -350,16 +351,16 @@ struct Batched {
             Np[l] = pad32(N[l]);
             S[l] = pick_splits(Np[l], Kp[l], Bp);
             const size_t nw = (size_t)Np[l] * Kp[l];
-            HIPCHK(hipMalloc(&W32[l], nw * 4));
-            HIPCHK(hipMalloc(&Wb[l], nw * 2));
-            HIPCHK(hipMalloc(&Wt[l], nw * 2));
-            HIPCHK(hipMalloc(&slab[l], nw * 4 * S[l]));
+            HIPCHK(hpnn_dev_malloc(&W32[l], nw * 4));
+            HIPCHK(hpnn_dev_malloc(&Wb[l], nw * 2));
+            HIPCHK(hpnn_dev_malloc(&Wt[l], nw * 2));
+            HIPCHK(hpnn_dev_malloc(&slab[l], nw * 4 * S[l]));
             if (momentum) {
-                HIPCHK(hipMalloc(&V32[l], nw * 4));
+                HIPCHK(hpnn_dev_malloc(&V32[l], nw * 4));
                 HIPCHK(hipMemsetAsync(V32[l], 0, nw * 4, s));
             }
-            HIPCHK(hipMalloc(&D[l], (size_t)Bp * Np[l] * 2));
-            if (l < L - 1) HIPCHK(hipMalloc(&H[l], (size_t)Bp * Np[l] * 2));
+            HIPCHK(hpnn_dev_malloc(&D[l], (size_t)Bp * Np[l] * 2));
+            if (l < L - 1) HIPCHK(hpnn_dev_malloc(&H[l], (size_t)Bp * Np[l] * 2));
             /* FP64 host -> padded FP32 master */
             std::vector<float> tmp(nw, 0.f);
             for (int n = 0; n < N[l]; n++)
@@ -368,8 +369,8 @@ struct Batched {
             HIPCHK(hipStreamSynchronize(s));
             if (hpnn_cast_weights(W32[l], Wb[l], Wt[l], Np[l], Kp[l], s)) return FALSE;
         }
-        HIPCHK(hipMalloc(&Z, (size_t)Bp * Np[L - 1] * 4));
-        HIPCHK(hipMalloc(&acc, ACC_BYTES));
+        HIPCHK(hpnn_dev_malloc(&Z, (size_t)Bp * Np[L - 1] * 4));
+        HIPCHK(hpnn_dev_malloc(&acc, ACC_BYTES));
         HIPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
         fused = (L == 3 && Np[0] == 128 && Np[1] == 64 && Np[2] == 32);
         fused_x = fused && (Kp[0] == 256 || Kp[0] == 512 || Kp[0] == 800 || Kp[0] == 832 || Kp[0] == 896);
@@ -378,14 +379,14 @@ struct Batched {
             mid_grid = fused_x ? hpnn_mlp3_fused_grid(Bp, 0) : (Bp / 64 < 512 ? Bp / 64 : 512);
             if (mid_grid <= 0) return FALSE;
             mid_groups = mid_grid < 16 ? mid_grid : 16;
-            HIPCHK(hipMalloc(&midslab, (size_t)mid_grid * slab_f * 4));
-            HIPCHK(hipMalloc(&midtmp, (size_t)16 * slab_f * 4));
-            HIPCHK(hipMalloc(&G12, (size_t)slab_f * 4));
+            HIPCHK(hpnn_dev_malloc(&midslab, (size_t)mid_grid * slab_f * 4));
+            HIPCHK(hpnn_dev_malloc(&midtmp, (size_t)16 * slab_f * 4));
+            HIPCHK(hpnn_dev_malloc(&G12, (size_t)slab_f * 4));
             if (fused_x) {
                 HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
                 HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
                 HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-                HIPCHK(hipMalloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
+                HIPCHK(hpnn_dev_malloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
                 hpnn_upd_layer c0 = {W32[0], nullptr, W32[0], 0, Wb[0], Wt[0], W0f, 1, Np[0], Kp[0]};
                 if (hpnn_sgd_update_multi(&c0, 1, 0.f, 0.f, 0.f, 0, s)) return FALSE; /* lr 0: a cast */
             }
@@ -497,7 +498,7 @@ struct Batched {
             own_flat = false;
             return TRUE;
         }
-        HIPCHK(hipMalloc(&gflat, goff[L] * 4));
+        HIPCHK(hpnn_dev_malloc(&gflat, goff[L] * 4));
         own_flat = true;
         return TRUE;
     }
@@ -598,12 +599,12 @@ struct Batched {
 /* upload n host rows (FP64) as a padded BF16 matrix [rows_p x cols_p] */
 BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t s) {
     void *tmp = nullptr;
-    HIPCHK(hipMalloc(dst, (size_t)rows_p * cols_p * 2));
-    HIPCHK(hipMalloc(&tmp, (size_t)rows * cols * 8));
+    HIPCHK(hpnn_dev_malloc(dst, (size_t)rows_p * cols_p * 2));
+    HIPCHK(hpnn_dev_malloc(&tmp, (size_t)rows * cols * 8));
     HIPCHK(hipMemcpyAsync(tmp, src, (size_t)rows * cols * 8, hipMemcpyHostToDevice, s));
     if (hpnn_pack_bf16(tmp, 1, rows, cols, cols, *dst, rows_p, cols_p, cols_p, s)) return FALSE;
     HIPCHK(hipStreamSynchronize(s));
-    hipFree(tmp);
+    hpnn_dev_free(tmp);
     return TRUE;
 }
 
@@ -654,7 +655,7 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     {
         std::vector<float> tf((size_t)rows_p * k->n_outputs, 0.f);
         for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (float)T[i];
-        HIPCHK(hipMalloc(&Td, tf.size() * 4));
+        HIPCHK(hpnn_dev_malloc(&Td, tf.size() * 4));
         HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice));
     }
     auto t0 = std::chrono::steady_clock::now();
@@ -667,8 +668,8 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
             const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * 2;
             const float *tb = Td + (size_t)b * B * k->n_outputs;
             if (!net.step(xb, tb, (int)k->n_outputs, nv, (float)o->lr, (float)o->alpha, mom)) {
-                hipFree(Xd);
-                hipFree(Td);
+                hpnn_dev_free(Xd);
+                hpnn_dev_free(Td);
                 return FALSE;
             }
         }
@@ -687,8 +688,8 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         st->correct = ep_hits;
         st->last_loss = st->epoch_loss;
     }
-    hipFree(Xd);
-    hipFree(Td);
+    hpnn_dev_free(Xd);
+    hpnn_dev_free(Td);
     /* device FP64 copy of the online engine (if any) is now stale */
     if (k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
     return TRUE;
@@ -718,13 +719,13 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         for (int g = 0; g < G; g++) {
             hipSetDevice(dev[g]);
             if (!loopback || g == 0) {
-                hipFree(Xd[g]);
-                hipFree(Td[g]);
+                hpnn_dev_free(Xd[g]);
+                hpnn_dev_free(Td[g]);
             }
             nets[g].reset();
             if (comms[g]) hpnn_comm_destroy(comms[g]);
         }
-        if (lb_flat) hipFree(lb_flat);
+        if (lb_flat) hpnn_dev_free(lb_flat);
         hipSetDevice(hpnn_rt_device(0));
     };
     for (int g = 0; g < G; g++) {
@@ -744,7 +745,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
             if (g == 0) {
                 size_t tot = 0;
                 for (int l = 0; l < nets[0]->L; l++) tot += (size_t)nets[0]->Np[l] * nets[0]->Kp[l];
-                if (hipMalloc(&lb_flat, tot * 4 * G) != hipSuccess) ok = FALSE;
+                if (hpnn_dev_malloc(&lb_flat, tot * 4 * G) != hipSuccess) ok = FALSE;
             }
             if (ok) {
                 size_t tot = 0;
@@ -760,7 +761,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
             if (ok) {
                 std::vector<float> tf((size_t)rows_p * n_out, 0.f);
                 for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (float)T[i];
-                ok = hipMalloc(&Td[g], tf.size() * 4) == hipSuccess &&
+                ok = hpnn_dev_malloc(&Td[g], tf.size() * 4) == hipSuccess &&
                      hipMemcpy(Td[g], tf.data(), tf.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
             }
         } else {
@@ -877,8 +878,8 @@ extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dty
     void *Xd = nullptr;
     float *O = nullptr, *Tz = nullptr;
     if (!upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
-    HIPCHK(hipMalloc(&O, (size_t)net.Bp * net.Np[net.L - 1] * 4));
-    HIPCHK(hipMalloc(&Tz, (size_t)net.Bp * k->n_outputs * 4));
+    HIPCHK(hpnn_dev_malloc(&O, (size_t)net.Bp * net.Np[net.L - 1] * 4));
+    HIPCHK(hpnn_dev_malloc(&Tz, (size_t)net.Bp * k->n_outputs * 4));
     HIPCHK(hipMemset(Tz, 0, (size_t)net.Bp * k->n_outputs * 4));
     std::vector<float> h((size_t)net.Bp * net.Np[net.L - 1]);
     for (int b = 0; b < n_batches; b++) {
@@ -892,8 +893,8 @@ extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dty
             for (UINT c = 0; c < k->n_outputs; c++)
                 Y[((size_t)b * B + r) * k->n_outputs + c] = h[(size_t)r * net.Np[net.L - 1] + c];
     }
-    hipFree(Xd);
-    hipFree(O);
-    hipFree(Tz);
+    hpnn_dev_free(Xd);
+    hpnn_dev_free(O);
+    hpnn_dev_free(Tz);
     return TRUE;
 }

@@ -18,6 +18,7 @@
 #include "../gpu/kernels.h"
 #include <libhpnn/comm.h>
 #include <libhpnn/xar.h>
+#include <libhpnn/devmem.h>
 
 namespace py = pybind11;
 using uptr = uintptr_t;
@@ -182,6 +183,12 @@ PYBIND11_MODULE(_native, m) {
         py::gil_scoped_release nogil;
         return hpnn_comm_all_ok((hpnn_comm *)c, ok, S(stream));
     });
+    m.def("devmem_stats", []() {
+        size_t a, b, c, d;
+        hpnn_dev_stats(&a, &b, &c, &d);
+        return py::make_tuple(a, b, c, d);
+    });
+    m.def("devmem_trim", []() { hpnn_dev_trim(); });
     m.def("fault_hit", [](const std::string &site) { return hpnn_fault_hit(site.c_str()); });
     /* one-shot xGMI all-reduce (include/libhpnn/xar.h) */
     m.attr("XAR_HANDLE_BYTES") = (int)HPNN_XAR_HANDLE_BYTES;
