@@ -51,6 +51,12 @@ int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C
  * ldg: row stride of a slab row (>= M); slab stride = N*ldg. */
 int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N,
                       int M, int Bt, int splits, hipStream_t stream);
+/* the same GEMM plus, in the same launch, hpnn_reduce_groups(rslab, rS, rstride, rn, rgroups,
+ * rout) run by extra workgroups appended to the grid (they fill the CUs the GEMM tiles
+ * leave idle; one launch less per fused training step) */
+int hpnn_gemm_tn_bf16_reduce(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M,
+                             int Bt, int splits, const float *rslab, int rS, long rstride, long rn, int rgroups,
+                             float *rout, hipStream_t stream);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)

@@ -217,11 +217,45 @@ __device__ __forceinline__ bf16x8 tnp_frag(const char *tile, int kbase, int c0, 
     return hpnn::frag_tr<BKR>(tile, kbase, c0, lane);
 }
 
+/* Optional tail work of a TN launch: a grouped slab reduction (reduce_groups_kernel of
+ * kernels_mlp3.hip: out[g*ostride + i] = sum of slabs [g*SG, min(S, (g+1)*SG)), float4 i)
+ * run by extra workgroups appended to the GEMM grid.  The fused MNIST step reduces its
+ * [G1 | G2] block slabs this way: the workgroups fill the CUs the 240-tile GEMM leaves
+ * idle, and a launch (plus its serialized ~5 us) disappears from the step. */
+struct TnTail {
+    const float *slab;
+    float *out;
+    long stride, n4, ostride;
+    int S, SG, bx, blocks;
+};
+
+__device__ __forceinline__ void tn_tail_reduce(const TnTail &t, int v) {
+    const long e = (long)(v % t.bx) * 256 + threadIdx.x;
+    const int g = v / t.bx;
+    if (e >= t.n4) return;
+    const int s_end = min(t.S, (g + 1) * t.SG);
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    int s = g * t.SG;
+    for (; s + 3 < s_end; s += 4) {
+        a0 += ((const f32x4 *)(t.slab + (long)s * t.stride))[e];
+        a1 += ((const f32x4 *)(t.slab + (long)(s + 1) * t.stride))[e];
+        a2 += ((const f32x4 *)(t.slab + (long)(s + 2) * t.stride))[e];
+        a3 += ((const f32x4 *)(t.slab + (long)(s + 3) * t.stride))[e];
+    }
+    for (; s < s_end; s++) a0 += ((const f32x4 *)(t.slab + (long)s * t.stride))[e];
+    ((f32x4 *)(t.out + (long)g * t.ostride))[e] = (a0 + a1) + (a2 + a3);
+}
+
 template <int TM, int TN, int BKR, int STAGES>
 __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
                                                            const __bf16 *__restrict__ H, int ldh,
                                                            float *__restrict__ slab, int ldg, int N, int units,
-                                                           int splits, int tiles_n, int tiles, int xcd_map) {
+                                                           int splits, int tiles_n, int tiles, int xcd_map,
+                                                           TnTail tail) {
+    if ((int)blockIdx.x >= tiles * splits) { /* appended reduction workgroups: no LDS, no barrier */
+        tn_tail_reduce(tail, (int)blockIdx.x - tiles * splits);
+        return;
+    }
     constexpr int WTM = TM / 2, WTN = TN / 2;
     constexpr int FM = WTM / 16, FN = WTN / 16;
     constexpr int H_PIECES = (TM / 32) * (BKR / 16), D_PIECES = (TN / 32) * (BKR / 16);
@@ -344,7 +378,7 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
 
 template <int TM, int TN>
 int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
-                hipStream_t s) {
+                hipStream_t s, const TnTail &tail) {
     const int tiles_n = N / TN, tiles_m = M / TM;
     const int units = Bt / 64;
     /* 32-row stages, ring of ~72 KiB (2 workgroups per CU) */
@@ -353,18 +387,30 @@ int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int
     constexpr int ST = (73728 / STAGE) < 2 ? 2 : ((73728 / STAGE) > 6 ? 6 : (73728 / STAGE));
     const int tiles = tiles_m * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits), dim3(256), 0, s,
+    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits + tail.blocks), dim3(256), 0, s,
                        (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, tiles,
-                       xcd_map);
+                       xcd_map, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 template <int TM>
 int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
-                hipStream_t s) {
-    if (N % 128 == 0) return launch_tn_t<TM, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s);
-    if (N % 64 == 0) return launch_tn_t<TM, 64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s);
-    return launch_tn_t<TM, 32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s);
+                hipStream_t s, const TnTail &t) {
+    if (N % 128 == 0) return launch_tn_t<TM, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+    if (N % 64 == 0) return launch_tn_t<TM, 64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+    return launch_tn_t<TM, 32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+}
+
+int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
+                     int splits, hipStream_t stream, const TnTail &t) {
+    if (N <= 0 || M <= 0 || Bt <= 0 || splits <= 0) return -1;
+    if (N % 32 || M % 32 || Bt % 64 || splits > Bt / 64) return -2;
+    if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
+    if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    if (M % 64 == 0) return launch_tn_m<64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    return launch_tn_m<32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
 }
 
 }  // namespace
@@ -392,12 +438,16 @@ extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb,
 
 extern "C" int hpnn_gemm_tn_bf16(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M,
                                  int Bt, int splits, hipStream_t stream) {
-    if (N <= 0 || M <= 0 || Bt <= 0 || splits <= 0) return -1;
-    if (N % 32 || M % 32 || Bt % 64 || splits > Bt / 64) return -2;
-    if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
-    if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
-    if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
-    if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
-    if (M % 64 == 0) return launch_tn_m<64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
-    return launch_tn_m<32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream);
+    const TnTail none = {nullptr, nullptr, 0, 0, 0, 0, 1, 1, 0};
+    return gemm_tn_dispatch(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, none);
+}
+
+extern "C" int hpnn_gemm_tn_bf16_reduce(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N,
+                                        int M, int Bt, int splits, const float *rslab, int rS, long rstride, long rn,
+                                        int rgroups, float *rout, hipStream_t stream) {
+    if (rn % 4 || rstride % 4 || rS < 1 || rgroups < 1 || rgroups > rS || !rslab || !rout) return -2;
+    const long n4 = rn / 4;
+    const int bx = (int)((n4 + 255) / 256);
+    const TnTail t = {rslab, rout, rstride, n4, rn, rS, (rS + rgroups - 1) / rgroups, bx, bx * rgroups};
+    return gemm_tn_dispatch(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
 }

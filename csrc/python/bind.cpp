@@ -108,6 +108,13 @@ PYBIND11_MODULE(_native, m) {
         return v;
     });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
+    m.def("gemm_tn_bf16_reduce", [](uptr D, int ldd, uptr H, int ldh, uptr slab, int ldg, int N, int M, int Bt,
+                                    int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,
+                                    uptr stream) {
+        check(hpnn_gemm_tn_bf16_reduce(P(D), ldd, P(H), ldh, (float *)P(slab), ldg, N, M, Bt, splits,
+                                       (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
+              "gemm_tn_bf16_reduce");
+    });
     m.def("reduce_groups", [](uptr slab, int Sn, long stride, long n, int groups, uptr out, uptr stream) {
         check(hpnn_reduce_groups((const float *)P(slab), Sn, stride, n, groups, (float *)P(out), S(stream)),
               "reduce_groups");

@@ -26,6 +26,8 @@ from .. import ops
 # G0 GEMM (fused path); off by default (cross-stream fork/join inside the graph measured
 # slower than back-to-back launches on MI355X)
 _SIDE_REDUCE = os.environ.get("HPNN_SIDE_REDUCE", "0") == "1"
+# HPNN_TAIL_REDUCE=0: separate reduce_groups launch instead of the GEMM's tail workgroups
+_TAIL_REDUCE = os.environ.get("HPNN_TAIL_REDUCE", "1") == "1"
 
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
@@ -283,6 +285,9 @@ class MLP:
                     ops.reduce_groups(self.midslab, self.mid_groups, groups)
                 ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
                 main.wait_stream(side)
+            elif _TAIL_REDUCE:
+                # one launch: the reduction rides on workgroups appended to the GEMM grid
+                ops.gemm_tn_reduce(self.D[0], X, self.S[0], self.slab[0], self.midslab, self.mid_groups, groups)
             else:
                 ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
                 ops.reduce_groups(self.midslab, self.mid_groups, groups)

@@ -75,6 +75,20 @@ def gemm_tn(D, H, splits=1, out=None):
     return out
 
 
+def gemm_tn_reduce(D, H, splits, out, rslab, groups, rout):
+    """gemm_tn(D, H, splits, out) and reduce_groups(rslab, groups, rout) in ONE launch:
+    the reduction runs on workgroups appended to the GEMM grid (csrc/gpu/kernels.h)."""
+    if _cpu(D):
+        gemm_tn(D, H, splits=splits, out=out)
+        return reduce_groups(rslab, groups, rout)
+    Bt, N = D.shape
+    M = H.shape[1]
+    native().gemm_tn_bf16_reduce(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), out.data_ptr(), out.stride(1),
+                                 N, M, Bt, splits, rslab.data_ptr(), rslab.shape[0], rslab.stride(0), rslab[0].numel(),
+                                 groups, rout.data_ptr(), _stream())
+    return rout
+
+
 def output_delta(Z, n_out, net_type, D, labels=None, T=None, t_hi=1.0, t_lo=0.0, n_valid=None, O=None,
                  loss_acc=None, correct=None):
     """Output layer: activation/softmax, loss sum, delta (bf16) and argmax hits."""

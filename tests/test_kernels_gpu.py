@@ -48,6 +48,25 @@ def test_gemm_nt_weight_stationary(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 2048, 512), (8192, 1024, 640), (4352, 4096, 576)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nt_big_tile(gpu, M, N, K, epi):
+    """shapes with >= 256 tiles of 256x128 take the large-tile kernel (3-stage 144 KiB ring);
+    padded row strides on every operand"""
+    torch.manual_seed(M + N + K + epi)
+    A = _rand(M, K + 64).bfloat16()[:, :K]
+    B = (_rand(N, K + 32) + torch.arange(N, device="cuda")[:, None] * 0.001).bfloat16()[:, :K]
+    aux = _rand(M, N + 32).bfloat16()[:, :N] if epi == ops.EPI_DACT else None
+    for f32 in (False, True):
+        out = torch.empty(M, N + 64, dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")[:, :N]
+        C = ops.gemm_nt(A, B, epi, aux=aux, out_f32=f32, out=out)
+        R = ops.ref_gemm_nt(A, B, epi, aux)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (C.float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+
+
 def test_gemm_nt_identity(gpu):
     """A = I checks the C layout with an asymmetric B (cdna guide section 3)."""
     M, N, K = 128, 64, 128
@@ -212,3 +231,25 @@ def test_pack_bf16(gpu):
     ops.pack_bf16(X, out)
     assert torch.equal(out[:100, :784], X.float().bfloat16())
     assert out[100:].abs().max().item() == 0 and out[:, 784:].abs().max().item() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,groups", [(256, 16), (100, 7), (5, 5)])
+def test_gemm_tn_with_tail_reduce(gpu, S, groups):
+    """gemm_tn + reduce_groups in one launch (reduction on appended workgroups) == the two
+    separate kernels, bit for bit"""
+    torch.manual_seed(S + groups)
+    Bt, N, M = 65536, 128, 800
+    D = _rand(Bt, N).bfloat16()
+    H = _rand(Bt, M).bfloat16()
+    sl = torch.randn(S, 10240, device="cuda")
+    a_slab = torch.empty(48, N, M, device="cuda")
+    b_slab = torch.empty_like(a_slab)
+    a_red = torch.full((groups, 10240), float("nan"), device="cuda")
+    b_red = torch.full_like(a_red, float("nan"))
+    ops.gemm_tn(D, H, splits=48, out=a_slab)
+    ops.reduce_groups(sl, groups, a_red)
+    ops.gemm_tn_reduce(D, H, 48, b_slab, sl, groups, b_red)
+    torch.cuda.synchronize()
+    assert torch.equal(a_slab, b_slab)
+    assert torch.equal(a_red, b_red)
