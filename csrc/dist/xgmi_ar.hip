@@ -71,7 +71,43 @@ __device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world,
     __threadfence_system();
 }
 
-__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, const float4 *__restrict__ in,
+/* the input of a call: up to HPNN_XAR_MAX_SEGS segments laid end to end in the output;
+ * segment j is the sum of S_j slabs (stride in float4) -- the local split-K / block-slab
+ * reduction happens in the copy-in phase, so no separate reduction launch precedes the
+ * exchange */
+struct XarIn {
+    const float4 *src[HPNN_XAR_MAX_SEGS];
+    long stride4[HPNN_XAR_MAX_SEGS];
+    long end4[HPNN_XAR_MAX_SEGS]; /* exclusive prefix ends in float4 */
+    int S[HPNN_XAR_MAX_SEGS];
+    int nseg;
+};
+
+__device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
+    int j = 0;
+    while (j + 1 < in.nseg && i >= in.end4[j]) j++;
+    const long li = i - (j ? in.end4[j - 1] : 0);
+    const float4 *p = in.src[j] + li;
+    const long st = in.stride4[j];
+    float4 a = p[0];
+    if (in.S[j] > 1) {
+        float4 b = p[st];
+        int s = 2;
+        for (; s + 1 < in.S[j]; s += 2) {
+            const float4 x = p[(long)s * st], y = p[(long)(s + 1) * st];
+            a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+            b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+        }
+        if (s < in.S[j]) {
+            const float4 x = p[(long)s * st];
+            a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        }
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    return a;
+}
+
+__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in,
                                                   float4 *__restrict__ out, long n4, unsigned long long timeout) {
     const int b = blockIdx.x;
     Signal *me = P.sig[rank];
@@ -86,7 +122,7 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
     const long per = (n4 + gridDim.x - 1) / gridDim.x;
     const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
     float4 *mine = P.buf[rank];
-    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = in[i];
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
     xbarrier(P, rank, world, b, e, false, timeout);
     for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         float4 v[HPNN_XAR_MAX_RANKS];
@@ -182,18 +218,48 @@ extern "C" int hpnn_xar_open(hpnn_xar *c, const void *all) {
 
 extern "C" size_t hpnn_xar_max_bytes(const hpnn_xar *c) { return c ? c->max_bytes : 0; }
 
-extern "C" int hpnn_xar_all_reduce_f32(hpnn_xar *c, const float *in, float *out, long count, hipStream_t stream) {
+static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipStream_t stream) {
     if (!c || count <= 0 || (count & 3) || (size_t)count * 4 > c->max_bytes) return -1;
-    if (((uintptr_t)in | (uintptr_t)out) & 15) return -1;
+    if ((uintptr_t)out & 15) return -1;
     for (int p = 0; p < c->world; p++)
         if (!c->peers.buf[p]) return -3; /* not opened */
     const long n4 = count / 4;
-    long blocks = (n4 + 511) / 512; /* ~2 float4 per thread per slice */
+    long blocks = (n4 + 127) / 128; /* ~half a float4 per thread: many CUs share the slab reads */
     if (blocks > HPNN_XAR_MAX_BLOCKS) blocks = HPNN_XAR_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(xar_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank, c->world,
-                       (const float4 *)in, (float4 *)out, n4, c->timeout);
+    hipLaunchKernelGGL(xar_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank, c->world, in,
+                       (float4 *)out, n4, c->timeout);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_xar_all_reduce_f32(hpnn_xar *c, const float *in, float *out, long count, hipStream_t stream) {
+    if ((uintptr_t)in & 15) return -1;
+    XarIn x = {};
+    x.src[0] = (const float4 *)in;
+    x.stride4[0] = 0;
+    x.end4[0] = count / 4;
+    x.S[0] = 1;
+    x.nseg = 1;
+    return xar_launch(c, x, out, count, stream);
+}
+
+extern "C" int hpnn_xar_all_reduce_slabs_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
+                                             hipStream_t stream) {
+    if (!segs || nseg < 1 || nseg > HPNN_XAR_MAX_SEGS) return -1;
+    XarIn x = {};
+    long tot = 0;
+    for (int j = 0; j < nseg; j++) {
+        const hpnn_xar_seg &g = segs[j];
+        if (!g.src || g.S < 1 || g.count <= 0 || (g.count & 3) || (g.stride & 3) || ((uintptr_t)g.src & 15))
+            return -1;
+        x.src[j] = (const float4 *)g.src;
+        x.stride4[j] = g.stride / 4;
+        x.S[j] = g.S;
+        tot += g.count;
+        x.end4[j] = tot / 4;
+    }
+    x.nseg = nseg;
+    return xar_launch(c, x, out, tot, stream);
 }
 
 extern "C" int hpnn_xar_status(hpnn_xar *c) {

@@ -13,6 +13,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <tuple>
 #include <pybind11/stl.h>
 
 #include "../gpu/kernels.h"
@@ -214,6 +215,13 @@ PYBIND11_MODULE(_native, m) {
     m.def("xar_all_reduce_f32", [](uptr c, uptr in, uptr out, long count, uptr stream) {
         check(hpnn_xar_all_reduce_f32((hpnn_xar *)c, (const float *)P(in), (float *)P(out), count, S(stream)),
               "xar_all_reduce_f32");
+    });
+    m.def("xar_all_reduce_slabs_f32", [](uptr c, std::vector<std::tuple<uptr, long, int, long>> segs, uptr out,
+                                         uptr stream) {
+        std::vector<hpnn_xar_seg> v;
+        for (auto &t : segs) v.push_back({(const float *)P(std::get<0>(t)), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+        check(hpnn_xar_all_reduce_slabs_f32((hpnn_xar *)c, v.data(), (int)v.size(), (float *)P(out), S(stream)),
+              "xar_all_reduce_slabs_f32");
     });
     m.def("xar_status", [](uptr c) { return hpnn_xar_status((hpnn_xar *)c); });
     m.def("xar_destroy", [](uptr c) { hpnn_xar_destroy((hpnn_xar *)c); });

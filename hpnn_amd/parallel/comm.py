@@ -47,15 +47,23 @@ class NativeComm:
     Bootstrap: rank 0 of `group` creates the RCCL unique id, torch.distributed
     broadcasts it, every rank calls ncclCommInitRank through libhpnn."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, rccl=True):
+        """rccl=False: no RCCL communicator, only the one-shot xGMI all-reduce (used to
+        exercise the data-parallel step with several processes on ONE GPU, where RCCL
+        refuses duplicate devices)"""
         if not dist.is_initialized():
             raise RuntimeError("NativeComm needs an initialised torch.distributed process group")
         n = native()
         self.h = 0
+        self.xar = 0
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = torch.cuda.current_device() if device is None else int(device)
+        if not rccl:
+            if self.world < 2 or not self._attach_xar(int(os.environ.get("HPNN_XAR_MAX_BYTES", str(4 << 20)))):
+                raise RuntimeError("xGMI all-reduce unavailable")
+            return
         uid = torch.zeros(ID_BYTES, dtype=torch.uint8)
         if self.rank == 0:
             uid = torch.tensor(list(n.comm_unique_id()), dtype=torch.uint8)
@@ -102,7 +110,9 @@ class NativeComm:
                 n.xar_destroy(x)
             return False
         self.xar = x
-        n.comm_set_xar(self.h, x, max_bytes)
+        self.xar_max = max_bytes
+        if self.h:
+            n.comm_set_xar(self.h, x, max_bytes)
         return True
 
     # -- collectives on the current stream ------------------------------------------
@@ -128,14 +138,31 @@ class NativeComm:
     def all_reduce_async(self, t):
         """sum all-reduce of t on the side stream, after the work already on the current
         stream; overlaps whatever is enqueued next until join()"""
+        if not self.h:  # xGMI-only: in order on the current stream
+            native().xar_all_reduce_f32(self.xar, t.data_ptr(), t.data_ptr(), t.numel(), _stream())
+            return
         native().comm_all_reduce_async(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], _stream())
 
     def join(self):
-        native().comm_join(self.h, _stream())
+        if self.h:
+            native().comm_join(self.h, _stream())
+
+    def all_reduce_slabs(self, out, segs):
+        """out = sum over ranks of [seg_0 | seg_1 | ...] where segment j = (slabs, S, n) is
+        the local sum of the S slabs slabs[s, :n]: split-K reduction and exchange in ONE
+        launch (xGMI all-reduce, include/libhpnn/xar.h), on the current stream"""
+        native().xar_all_reduce_slabs_f32(self.xar, [(t.data_ptr(), t.stride(0), S, n) for t, S, n in segs],
+                                          out.data_ptr(), _stream())
+        return out
 
     # -- failure detection ----------------------------------------------------------
     def check(self):
-        """raise if the communicator saw an asynchronous error (peer died, link down)"""
+        """raise if the communicator saw an asynchronous error (peer died, link down) or an
+        xGMI all-reduce barrier timed out"""
+        if not self.h:
+            if self.xar and native().xar_status(self.xar) != 0:
+                raise RuntimeError(f"xGMI all-reduce barrier timed out on rank {self.rank}")
+            return
         if native().comm_check(self.h) != 0:
             native().comm_abort(self.h)
             raise RuntimeError(f"RCCL communicator failed on rank {self.rank}")
@@ -143,11 +170,18 @@ class NativeComm:
     def all_ok(self, ok=True):
         """MIN over ranks of ok (the collective replacement of the reference's MPI
         bail-out after a failed kernel load, ann.c:237-249)"""
+        if not self.h:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            if dist.get_backend(self.group) == "nccl":
+                t = t.cuda(self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            return bool(t.item())
         return bool(native().comm_all_ok(self.h, 1 if ok else 0, _stream()))
 
     def close(self):
         if getattr(self, "xar", 0):
-            native().comm_set_xar(self.h, 0, 0)
+            if self.h:
+                native().comm_set_xar(self.h, 0, 0)
             native().xar_destroy(self.xar)
             self.xar = 0
         if self.h:

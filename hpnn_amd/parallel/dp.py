@@ -21,7 +21,8 @@ from .. import ops
 
 class DataParallel:
     """comm: "auto" (libhpnn's native RCCL communicator when the model is on a GPU and the
-    group runs on the nccl backend, else torch.distributed), "native" or "torch"."""
+    group runs on the nccl backend, else torch.distributed), "native", "torch", or "xar"
+    (xGMI all-reduce only, no RCCL: several ranks on one GPU in tests)."""
 
     def __init__(self, model, group=None, bucket_bytes=256 * 1024, comm="auto"):
         self.m = model
@@ -31,7 +32,10 @@ class DataParallel:
         self.buckets = self._plan(bucket_bytes)
         self.native = None
         on_gpu = getattr(model, "device", torch.device("cpu")).type == "cuda"
-        if self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
+        if self.active and on_gpu and comm == "xar":
+            from .comm import NativeComm
+            self.native = NativeComm(group, device=model.device.index, rccl=False)
+        elif self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
             from .comm import NativeComm
             self.native = NativeComm(group, device=model.device.index)
 
@@ -59,8 +63,12 @@ class DataParallel:
             for t in (self.m.W32[l], self.m.V32[l]):
                 if t is None:
                     continue
-                if self.native is not None:
+                if self.native is not None and self.native.h:
                     self.native.broadcast(t, root=dist.get_group_rank(self.group, src) if self.group else src)
+                elif dist.get_backend(self.group) != "nccl" and t.is_cuda:
+                    c = t.cpu()
+                    dist.broadcast(c, src, group=self.group)
+                    t.copy_(c)
                 else:
                     dist.broadcast(t, src, group=self.group)
         self.m.refresh_bf16()
@@ -88,11 +96,29 @@ class DataParallel:
         end = m.G[hi].data_ptr() - m.grad_flat.data_ptr() + m.G[hi].numel() * 4
         return m.grad_flat[start // 4:end // 4]
 
+    def _fused_xgmi_step(self, X, labels, T, n_valid, lr, alpha):
+        """MNIST fused path on the xGMI all-reduce: 4 launches per step -- fused front, G0
+        GEMM (+ first [G1|G2] reduction pass on its tail workgroups), ONE all-reduce whose
+        copy-in phase also sums the local split-K slabs of G0 and the [G1|G2] groups, the
+        update of every layer from the reduced gradients"""
+        m = self.m
+        m._fused_front(X, labels, T, n_valid)
+        groups = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
+        ops.gemm_tn_reduce(m.D[0], X, m.S[0], m.slab[0], m.midslab, m.mid_groups, groups)
+        n0 = m.G[0].numel()
+        self.native.all_reduce_slabs(m.grad_flat, [(m.slab[0].view(m.S[0], n0), m.S[0], n0),
+                                                   (groups, m.mid_groups, m.grad_flat.numel() - n0)])
+        m.update_all(lr, alpha, 1.0 / (n_valid * self.world), m.G)
+
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         m = self.m
         n_valid = m.Bp if n_valid is None else n_valid
         if not self.active:
             return m.train_step(X, labels=labels, T=T, n_valid=n_valid, lr=lr, alpha=alpha)
+        if (self.native is not None and self.native.xar and getattr(m, "fused_mode", None) == "x"
+                and m.grad_flat.numel() * 4 <= self.native.xar_max
+                and m.grad_flat.numel() - m.G[0].numel() == ops.MLP3_SLAB):
+            return self._fused_xgmi_step(X, labels, T, n_valid, lr, alpha)
         works = []
         done = set()
 

@@ -31,7 +31,8 @@ extern "C" {
 #endif
 
 #define HPNN_XAR_MAX_RANKS 8
-#define HPNN_XAR_MAX_BLOCKS 80
+#define HPNN_XAR_MAX_BLOCKS 256
+#define HPNN_XAR_MAX_SEGS 4
 #define HPNN_XAR_HANDLE_BYTES 128
 
 typedef struct hpnn_xar hpnn_xar;
@@ -45,6 +46,16 @@ size_t hpnn_xar_max_bytes(const hpnn_xar *c);
 /* out = sum over ranks of in (float32, count % 4 == 0, count * 4 <= max_bytes);
  * in == out allowed */
 int hpnn_xar_all_reduce_f32(hpnn_xar *c, const float *in, float *out, long count, hipStream_t stream);
+/* out = sum over ranks of [seg_0 | seg_1 | ...], segment j being the LOCAL sum of S_j
+ * slabs src_j + s * stride_j (count_j floats each, multiples of 4): the split-K slab
+ * reduction of the weight gradients happens inside the all-reduce's copy-in phase */
+typedef struct {
+    const float *src;
+    long stride; /* floats between slabs */
+    int S;       /* slabs */
+    long count;  /* floats */
+} hpnn_xar_seg;
+int hpnn_xar_all_reduce_slabs_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out, hipStream_t stream);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
 int hpnn_xar_status(hpnn_xar *c);
 void hpnn_xar_destroy(hpnn_xar *c);

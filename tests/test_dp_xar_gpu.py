@@ -1,0 +1,102 @@
+"""The data-parallel MNIST step on the one-shot xGMI all-reduce with two real processes
+(both on the box's single MI355X; RCCL refuses two ranks on one device, so the ranks run
+the xGMI-only communicator, comm="xar").  This is the exact step bench.py runs at N > 1:
+fused front, G0 GEMM with the [G1|G2] reduction on its tail workgroups, ONE all-reduce
+that also sums the local split-K slabs, the update.  Checked: both ranks end with
+bit-identical weights, equal (to FP32 summation order) to one process training on the
+concatenated batch; a HIP-graph-captured step gives the same result as eager steps."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+SIZES = [784, 128, 64, 10]
+B = 8192
+
+
+def _data(rank, step):
+    g = torch.Generator().manual_seed(100 * rank + step)
+    return torch.rand(B, SIZES[0], generator=g), torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
+
+
+def _worker(rank, world, port, graph, q):
+    try:
+        os.environ["LOCAL_WORLD_SIZE"] = str(world)
+        os.environ["HPNN_XAR_TIMEOUT_MS"] = "2000"
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        from hpnn_amd.models import MLP
+        from hpnn_amd.parallel import DataParallel
+        dev = torch.device("cuda", 0)
+        m = MLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=3)
+        dp = DataParallel(m, comm="xar")
+        assert dp.native is not None and dp.native.xar and m.fused_mode == "x"
+        dp.broadcast_parameters()
+        batches = []
+        for step in range(3):
+            x, lab = _data(rank, step)
+            batches.append((m.prepare_input(x.to(dev)), lab.to(dev)))
+        if graph:
+            # step 0 eager, steps 1-2 from one captured graph replayed twice over the same inputs
+            dp.train_step(batches[0][0], labels=batches[0][1], lr=0.05, alpha=0.2)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g):
+                    dp.train_step(batches[1][0], labels=batches[1][1], lr=0.05, alpha=0.2)
+            torch.cuda.current_stream().wait_stream(s)
+            g.replay()
+            g.replay()
+        else:
+            for step in (0, 1, 1):
+                dp.train_step(batches[step][0], labels=batches[step][1], lr=0.05, alpha=0.2)
+        torch.cuda.synchronize()
+        dp.check()
+        W = torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
+        q.put((rank, W))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def _reference():
+    from hpnn_amd.models import MLP
+    dev = torch.device("cuda", 0)
+    m = MLP(SIZES, "SNN", batch=2 * B, device=dev, momentum=True, seed=3)
+    for step in (0, 1, 1):
+        xs, ls = zip(*[_data(r, step) for r in range(2)])
+        X = m.prepare_input(torch.cat(xs).to(dev))
+        m.train_step(X, labels=torch.cat(ls).to(dev), lr=0.05, alpha=0.2)
+    torch.cuda.synchronize()
+    return torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, graph, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=110) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    for r in (0, 1):
+        assert isinstance(res[r], torch.Tensor), res[r]
+    assert torch.equal(res[0], res[1])  # deterministic, identical on every rank
+    ref = _reference()
+    err = (res[0] - ref).abs().max().item()
+    assert err < 2e-6, err
