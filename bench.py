@@ -85,6 +85,18 @@ def main():
             graphs[n] = g
         return graphs[n]
 
+    # one eager step first: when the xGMI all-reduce is in use, every rank checks that its
+    # barriers completed and all ranks agree, else all fall back to RCCL before anything
+    # is captured or timed
+    step(0)
+    torch.cuda.synchronize()
+    if dp.native is not None and dp.native.xar:
+        if not dp.all_ok(dp.native.xar_healthy()):
+            if rank == 0:
+                print("xGMI all-reduce barrier timed out on some rank; using RCCL", file=sys.stderr)
+            dp.native.detach_xar()
+            dp.broadcast_parameters()
+
     if use_graph:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -167,7 +179,10 @@ def main():
             "train_loss_mean": loss_sum / max(1, samples // world),
         }
         print(json.dumps(out))
-    if world > 1:
+    if dp.active:
+        dist.barrier()
+        if dp.native is not None:
+            dp.native.close()
         dist.destroy_process_group()
 
 

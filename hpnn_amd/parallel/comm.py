@@ -178,7 +178,22 @@ class NativeComm:
             return bool(t.item())
         return bool(native().comm_all_ok(self.h, 1 if ok else 0, _stream()))
 
+    def xar_healthy(self):
+        """False when an xGMI all-reduce barrier of this rank timed out"""
+        return not self.xar or native().xar_status(self.xar) == 0
+
+    def detach_xar(self):
+        """stop using the xGMI all-reduce (every rank must call it: RCCL takes over).  The
+        buffers stay mapped until close(): a peer may still be inside a timed-out call."""
+        if self.xar and self.h:
+            native().comm_set_xar(self.h, 0, 0)
+        self._xar_detached = self.xar
+        self.xar = 0
+
     def close(self):
+        if getattr(self, "_xar_detached", 0):
+            native().xar_destroy(self._xar_detached)
+            self._xar_detached = 0
         if getattr(self, "xar", 0):
             if self.h:
                 native().comm_set_xar(self.h, 0, 0)
