@@ -94,7 +94,7 @@ __device__ __forceinline__ void glds_piece(const char *gbase, size_t ld_bytes, c
 }
 
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int EPI, bool CF32>
-__global__ __launch_bounds__(256) void gemm_nt_pipe_kernel(const __bf16 *__restrict__ A, int lda,
+__global__ __launch_bounds__(WM * WN * 64) void gemm_nt_pipe_kernel(const __bf16 *__restrict__ A, int lda,
                                                            const __bf16 *__restrict__ B, int ldb,
                                                            void *__restrict__ C, int ldc,
                                                            const __bf16 *__restrict__ aux, int ldaux, int K,
@@ -109,9 +109,10 @@ __global__ __launch_bounds__(256) void gemm_nt_pipe_kernel(const __bf16 *__restr
     /* every wave issues exactly LPS LDS-DMA loads per stage (a wave short of work
      * re-issues the last piece: same bytes to the same place), so one counted
      * vmcnt is exact for all waves */
-    constexpr int LPS = (PIECES + 3) / 4;
+    constexpr int NW = WM * WN; /* waves per workgroup (4, or 8 for the 256x256 tile) */
+    constexpr int LPS = (PIECES + NW - 1) / NW;
     constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
-    static_assert(WM * WN == 4 && FM >= 1 && FN >= 1, "wave tiling");
+    static_assert((NW == 4 || NW == 8) && FM >= 1 && FN >= 1, "wave tiling");
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_nt_pipe_kernel(const __bf16 *__restr
         const char *ga = Ag + (size_t)kt * RB, *gb = Bg + (size_t)kt * RB;
 #pragma unroll
         for (int i = 0; i < LPS; i++) {
-            int c = wave + 4 * i;
+            int c = wave + NW * i;
             c = c < PIECES ? c : PIECES - 1;
             if (c < A_PIECES) glds_piece<BK>(ga, lda_b, sa + c * 1024, c * ROWS_PER_PIECE, lane);
             else glds_piece<BK>(gb, ldb_b, sb + (c - A_PIECES) * 1024, (c - A_PIECES) * ROWS_PER_PIECE, lane);
@@ -246,8 +247,8 @@ __device__ __forceinline__ void tn_tail_reduce(const TnTail &t, int v) {
     ((f32x4 *)(t.out + (long)g * t.ostride))[e] = (a0 + a1) + (a2 + a3);
 }
 
-template <int TM, int TN, int BKR, int STAGES>
-__global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
+template <int TM, int TN, int BKR, int STAGES, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_tn_pipe_kernel(const __bf16 *__restrict__ D, int ldd,
                                                            const __bf16 *__restrict__ H, int ldh,
                                                            float *__restrict__ slab, int ldg, int N, int units,
                                                            int splits, int tiles_n, int tiles, int xcd_map,
@@ -256,17 +257,18 @@ __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restr
         tn_tail_reduce(tail, (int)blockIdx.x - tiles * splits);
         return;
     }
-    constexpr int WTM = TM / 2, WTN = TN / 2;
+    constexpr int NW = WM * WN; /* 4 waves (2 x 2), or 8 (2 x 4) for the 256x256 tile */
+    constexpr int WTM = TM / WM, WTN = TN / WN;
     constexpr int FM = WTM / 16, FN = WTN / 16;
     constexpr int H_PIECES = (TM / 32) * (BKR / 16), D_PIECES = (TN / 32) * (BKR / 16);
     constexpr int PIECES = H_PIECES + D_PIECES;
-    constexpr int LPS = (PIECES + 3) / 4;
+    constexpr int LPS = (PIECES + NW - 1) / NW;
     constexpr int H_BYTES = BKR * TM * 2, STAGE = BKR * (TM + TN) * 2;
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     /* XCD-aware order: workgroups are dealt round-robin to the 8 XCDs in dispatch order;
      * put all output tiles of one batch slice on the same XCD, back to back, so the
      * slice's D (shared by every tile of the slice) is fetched once into that XCD's L2 */
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(256) void gemm_tn_pipe_kernel(const __bf16 *__restr
         const char *gh = Hg + (size_t)kt * BKR * ldh_b, *gd = Dg + (size_t)kt * BKR * ldd_b;
 #pragma unroll
         for (int i = 0; i < LPS; i++) {
-            int c = wave + 4 * i;
+            int c = wave + NW * i;
             c = c < PIECES ? c : PIECES - 1;
             if (c < H_PIECES) glds_tn_piece<BKR>(gh, ldh_b, sh, c, lane);
             else glds_tn_piece<BKR>(gd, ldd_b, sd, c - H_PIECES, lane);
@@ -363,10 +365,27 @@ int launch_nt_bn(const void *A, int lda, const void *B, int ldb, void *C, int ld
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* large GEMMs: 256x256 tiles, 8 waves (2 x 4, each 128x64), 2-stage ring of 64 KiB
+ * stages, one workgroup per CU (HPNN_NT_BIG=0 disables).  8192x4096x4096: 974 / 1004
+ * TFLOP/s (forward / backward epilogue) vs 870 / 918 with the 128x128 4-wave tile;
+ * measured and rejected: BK=32 with 4 stages (913), s_setprio around the MFMA block (910) */
+template <int EPI, bool CF32>
+int launch_nt_big(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
+                  int N, int K, hipStream_t s) {
+    constexpr int BM = 256, BN = 256;
+    const int tiles_n = N / BN, tiles_m = M / BM;
+    hipLaunchKernelGGL((gemm_nt_pipe_kernel<BM, BN, 64, 2, 4, 2, EPI, CF32>), dim3(tiles_m * tiles_n), dim3(512), 0, s,
+                       (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 template <int EPI, bool CF32>
 int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
                   int N, int K, hipStream_t s) {
     const bool k64 = (K % 64) == 0;
+    static const int big_off = [] { const char *e = getenv("HPNN_NT_BIG"); return e && e[0] == '0'; }();
+    if (!big_off && k64 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 && K >= 512)
+        return launch_nt_big<EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s);
 #define HPNN_NT(BN_)                                                                                  \
     return k64 ? launch_nt_bn<BN_, 64, EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s)      \
                : launch_nt_bn<BN_, 32, EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s)
@@ -401,11 +420,27 @@ int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int
     return launch_tn_t<TM, 32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
 }
 
+/* large weight gradients (>= 256 output tiles of 256x256, one split): 8-wave 256x256 tiles,
+ * 4-stage ring of 32-row stages (128 KiB), one workgroup per CU (HPNN_TN_BIG=0 disables) */
+int launch_tn_big(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
+                  int splits, hipStream_t s, const TnTail &t) {
+    constexpr int TM = 256, TN = 256, BKR = 32, ST = 4;
+    const int tiles_n = N / TN, tiles_m = M / TM, tiles = tiles_m * tiles_n;
+    const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST, 2, 4>), dim3(tiles * splits + t.blocks), dim3(512), 0, s,
+                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, Bt / 64, splits, tiles_n, tiles,
+                       xcd_map, t);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
                      int splits, hipStream_t stream, const TnTail &t) {
     if (N <= 0 || M <= 0 || Bt <= 0 || splits <= 0) return -1;
     if (N % 32 || M % 32 || Bt % 64 || splits > Bt / 64) return -2;
     if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
+    static const int big_off = [] { const char *e = getenv("HPNN_TN_BIG"); return e && e[0] == '0'; }();
+    if (!big_off && N % 256 == 0 && M % 256 == 0 && (long)(N / 256) * (M / 256) * splits >= 256)
+        return launch_tn_big(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);

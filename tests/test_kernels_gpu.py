@@ -48,10 +48,10 @@ def test_gemm_nt_weight_stationary(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 2048, 512), (8192, 1024, 640), (4352, 4096, 576)])
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 512), (8192, 2048, 640), (4352, 4096, 576)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
 def test_gemm_nt_big_tile(gpu, M, N, K, epi):
-    """shapes with >= 256 tiles of 256x128 take the large-tile kernel (3-stage 144 KiB ring);
+    """shapes with >= 256 tiles of 256x256 take the 8-wave large-tile kernel (128 KiB ring);
     padded row strides on every operand"""
     torch.manual_seed(M + N + K + epi)
     A = _rand(M, K + 64).bfloat16()[:, :K]
@@ -100,6 +100,20 @@ def test_gemm_tn(gpu, Bt, N, M, S):
     c = Bt // S
     R0 = ops.ref_gemm_tn(D[:c], H[:c])
     assert (slab[0] - R0).abs().max().item() <= 1e-3 * R0.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("Bt,N,M,S", [(1024, 4096, 4096, 1), (2048, 2048, 4096, 2), (640, 4096, 2048, 3)])
+def test_gemm_tn_big_tile(gpu, Bt, N, M, S):
+    """>= 256 tiles of 256x256 take the 8-wave large-tile kernel; padded strides, uneven splits"""
+    torch.manual_seed(Bt + N + M)
+    D = (_rand(Bt, N + 32) + torch.arange(N + 32, device="cuda")[None, :] * 0.001).bfloat16()[:, :N]
+    H = _rand(Bt, M + 64).bfloat16()[:, :M]
+    slab = ops.gemm_tn(D, H, splits=S)
+    R = ops.ref_gemm_tn(D, H)
+    assert (slab.sum(0) - R).abs().max().item() <= 1e-3 * R.abs().max().item() + 1e-4
+    a, b = ops.split_rows(Bt, S)[S - 1]
+    R1 = ops.ref_gemm_tn(D[a:b], H[a:b])
+    assert (slab[S - 1] - R1).abs().max().item() <= 1e-3 * R1.abs().max().item() + 1e-4
 
 
 @pytest.mark.parametrize("Bt,S", [(640, 3), (65536 // 8, 12), (1024, 16)])
