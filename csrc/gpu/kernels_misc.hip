@@ -151,6 +151,88 @@ __global__ __launch_bounds__(256) void output_delta_rows_kernel(const float *__r
     block_reduce_store(my_loss, my_hit, loss_acc, correct);
 }
 
+/* wide outputs up to 64*NPL classes (RRUFF: 230): one wave per sample row, the row kept in
+ * registers (NPL values per lane) so Z is read once instead of three times, and one row
+ * per wave (the grid covers the batch): the three dependent wave reductions of a row no
+ * longer serialize over many rows per wave */
+template <int NPL>
+__global__ __launch_bounds__(256) void output_delta_reg_kernel(const float *__restrict__ Z, int ldz,
+                                                               const float *__restrict__ T, int ldt,
+                                                               const int *__restrict__ labels, float t_hi, float t_lo,
+                                                               __bf16 *__restrict__ D, int ldd, float *__restrict__ O,
+                                                               int ldo, float *__restrict__ loss_acc,
+                                                               unsigned int *__restrict__ correct, int B, int n_valid,
+                                                               int n_out, int type) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    for (int row = blockIdx.x * 4 + wave; row < B; row += gridDim.x * 4) {
+        const bool valid = row < n_valid;
+        const int lab = (labels && valid) ? labels[row] : -1;
+        float z[NPL];
+#pragma unroll
+        for (int j = 0; j < NPL; j++) {
+            const int c = lane + 64 * j;
+            z[j] = c < n_out ? Z[(size_t)row * ldz + c] : -INFINITY;
+        }
+        float inv = 0.f, zmax = 0.f;
+        if (type == 2) {
+            zmax = z[0];
+#pragma unroll
+            for (int j = 1; j < NPL; j++) zmax = fmaxf(zmax, z[j]);
+            zmax = wave_max(zmax);
+            float denom = 0.f;
+#pragma unroll
+            for (int j = 0; j < NPL; j++)
+                if (lane + 64 * j < n_out) denom += __expf(z[j] - zmax);
+            denom = wave_sum(denom);
+            /* reference: e^{z-1} / (TINY + sum e^{z-1}); shifted by m=zmax */
+            denom += __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
+            inv = 1.0f / denom;
+        }
+        float bo = -INFINITY, bt = -INFINITY;
+        int io = -1, it = -1;
+        float l = 0.f;
+#pragma unroll
+        for (int j = 0; j < NPL; j++) {
+            const int c = lane + 64 * j;
+            float d = 0.f;
+            if (c < n_out) {
+                float o;
+                if (type == 2) o = __expf(z[j] - zmax) * inv;
+                else if (type == 0) o = 2.0f / (1.0f + __expf(-z[j])) - 1.0f;
+                else o = z[j];
+                if (valid) {
+                    const float t = labels ? (c == lab ? t_hi : t_lo) : T[(size_t)row * ldt + c];
+                    if (type == 2) {
+                        if (o > 0.f) l += t * logf(o + TINY);
+                        d = t - o;
+                    } else if (type == 0) {
+                        l += (t - o) * (t - o);
+                        d = (t - o) * (-0.5f * (o * o - 1.0f));
+                    } else {
+                        l += (t - o) * (t - o);
+                        d = t - o;
+                    }
+                    if (o > bo) { bo = o; io = c; }
+                    if (t > bt) { bt = t; it = c; }
+                }
+                if (O) O[(size_t)row * ldo + c] = o;
+            }
+            if (c < ldd) D[(size_t)row * ldd + c] = (__bf16)d;
+        }
+        for (int c = 64 * NPL + lane; c < ldd; c += 64) D[(size_t)row * ldd + c] = (__bf16)0.f;
+        l = wave_sum(l);
+        wave_argmax(bo, io);
+        wave_argmax(bt, it);
+        if (valid && lane == 0) {
+            my_loss += (type == 2) ? -l / (float)n_out : 0.5f * l;
+            my_hit += (io == it) ? 1u : 0u;
+        }
+    }
+    block_reduce_store(my_loss, my_hit, loss_acc, correct);
+}
+
 /* wide outputs: one WAVE per sample row, grid-stride */
 __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restrict__ Z, int ldz,
                                                            const float *__restrict__ T, int ldt,
@@ -462,8 +544,19 @@ extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ld
         const int grid = (B + 255) / 256 < 256 ? (B + 255) / 256 : 256;
         hipLaunchKernelGGL(output_delta_rows_kernel<32>, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels,
                            t_hi, t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    } else if (n_out <= 256) {
+        /* one row per wave: the grid covers the batch (up to 16 waves per CU) */
+        const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
+#define HPNN_OD(NPL_)                                                                                              \
+    hipLaunchKernelGGL(output_delta_reg_kernel<NPL_>, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi, \
+                       t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type)
+        if (n_out <= 64) HPNN_OD(1);
+        else if (n_out <= 128) HPNN_OD(2);
+        else if (n_out <= 192) HPNN_OD(3);
+        else HPNN_OD(4);
+#undef HPNN_OD
     } else {
-        const int grid = (B + 3) / 4 < 256 ? (B + 3) / 4 : 256;
+        const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
         hipLaunchKernelGGL(output_delta_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
                            t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
     }
