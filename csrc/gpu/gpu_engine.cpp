@@ -50,6 +50,9 @@ struct GpuModel {
     double *W[16] = {0};
     double *dW[16] = {0};
     double *x = nullptr, *t = nullptr, *out = nullptr, *result = nullptr, *scratch = nullptr;
+    double *xch = nullptr;     /* cooperative online kernel: exchange vectors + partials */
+    unsigned int *ctl = nullptr;
+    long xch_bytes = 0;
     bool device_newer = false; /* device weights not yet copied to host */
     bool host_newer = true;    /* host weights not yet uploaded         */
 };
@@ -71,6 +74,8 @@ void free_model(GpuModel *g) {
     if (g->out) hpnn_dev_free(g->out);
     if (g->result) hpnn_dev_free(g->result);
     if (g->scratch) hpnn_dev_free(g->scratch);
+    if (g->xch) hpnn_dev_free(g->xch);
+    if (g->ctl) hpnn_dev_free(g->ctl);
     delete g;
 }
 
@@ -213,7 +218,23 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
     a.forward_only = 0;
     hipMemcpyAsync(g->x, in, sizeof(double) * k->n_inputs, hipMemcpyHostToDevice, s);
     hipMemcpyAsync(g->t, out, sizeof(double) * k->n_outputs, hipMemcpyHostToDevice, s);
-    if (hpnn_online_launch(&a, s) != 0) {
+    /* layers wide enough to spread over many CUs: the cooperative kernel (rows dealt to
+     * resident workgroups), else the single-workgroup kernel */
+    const int grid = hpnn_online_coop_grid(&a);
+    if (grid > 0) {
+        const long need = hpnn_online_coop_xch_bytes(&a, grid);
+        if (need > g->xch_bytes) {
+            if (g->xch) hpnn_dev_free(g->xch);
+            g->xch = nullptr;
+            g->xch_bytes = 0;
+            if (hpnn_dev_malloc(&g->xch, (size_t)need) != hipSuccess) return 0.0;
+            g->xch_bytes = need;
+        }
+        if (!g->ctl && hpnn_dev_malloc(&g->ctl, HPNN_ONLINE_CTL_BYTES) != hipSuccess) return 0.0;
+        a.xch = g->xch;
+        a.ctl = g->ctl;
+    }
+    if ((grid > 0 ? hpnn_online_coop_launch(&a, grid, s) : hpnn_online_launch(&a, s)) != 0) {
         NN_ERROR(stderr, "online kernel launch failed\n");
         return 0.0;
     }
@@ -221,6 +242,12 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
     hipMemcpyAsync(res, g->result, sizeof(res), hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(k->output.vec, g->out, sizeof(double) * k->n_outputs, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
+    if (grid > 0 && hpnn_online_coop_status(&a) != 0) {
+        NN_ERROR(stderr, "cooperative online kernel: a grid barrier timed out\n");
+        g->device_newer = true;
+        if (ok) *ok = FALSE;
+        return 0.0;
+    }
     g->device_newer = true;
     if (n_iter) *n_iter = (UINT)res[2];
     if (ok) *ok = res[3] != 0.0;

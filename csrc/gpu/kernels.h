@@ -167,7 +167,22 @@ typedef struct {
     double *result;    /* [0]=dEp [1]=init_err [2]=iter [3]=ok [4]=first_ok */
     int use_lds;
     int forward_only;
+    /* multi-workgroup (cooperative) variant, online.hip: exchange vectors + partials
+     * (hpnn_online_coop_xch_bytes) and the control words (HPNN_ONLINE_CTL_BYTES) */
+    double *xch;
+    unsigned int *ctl;
 } hpnn_online_args;
+
+#define HPNN_ONLINE_CTL_BYTES 256
+/* grid of the cooperative online kernel (0: not applicable -> single-workgroup kernel) */
+int hpnn_online_coop_grid(const hpnn_online_args *a);
+long hpnn_online_coop_xch_bytes(const hpnn_online_args *a, int grid);
+/* one sample on `grid` workgroups (all resident): every layer's rows are spread over the
+ * workgroups, vectors and delta partials are exchanged through write-through stores and
+ * a counter barrier; returns 0, or < 0 (launch error) */
+int hpnn_online_coop_launch(const hpnn_online_args *a, int grid, hipStream_t stream);
+/* 0, or -1 when a barrier of the last cooperative launch timed out (ctl read back) */
+int hpnn_online_coop_status(const hpnn_online_args *a);
 
 int hpnn_online_launch(const hpnn_online_args *a, hipStream_t stream);
 /* bytes of vector storage the online kernel needs */

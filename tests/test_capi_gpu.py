@@ -36,14 +36,19 @@ def _data(d, n, n_in, n_out, snn, seed=0):
         formats.write_sample(os.path.join(d, f"s{i:05d}.txt"), x, t)
 
 
-@pytest.mark.parametrize("net,train", [("SNN", "BP"), ("ANN", "BPM")])
-def test_online_gpu_matches_cpu(tmp_path, net, train):
-    """FP64 persistent online kernel == FP64 CPU engine (reference semantics)."""
+@pytest.mark.parametrize("net,train,dims", [("SNN", "BP", (40, [24, 16], 5)), ("ANN", "BPM", (40, [24, 16], 5)),
+                                            ("SNN", "BPM", (120, [64, 40], 10)), ("ANN", "BP", (90, [300], 10)),
+                                            ("ANN", "BPM", (70, [48, 200, 33], 7))])
+def test_online_gpu_matches_cpu(tmp_path, net, train, dims):
+    """FP64 online engines == FP64 CPU engine (reference semantics).  The small net runs the
+    single-workgroup kernel, the wider ones the cooperative multi-workgroup kernel (rows
+    dealt to resident workgroups, delta partials summed in workgroup order)."""
+    n_in, hid, n_out = dims
     for dev in ("cpu", "gpu"):
         d = str(tmp_path / dev)
-        _data(os.path.join(d, "samples"), 3, 40, 5, net == "SNN")
-        formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=5, inputs=40, hiddens=[24, 16],
-                           outputs=5, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
+        _data(os.path.join(d, "samples"), 3, n_in, n_out, net == "SNN")
+        formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=5, inputs=n_in, hiddens=hid,
+                           outputs=n_out, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
         out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, cpu=(dev == "cpu"))
         assert out.count("TRAINING FILE") == 3
     kc = formats.read_kernel(str(tmp_path / "cpu" / "kernel.opt"))["weights"]
