@@ -173,7 +173,7 @@ typedef struct {
     unsigned int *ctl;
 } hpnn_online_args;
 
-#define HPNN_ONLINE_CTL_BYTES 256
+#define HPNN_ONLINE_CTL_BYTES 1024
 /* grid of the cooperative online kernel (0: not applicable -> single-workgroup kernel) */
 int hpnn_online_coop_grid(const hpnn_online_args *a);
 long hpnn_online_coop_xch_bytes(const hpnn_online_args *a, int grid);

@@ -390,19 +390,28 @@ __device__ __forceinline__ double xget(const double *p, size_t i) {
 }
 
 /* counter barrier: every wave drains its write-through stores, one lane adds, one lane
- * polls until all G workgroups of this phase arrived (the counter is never reset inside a
- * launch; it is zeroed by the launcher's memset) */
+ * polls until all G workgroups of this phase arrived.  Arrivals are spread over 8
+ * counters on separate 64-byte lines (workgroup g adds to counter g % 8) so the adds do
+ * not serialize on one address; the poller sums the 8.  Counters are never reset inside a
+ * launch (zeroed by the launcher's memset); the timeout word is ctl[COOP_ERR]. */
+constexpr int COOP_SUB = 8, COOP_LINE = 16, COOP_ERR = COOP_SUB * COOP_LINE;
 __device__ __forceinline__ void coop_barrier(unsigned int *ctl, unsigned int target) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        gu32 *cnt = (gu32 *)ctl;
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gu32 *c = (gu32 *)ctl;
+        __hip_atomic_fetch_add(c + (blockIdx.x % COOP_SUB) * COOP_LINE, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        for (;;) {
+            unsigned int sum = 0;
+#pragma unroll
+            for (int k = 0; k < COOP_SUB; k++)
+                sum += __hip_atomic_load(c + k * COOP_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (sum >= target) break;
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > COOP_TIMEOUT) {
-                __hip_atomic_store((gu32 *)ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(c + COOP_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }
@@ -423,7 +432,8 @@ __device__ double cblock_sum(double v, double *red) {
 }
 
 /* same arithmetic as softmax_out / error_of / argmax_pair, on CNT threads */
-__device__ void c_softmax(double *o, int N, double *red) {
+template <class P>
+__device__ void c_softmax(P o, int N, double *red) {
     double part = 0.0;
     for (int j = threadIdx.x; j < N; j += CNT) {
         o[j] = exp(o[j] - 1.0);
@@ -434,7 +444,8 @@ __device__ void c_softmax(double *o, int N, double *red) {
     __syncthreads();
 }
 
-__device__ double c_error(const hpnn_online_args &a, const double *o, const double *t, double *red) {
+template <class P>
+__device__ double c_error(const hpnn_online_args &a, P o, P t, double *red) {
     const int N = a.N[a.L - 1];
     double part = 0.0;
     for (int j = threadIdx.x; j < N; j += CNT) {
@@ -448,7 +459,8 @@ __device__ double c_error(const hpnn_online_args &a, const double *o, const doub
     return a.type == 2 ? s * (-1.0 / (double)N) : 0.5 * s;
 }
 
-__device__ void c_argmax(int N, const double *o, const double *t, int *sidx, double *sval, int &max_p, int &p_trg) {
+template <class P>
+__device__ void c_argmax(int N, P o, P t, int *sidx, double *sval, int &max_p, int &p_trg) {
     double bv = -1.0;
     int bi = -1, ti = -1;
     for (int j = threadIdx.x; j < N; j += CNT) {
@@ -521,16 +533,18 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
     const int L = a.L, n_out = a.N[L - 1];
     const CoopLayout X = coop_layout(a, G);
     /* LDS: x | t | h[0][l] | h[1][l] | d[l] (full-length copies; d valid for own rows) */
-    double *xin = cs, *tt = cs + a.n_in;
-    double *h[2][16], *d[16];
+    /* LDS-typed pointers: ds_read / ds_write instead of flat accesses */
+    lds_d *const lb = (lds_d *)cs;
+    lds_d *xin = lb, *tt = lb + a.n_in;
+    lds_d *h[2][16], *d[16];
     {
         long off = a.n_in + n_out;
         for (int l = 0; l < L; l++) {
-            h[0][l] = cs + off;
+            h[0][l] = lb + off;
             off += a.N[l];
-            h[1][l] = cs + off;
+            h[1][l] = lb + off;
             off += a.N[l];
-            d[l] = cs + off;
+            d[l] = lb + off;
             off += a.N[l];
         }
     }
@@ -544,7 +558,7 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
     auto forward = [&](int gen) {
         for (int l = 0; l < L; l++) {
             const int N = a.N[l], M = a.M[l];
-            const double *in = l ? h[gen][l - 1] : xin;
+            const lds_d *in = l ? h[gen][l - 1] : xin;
             const bool use_act = (l < L - 1) || a.type == 0;
             for (int r = wave; g + (long)G * r < N; r += CNW) {
                 const int j = g + G * r;
@@ -577,7 +591,7 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
         iter++;
         /* ---- deltas with the pre-update weights ---- */
         {
-            const double *o = h[cur][L - 1];
+            const lds_d *o = h[cur][L - 1];
             for (int j = threadIdx.x; j < n_out; j += CNT) {
                 const double diff = tt[j] - o[j];
                 d[L - 1][j] = (a.type == 0) ? diff * dact(o[j]) : diff;
@@ -610,8 +624,8 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
         const int nxt = cur ^ 1;
         for (int l = 0; l < L; l++) {
             const int N = a.N[l], M = a.M[l];
-            const double *hin_old = l ? h[cur][l - 1] : xin;
-            const double *hin_new = l ? h[nxt][l - 1] : xin;
+            const lds_d *hin_old = l ? h[cur][l - 1] : xin;
+            const lds_d *hin_new = l ? h[nxt][l - 1] : xin;
             const bool use_act = (l < L - 1) || a.type == 0;
             for (int r = wave; g + (long)G * r < N; r += CNW) {
                 const int j = g + G * r;
@@ -660,7 +674,7 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
         is_ok = ok;
         /* every workgroup holds the same values: the same decision everywhere; a timed-out
          * barrier (ctl[1]) ends the loop on every workgroup that sees it */
-        if (__hip_atomic_load((gu32 *)a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) stop = 1;
+        if (__hip_atomic_load((gu32 *)a.ctl + COOP_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) stop = 1;
         if (stop) break;
     }
     if (g == 0) {
@@ -711,7 +725,7 @@ extern "C" int hpnn_online_coop_launch(const hpnn_online_args *a, int grid, hipS
 }
 
 extern "C" int hpnn_online_coop_status(const hpnn_online_args *a) {
-    unsigned int v[2] = {0, 0};
-    if (hipMemcpy(v, a->ctl, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -2;
-    return v[1] ? -1 : 0;
+    unsigned int v = 0;
+    if (hipMemcpy(&v, a->ctl + COOP_ERR, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    return v ? -1 : 0;
 }
