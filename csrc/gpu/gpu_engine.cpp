@@ -19,6 +19,8 @@
 #include <libhpnn/comm.h>
 #include <libhpnn/observe.h>
 #include <libhpnn/devmem.h>
+#include <libhpnn/bootstrap.h>
+#include <libhpnn/xar.h>
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
@@ -663,6 +665,8 @@ namespace {
  * live in one allocation and the all-reduce is a deterministic slab sum. */
 BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
               hpnn_batched_stats *st, int G, bool loopback);
+BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                 hpnn_batched_stats *st);
 
 }  // namespace
 
@@ -673,6 +677,9 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         const int lbr = lb ? atoi(lb) : 0;
         const char *fr = getenv("HPNN_FORCE_RCCL");
         if (lbr >= 2) return train_dp(k, X, T, n, o, st, lbr, true);
+        /* one process per GPU under a launcher (torchrun --no-python bin/train_nn ...) */
+        const char *nd = getenv("HPNN_NATIVE_DP");
+        if (hpnn_boot_world() > 1 && !(nd && nd[0] == '0')) return train_dp_mp(k, X, T, n, o, st);
         if (o->n_gpu > 1 || (fr && fr[0] == '1')) return train_dp(k, X, T, n, o, st, (int)(o->n_gpu ? o->n_gpu : 1), false);
     }
     if (o->dtype != NN_DTYPE_BF16) {
@@ -898,6 +905,135 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         st->last_loss = st->epoch_loss;
     }
     cleanup();
+    if (ok && k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
+    return ok;
+}
+
+/* Data parallelism with ONE process per GPU (any launcher exporting RANK / WORLD_SIZE /
+ * LOCAL_RANK; the reference ran `mpirun -np N train_nn` and replicated the same sample on
+ * every rank).  Rank r trains rows [b*B + r*ceil(B/W), ...) of every global
+ * minibatch b; the FP32 gradients are summed with the one-shot xGMI all-reduce (all
+ * ranks on one node, gradients <= 4 MiB) or RCCL, the bootstrap exchange (IPC handles /
+ * unique id / epoch statistics) goes through include/libhpnn/bootstrap.h; every rank
+ * applies the same update, so the weights stay identical (rank 0 writes the files). */
+BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                 hpnn_batched_stats *st) {
+    const int W = hpnn_boot_world(), R = hpnn_boot_rank();
+    if (k->n_hiddens + 1 > 16 || W < 2 || W > 64) return FALSE;
+    hpnn_gpu_sync_host(k);
+    const int dev = hpnn_rt_device(0);
+    HIPCHK(hipSetDevice(dev));
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    const int B = (int)(o->batch ? o->batch : 256);
+    const int Bg = (B + W - 1) / W;
+    const bool mom = o->train == NN_TRAIN_BPM;
+    const int n_out = (int)k->n_outputs;
+    Batched net;
+    if (!net.init(k, Bg, o->type, mom, s) || !net.alloc_flat()) return FALSE;
+    if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
+    const size_t count = net.flat_count();
+    /* gradient exchange: one-shot xGMI all-reduce when every rank is on this node and the
+     * gradients are small, else RCCL; every rank takes the same decision */
+    hpnn_xar *xar = nullptr;
+    hpnn_comm *comm = nullptr;
+    const char *xe = getenv("HPNN_XAR");
+    const char *lws = getenv("LOCAL_WORLD_SIZE");
+    bool use_xar = !(xe && xe[0] == '0') && lws && atoi(lws) == W && W <= HPNN_XAR_MAX_RANKS &&
+                   count * 4 <= ((size_t)4 << 20);
+    if (use_xar) {
+        xar = hpnn_xar_create(R, W, count * 4);
+        std::vector<char> h(HPNN_XAR_HANDLE_BYTES, 0), all((size_t)W * HPNN_XAR_HANDLE_BYTES);
+        int ok = xar && hpnn_xar_handles(xar, h.data()) == 0;
+        if (hpnn_boot_allgather(h.data(), h.size(), all.data()) != 0) return FALSE;
+        if (ok) ok = hpnn_xar_open(xar, all.data()) == 0;
+        std::vector<int> oks(W);
+        if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return FALSE;
+        for (int v : oks) use_xar = use_xar && v;
+        if (!use_xar && xar) {
+            hpnn_xar_destroy(xar);
+            xar = nullptr;
+        }
+    }
+    if (!use_xar) {
+        unsigned char id[HPNN_COMM_ID_BYTES] = {0};
+        std::vector<unsigned char> all((size_t)W * HPNN_COMM_ID_BYTES);
+        if (R == 0 && hpnn_comm_unique_id(id) != 0) return FALSE;
+        if (hpnn_boot_allgather(id, sizeof id, all.data()) != 0) return FALSE;
+        comm = hpnn_comm_init_rank(all.data(), W, R, dev); /* rank 0's id */
+        if (!comm) return FALSE;
+    }
+    NN_OUT(stdout, "data-parallel batched training: %d processes (%s), %d samples per rank per step\n", W,
+           use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Bg);
+    const int n_batches = (int)((n + B - 1) / B);
+    const int rows_p = n_batches * B + Bg + 128;
+    void *Xd = nullptr;
+    float *Td = nullptr;
+    BOOL ok = upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s);
+    if (ok) {
+        std::vector<float> tf((size_t)rows_p * n_out, 0.f);
+        for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (float)T[i];
+        ok = hpnn_dev_malloc(&Td, tf.size() * 4) == hipSuccess &&
+             hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    double ep_loss = 0.0;
+    unsigned int ep_hits = 0;
+    for (UINT e = 0; e < o->epochs && ok; e++) {
+        ok = hipMemsetAsync(net.acc, 0, Batched::ACC_BYTES, s) == hipSuccess;
+        for (int b = 0; b < n_batches && ok; b++) {
+            const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
+            const int start = b * B + R * Bg;
+            int nv = end - start;
+            nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
+            const char *xb = (const char *)Xd + (size_t)start * net.Kp[0] * 2;
+            const float *tb = Td + (size_t)start * n_out;
+            ok = net.grads(xb, tb, n_out, nv);
+            if (!ok) break;
+            ok = (use_xar ? hpnn_xar_all_reduce_f32(xar, net.gflat, net.gflat, (long)count, s)
+                          : hpnn_comm_all_reduce(comm, net.gflat, net.gflat, (long)count, HPNN_DT_F32, HPNN_OP_SUM,
+                                                 s)) == 0;
+            const int total = end - b * B;
+            if (ok) ok = net.update_flat(net.gflat, (float)o->lr, (float)o->alpha, 1.0f / (float)(total > 0 ? total : 1),
+                                         mom);
+        }
+        if (!ok) break;
+        double l = 0.0;
+        unsigned int h = 0;
+        ok = net.read_stats(&l, &h);
+        if (ok) ok = use_xar ? hpnn_xar_status(xar) == 0 : hpnn_comm_check(comm) == 0;
+        struct {
+            double loss;
+            unsigned int hits, ok;
+        } mine = {l, h, (unsigned)ok}, *every = new decltype(mine)[W];
+        if (hpnn_boot_allgather(&mine, sizeof mine, every) != 0) ok = FALSE;
+        ep_loss = 0.0;
+        ep_hits = 0;
+        for (int r = 0; r < W && ok; r++) {
+            ep_loss += every[r].loss;
+            ep_hits += every[r].hits;
+            ok = ok && every[r].ok;
+        }
+        delete[] every;
+        if (ok && hpnn_metrics_active())
+            hpnn_metrics_epoch("gpu-dp-mp", o->epoch0 + e + 1, ep_loss / (double)n, ep_hits, n,
+                               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
+                               (UINT64)n * (e + 1));
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (ok) ok = net.download(k);
+    if (ok && st) {
+        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->samples = (UINT64)n * o->epochs;
+        st->epoch_loss = ep_loss / (double)n;
+        st->correct = ep_hits;
+        st->last_loss = st->epoch_loss;
+    }
+    hipStreamSynchronize(s);
+    hpnn_boot_finish(); /* every rank is past its last all-reduce before any buffer goes */
+    if (Xd) hpnn_dev_free(Xd);
+    if (Td) hpnn_dev_free(Td);
+    if (xar) hpnn_xar_destroy(xar);
+    if (comm) hpnn_comm_destroy(comm);
     if (ok && k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
     return ok;
 }

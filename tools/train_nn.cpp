@@ -69,7 +69,12 @@ int main(int argc, char *argv[]) {
         return -1;
     }
     if (_NN(return, verbose)() > 1) _NN(dump, conf)(neural, stdout);
-    if (!_NN(return, dry)()) {
+    /* rank 0 alone writes the kernel files (every rank holds the same weights; a second
+     * fopen("w") of the same path would truncate rank 0's file) */
+    UINT task = 0;
+    _NN(get, curr_mpi_task)(&task);
+    const bool writer = !_NN(return, dry)() && task == 0;
+    if (writer) {
         FILE *f = fopen("./kernel.tmp", "w");
         if (!f) {
             _OUT(stderr, "FAILED to open kernel.tmp for writing!\n");
@@ -80,7 +85,7 @@ int main(int argc, char *argv[]) {
     }
     BOOL ok = _NN(train, kernel)(neural);
     if (!ok) _OUT(stderr, "Training FAILED!\n");
-    if (!_NN(return, dry)()) {
+    if (writer) {
         FILE *f = fopen("./kernel.opt", "w");
         if (!f) {
             _OUT(stderr, "FAILED to open kernel.opt for writing!\n");
