@@ -395,15 +395,17 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
 #undef HPNN_NT
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int RING = 73728, int MAXST = 6>
 int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s, const TnTail &tail) {
     const int tiles_n = N / TN, tiles_m = M / TM;
     const int units = Bt / 64;
-    /* 32-row stages, ring of ~72 KiB (2 workgroups per CU) */
+    /* 32-row stages, ring of ~72 KiB (2 workgroups per CU), or the deep ring (~144 KiB,
+     * one workgroup per CU: twice the bytes in flight per CU for a grid of <= 1 GEMM
+     * workgroup per CU, where the stream is latency-bound by the ring depth) */
     constexpr int BKR = 32;
     constexpr int STAGE = BKR * (TM + TN) * 2;
-    constexpr int ST = (73728 / STAGE) < 2 ? 2 : ((73728 / STAGE) > 6 ? 6 : (73728 / STAGE));
+    constexpr int ST = (RING / STAGE) < 2 ? 2 : ((RING / STAGE) > MAXST ? MAXST : (RING / STAGE));
     const int tiles = tiles_m * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
     hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits + tail.blocks), dim3(256), 0, s,
@@ -412,9 +414,28 @@ int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* HPNN_TN_DEEP: 1 forces the deep ring, 0 disables it; unset = deep ring when the GEMM
+ * grid has at most HPNN_TN_DEEP_MAX_WG workgroups (default 0: off).  Measured and rejected
+ * for MNIST's G0 (800x128 over 65536 rows, 48 splits): 74.3-74.6 us/step with the deep
+ * ring vs 73.4-73.5 us with the 72 KiB ring (the tail reduction workgroups lose their
+ * co-residence with the GEMM workgroups); fewer / more splits with the deep ring were
+ * slower still (32: 80.3, 40: 76.2, 64: 88.3, 96: 84.1 us) -- scripts/gpu_ab_tn.sh */
+int tn_deep_mode() {
+    static const int v = [] { const char *e = getenv("HPNN_TN_DEEP"); return e ? atoi(e) : -1; }();
+    return v;
+}
+
+#ifndef HPNN_TN_DEEP_MAX_WG
+#define HPNN_TN_DEEP_MAX_WG 0
+#endif
+
 template <int TM>
 int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s, const TnTail &t) {
+    const int dm = tn_deep_mode();
+    const long wgs = (long)(N / 128) * (M / TM) * splits;
+    if (N % 128 == 0 && (dm == 1 || (dm < 0 && wgs <= HPNN_TN_DEEP_MAX_WG)))
+        return launch_tn_t<TM, 128, 147456, 8>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     if (N % 128 == 0) return launch_tn_t<TM, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     if (N % 64 == 0) return launch_tn_t<TM, 64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     return launch_tn_t<TM, 32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
