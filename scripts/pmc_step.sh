@@ -12,13 +12,14 @@ for grp in "${groups[@]}"; do
   i=$((i+1))
 done
 python3 - <<'PY' | tee gpurun_out/pmc_step.txt
-import csv, glob, collections
+import csv, glob, collections, re
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob("gpurun_out/pmcs/g*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:48]
-        if not any(t in k for t in ("mlp3", "gemm_tn", "sgd_update")): continue
-        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+        m = re.search(r"(mlp3_fused_kernel|gemm_tn_pipe_kernel<[^>]*>|sgd_update_multi_wide_kernel)", k)
+        if not m: continue
+        acc[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():
     print(k)
     for c, v in sorted(d.items()):
