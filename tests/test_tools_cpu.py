@@ -90,3 +90,22 @@ def test_tutorial_end_to_end(tmp_path, tut, env):
     acc = [float(r[1]) for r in rows]
     assert all(0.0 <= a <= 100.0 for a in acc)
     assert (tmp_path / "run" / "kernel.opt").exists()
+
+
+def test_monitor_renders_tutorial_raw(tmp_path):
+    """ASCII monitor of a tutorial's raw file (reference: tutorial.bash:138-174 watch +
+    plot.gnuplot): parses pass / accuracy / loss, skips partial lines, marks every pass"""
+    from hpnn_amd.utils import monitor
+    raw = tmp_path / "raw"
+    raw.write_text("1 10.5 loss=2.30\n2 35.0 loss=1.90\n3 71.25\n4 \nbroken line\n")
+    rows = monitor.read_raw(str(raw))
+    assert rows == [(1, 10.5, 2.30), (2, 35.0, 1.90), (3, 71.25, None)]
+    chart = monitor.render(rows, width=30, height=8)
+    lines = chart.splitlines()
+    assert lines[0].startswith("test accuracy")
+    assert sum(ln.count("*") for ln in lines) == 3
+    assert "pass 3: 71.25 %" in chart and "best 71.25 % at pass 3" in chart
+    assert "(no data yet)" in monitor.render(monitor.read_raw(str(tmp_path / "missing")))
+    r = subprocess.run([sys.executable, "-m", "hpnn_amd.utils.monitor", str(raw), "--width", "20"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.count("*") == 3, r.stdout + r.stderr
