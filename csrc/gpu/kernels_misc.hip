@@ -509,6 +509,82 @@ __global__ __launch_bounds__(1024) void sgd_update_multi_wide_kernel(UpdArgs a) 
     }
 }
 
+/* Same step over 8-row sub-tiles (8 x 32 elements, one f32x4 per lane of a wave): four
+ * workgroups per 32x32 tile, so MNIST's update (~110 tiles) fills the 256 CUs (~440
+ * workgroups) instead of leaving half the chip idle while the slabs stream.  8 waves; wave
+ * w sums slabs w, w+8, ... two per iteration; partials meet in LDS in wave order
+ * (deterministic); wave 0 applies the step.  tile0[] counts sub-tiles here. */
+__global__ __launch_bounds__(512) void sgd_update_multi_sub_kernel(UpdArgs a) {
+    __shared__ f32x4 part[8][64];
+    __shared__ float tilebuf[8][33];
+    int l = 0;
+    while (l + 1 < a.n && (int)blockIdx.x >= a.tile0[l + 1]) l++;
+    const hpnn_upd_layer &L = a.L[l];
+    const int local = blockIdx.x - a.tile0[l];
+    const int tile = local >> 2, sub = local & 3;
+    const int tiles_k = L.K / 32;
+    const int tn = tile / tiles_k, tk = tile % tiles_k;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ty = lane >> 3, tx = lane & 7;
+    const int n = tn * 32 + sub * 8 + ty, k = tk * 32 + tx * 4;
+    const size_t idx = (size_t)n * L.K + k;
+    /* up to 8 slab loads per lane in flight at once (the step is load-latency bound:
+     * each wave owns only S/8 slabs), summed in a fixed order */
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = w; s0 < L.S; s0 += 64) {
+        f32x4 x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int s = s0 + 8 * j;
+            x[j] = s < L.S ? *(const f32x4 *)(L.G + (long)s * L.gstride + idx) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        acc += ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
+    }
+    part[w][lane] = acc;
+    __syncthreads();
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    if (w == 0) {
+        f32x4 g = part[0][lane];
+#pragma unroll
+        for (int ww = 1; ww < 8; ww++) g += part[ww][lane];
+        f32x4 wv = *(const f32x4 *)(L.W32 + idx);
+        if (a.momentum) {
+            f32x4 v = *(const f32x4 *)(L.V32 + idx);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                v[r] += a.lr * (g[r] * a.scale);
+                wv[r] += v[r];
+                v[r] *= a.alpha;
+            }
+            *(f32x4 *)(L.V32 + idx) = v;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) wv[r] += a.lr * (g[r] * a.scale);
+        }
+        *(f32x4 *)(L.W32 + idx) = wv;
+        bf16x4 wb;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            wb[r] = (__bf16)wv[r];
+            tilebuf[ty][tx * 4 + r] = wv[r];
+        }
+        *(bf16x4 *)((__bf16 *)L.Wbf + idx) = wb;
+        if (L.Wf) {
+            const size_t fo = (((size_t)(n >> 4) * tiles_k + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+            *(bf16x4 *)((__bf16 *)L.Wf + fo) = wb;
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+        /* transposed: lane writes Wt[k = tk*32 + lane/2][n = tn*32 + sub*8 + 4(lane&1) .. +3] */
+        const int kk = lane >> 1, nh = (lane & 1) * 4;
+        bf16x4 tb;
+#pragma unroll
+        for (int r = 0; r < 4; r++) tb[r] = (__bf16)tilebuf[nh + r][kk];
+        *(bf16x4 *)((__bf16 *)L.Wt + (size_t)(tk * 32 + kk) * L.N + tn * 32 + sub * 8 + nh) = tb;
+    }
+}
+
 __global__ void pack_bf16_kernel(const void *__restrict__ src, int src_f64, int rows, int cols, int lds,
                                  __bf16 *__restrict__ dst, int prow, int pcol, int ldd) {
     const long total = (long)prow * pcol;
@@ -607,7 +683,12 @@ extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float 
     int max_s = 0;
     for (int l = 0; l < n; l++) max_s = layers[l].S > max_s ? layers[l].S : max_s;
     static const int wide_off = [] { const char *e = getenv("HPNN_UPD_NARROW"); return e && atoi(e) ? 1 : 0; }();
-    if (max_s >= 8 && !wide_off)
+    /* HPNN_UPD_MODE=1: one 16-wave workgroup per 32x32 tile (previous default) */
+    static const int tile_mode = [] { const char *e = getenv("HPNN_UPD_MODE"); return e ? atoi(e) : 0; }();
+    if (max_s >= 8 && !wide_off && tile_mode != 1) {
+        for (int l = 0; l <= n; l++) a.tile0[l] *= 4;
+        hipLaunchKernelGGL(sgd_update_multi_sub_kernel, dim3(4 * t), dim3(512), 0, stream, a);
+    } else if (max_s >= 8 && !wide_off)
         hipLaunchKernelGGL(sgd_update_multi_wide_kernel, dim3(t), dim3(1024), 0, stream, a);
     else
         hipLaunchKernelGGL(sgd_update_multi_kernel, dim3(t), dim3(256), 0, stream, a);

@@ -1,8 +1,12 @@
 """Numerics of the gfx950 kernels against plain PyTorch FP32 references."""
+import os
+
 import pytest
 import torch
 
 from hpnn_amd import ops
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -147,22 +151,50 @@ def test_reduce_slabs_many(gpu, S):
     assert torch.equal(out, out2)  # deterministic
 
 
-@pytest.mark.parametrize("momentum", [False, True])
-def test_sgd_update_multi_wide(gpu, momentum):
-    """many slabs (>= 8) take the 1024-thread kernel: same step as the FP64 reference"""
-    torch.manual_seed(11)
+def _sgd_multi_case(momentum, seed=11):
+    torch.manual_seed(seed)
     layers, refs = [], []
-    for (N, K, S) in [(128, 800, 96), (64, 128, 16), (32, 64, 9)]:
+    for i, (N, K, S) in enumerate([(128, 800, 96), (64, 128, 16), (32, 64, 9)]):
         W = torch.randn(N, K, device="cuda")
         V = torch.randn(N, K, device="cuda") * 0.1 if momentum else None
         G = torch.randn(S, N, K, device="cuda")
         Wb = torch.empty(N, K, dtype=torch.bfloat16, device="cuda")
         Wt = torch.empty(K, N, dtype=torch.bfloat16, device="cuda")
+        Wf = torch.empty(N * K, dtype=torch.bfloat16, device="cuda") if i == 0 else None
         refs.append((W.double().clone(), None if V is None else V.double().clone(), G.double().sum(0)))
-        layers.append((W, V, G, Wb, Wt, None))
+        layers.append((W, V, G, Wb, Wt, Wf))
+    return layers, refs
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("momentum", [False, True])
+def test_sgd_update_multi_wide(gpu, momentum, mode):
+    """many slabs (>= 8): HPNN_UPD_MODE 0 = 8-row sub-tile kernel (default), 1 = one
+    16-wave workgroup per 32x32 tile; same step as the FP64 reference, bitwise repeatable.
+    The mode is read once per process, so mode 1 runs in a child process."""
+    if mode == "1":
+        import subprocess
+        import sys
+        env = dict(os.environ, HPNN_UPD_MODE="1")
+        code = ("import sys, importlib.util as u; sys.path.insert(0, %r); "
+                "s = u.spec_from_file_location('tk', %r); t = u.module_from_spec(s); s.loader.exec_module(t); "
+                "t._sgd_multi_check(%r)" % (ROOT, os.path.abspath(__file__), momentum))
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return
+    _sgd_multi_check(momentum)
+
+
+def _sgd_multi_check(momentum):
+    layers, refs = _sgd_multi_case(momentum)
     lr, alpha, scale = 0.05, 0.2, 1.0 / 512
     ops.sgd_update_multi(layers, lr, alpha, scale, momentum)
     torch.cuda.synchronize()
+    again, _ = _sgd_multi_case(momentum)
+    ops.sgd_update_multi(again, lr, alpha, scale, momentum)
+    torch.cuda.synchronize()
+    assert torch.equal(again[0][0], layers[0][0])  # deterministic
+    assert torch.equal(layers[0][5], ops.frag_major(layers[0][0].bfloat16()))
     for (W, V, G, Wb, Wt, _), (W0, V0, g) in zip(layers, refs):
         if momentum:
             v = V0 + lr * g * scale
