@@ -512,8 +512,11 @@ __global__ __launch_bounds__(1024) void sgd_update_multi_wide_kernel(UpdArgs a) 
 /* Same step over 8-row sub-tiles (8 x 32 elements, one f32x4 per lane of a wave): four
  * workgroups per 32x32 tile, so MNIST's update (~110 tiles) fills the 256 CUs (~440
  * workgroups) instead of leaving half the chip idle while the slabs stream.  8 waves; wave
- * w sums slabs w, w+8, ... two per iteration; partials meet in LDS in wave order
- * (deterministic); wave 0 applies the step.  tile0[] counts sub-tiles here. */
+ * w sums slabs w, w+8, ..., up to 8 per iteration, added as a fixed pairwise tree (a wave
+ * whose layer has fewer than w+1 slabs adds nothing); partials meet in LDS in wave order
+ * (deterministic); wave 0 applies the step.  tile0[] counts sub-tiles here.  The slab sum
+ * order differs from the HPNN_UPD_MODE=1 kernel, so the two modes agree only to the last
+ * FP32 bits. */
 __global__ __launch_bounds__(512) void sgd_update_multi_sub_kernel(UpdArgs a) {
     __shared__ f32x4 part[8][64];
     __shared__ float tilebuf[8][33];
@@ -674,6 +677,8 @@ extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float 
     for (int l = 0; l < n; l++) {
         const hpnn_upd_layer &L = layers[l];
         if (L.N % 32 || L.K % 32 || L.S < 1) return -2;
+        /* the slab-reduction kernels read 16-byte f32x4 vectors at s * gstride */
+        if (L.S > 1 && L.gstride % 4) return -2;
         if (momentum && !L.V32) return -1;
         a.L[l] = L;
         a.tile0[l] = t;

@@ -154,7 +154,9 @@ def test_reduce_slabs_many(gpu, S):
 def _sgd_multi_case(momentum, seed=11):
     torch.manual_seed(seed)
     layers, refs = [], []
-    for i, (N, K, S) in enumerate([(128, 800, 96), (64, 128, 16), (32, 64, 9)]):
+    # (32, 64, 3) and (64, 96, 1): layers with fewer than 8 slabs next to a 96-slab layer,
+    # so some waves of the sub-tile kernel hold no slab at all
+    for i, (N, K, S) in enumerate([(128, 800, 96), (64, 128, 16), (32, 64, 9), (32, 64, 3), (64, 96, 1)]):
         W = torch.randn(N, K, device="cuda")
         V = torch.randn(N, K, device="cuda") * 0.1 if momentum else None
         G = torch.randn(S, N, K, device="cuda")
@@ -171,18 +173,17 @@ def _sgd_multi_case(momentum, seed=11):
 def test_sgd_update_multi_wide(gpu, momentum, mode):
     """many slabs (>= 8): HPNN_UPD_MODE 0 = 8-row sub-tile kernel (default), 1 = one
     16-wave workgroup per 32x32 tile; same step as the FP64 reference, bitwise repeatable.
-    The mode is read once per process, so mode 1 runs in a child process."""
-    if mode == "1":
-        import subprocess
-        import sys
-        env = dict(os.environ, HPNN_UPD_MODE="1")
-        code = ("import sys, importlib.util as u; sys.path.insert(0, %r); "
-                "s = u.spec_from_file_location('tk', %r); t = u.module_from_spec(s); s.loader.exec_module(t); "
-                "t._sgd_multi_check(%r)" % (ROOT, os.path.abspath(__file__), momentum))
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stdout + r.stderr
-        return
-    _sgd_multi_check(momentum)
+    The mode is read once per process, so each mode runs in a child process whose
+    environment sets HPNN_UPD_MODE explicitly and drops HPNN_UPD_NARROW."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("HPNN_UPD_MODE", "HPNN_UPD_NARROW")}
+    env["HPNN_UPD_MODE"] = mode
+    code = ("import sys, importlib.util as u; sys.path.insert(0, %r); "
+            "s = u.spec_from_file_location('tk', %r); t = u.module_from_spec(s); s.loader.exec_module(t); "
+            "t._sgd_multi_check(%r)" % (ROOT, os.path.abspath(__file__), momentum))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def _sgd_multi_check(momentum):
