@@ -1,0 +1,77 @@
+// LDS-DMA streaming probe: one 256-thread workgroup per CU streams its share of a 105 MB
+// bf16 matrix [65536][800] into an LDS ring by global_load_lds_dwordx4 (1 KiB per wave
+// instruction), waiting with a counted vmcnt so that `depth` KiB stay in flight per CU.
+// Patterns: 0 = linear 1 KiB pieces of the CU's contiguous rows; 1 = the mlp3 X-tile piece
+// (8 rows x 128 B, rows 1600 B apart); 2 = TN piece (16 rows x 64 B).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+__device__ __forceinline__ void glds16(const void *gsrc, char *lds_dst) {
+    const unsigned int m0 =
+        __builtin_amdgcn_readfirstlane((unsigned int)(uintptr_t)(__attribute__((address_space(3))) char *)lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// each wave keeps DEPTH pieces (KiB) in flight; the ring has DEPTH+4 slots per wave
+template <int PAT, int DEPTH>
+__global__ __launch_bounds__(256) void dma_stream(const char *X, int rows_per_block, float *out) {
+    extern __shared__ char lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int SLOTS = DEPTH + 4;
+    char *ring = lds + wave * SLOTS * 1024;
+    const size_t pitch = 1600;
+    const char *base = X + (size_t)blockIdx.x * rows_per_block * pitch;
+    const int pieces = rows_per_block * 1600 / 1024; // per block
+    // wave w takes pieces w, w+4, ...
+    int issued = 0;
+    auto src = [&](int p) -> const char * {
+        if (PAT == 0) return base + (size_t)p * 1024 + lane * 16;
+        if (PAT == 1) {  // 32-row tiles, 13 sub-tiles of 64 cols (tail ignored: treat as 12.5), 4 pieces each
+            const int tile = p / 50, q = p % 50, sub = q / 4, rp = (q % 4) * 8;
+            const int r = tile * 32 + rp + (lane >> 3);
+            return base + (size_t)r * pitch + sub * 128 + (lane & 7) * 16;
+        }
+        const int tile = p / 50, q = p % 50, sub = q / 2, rp = (q % 2) * 16;  // 25 subtiles of 32 cols, 16 rows x 64 B
+        const int r = tile * 32 + rp + (lane >> 2);
+        return base + (size_t)r * pitch + sub * 64 + (lane & 3) * 16;
+    };
+    for (int p = wave; p < pieces; p += 4) {
+        glds16(src(p), ring + (issued % SLOTS) * 1024);
+        issued++;
+        if (issued >= DEPTH) wait_vm<DEPTH - 1>();
+    }
+    wait_vm<0>();
+    if (lane == 0 && ring[0] == 123) out[0] = 1.f;
+}
+
+int main() {
+    const int B = 65536, G = 256;
+    char *X;
+    float *o;
+    if (hipMalloc(&X, (size_t)B * 1600) || hipMalloc(&o, 4)) return 1;
+    (void)hipMemset(X, 0, (size_t)B * 1600);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+#define RUN(PAT, D)                                                                                       \
+    do {                                                                                                  \
+        const int lds = 4 * (D + 4) * 1024;                                                               \
+        (void)hipFuncSetAttribute((const void *)dma_stream<PAT, D>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL((dma_stream<PAT, D>), dim3(G), dim3(256), lds, 0, X, B / G, o); \
+        (void)hipEventRecord(a);                                                                          \
+        for (int r = 0; r < 20; r++) hipLaunchKernelGGL((dma_stream<PAT, D>), dim3(G), dim3(256), lds, 0, X, B / G, o); \
+        (void)hipEventRecord(b);                                                                          \
+        (void)hipEventSynchronize(b);                                                                     \
+        float ms;                                                                                         \
+        (void)hipEventElapsedTime(&ms, a, b);                                                             \
+        printf("pattern %d  in-flight %3d KiB/CU: %6.1f us  %5.2f TB/s\n", PAT, 4 * D, ms * 50,          \
+               (double)B * 1600 / (ms / 20 * 1e-3) / 1e12);                                               \
+    } while (0)
+    RUN(0, 4); RUN(0, 8); RUN(0, 16); RUN(0, 24); RUN(0, 32);
+    RUN(1, 4); RUN(1, 8); RUN(1, 16); RUN(1, 24); RUN(1, 32);
+    RUN(2, 8); RUN(2, 16); RUN(2, 24); RUN(2, 32);
+    return 0;
+}

@@ -131,6 +131,13 @@ int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void 
                     const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                     float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
                     hipStream_t stream);
+/* role-split variant of hpnn_mlp3_fused (kernels_mlp3f.hip, selected by HPNN_FRONT=f for
+ * K0 >= 800): same arguments, outputs and slab layout; grid > 0 required */
+int hpnn_mlp3_front(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,
+                    const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
+                    float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
+                    hipStream_t stream);
+int hpnn_mlp3_front_trace(unsigned long long *out);
 /* profiling: s_memtime timeline of block 0 (HPNN_FZ_MODE=9), [8 waves][8 stages][8 marks] */
 int hpnn_mlp3_fused_trace(unsigned long long *out);
 /* grid hpnn_mlp3_fused will use for Bp samples (slab rows to allocate) */

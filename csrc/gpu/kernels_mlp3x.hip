@@ -469,6 +469,12 @@ int launch_fused_k(const void *X, int ldx, const void *W0f, const void *W1, cons
 #undef HPNN_FZ
 }
 
+/* HPNN_FRONT=f selects the role-split kernel (kernels_mlp3f.hip); default: this one */
+bool front_split() {
+    static const bool v = [] { const char *e = getenv("HPNN_FRONT"); return e && e[0] == 'f'; }();
+    return v;
+}
+
 }  // namespace
 
 extern "C" int hpnn_mlp3_fused_grid(int Bp, int grid) { return Bp > 0 && Bp % FR == 0 ? fused_grid(Bp, grid) : -2; }
@@ -480,6 +486,10 @@ extern "C" int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, 
     if (Bp <= 0 || Bp % FR || n_out > NO || n_out < 1 || ldx % 8 || ldx < K0) return -2;
     if (!labels && !T) return -1;
     grid = fused_grid(Bp, grid);
+    /* HPNN_FRONT=f: the role-split kernel (kernels_mlp3f.hip) */
+    if (front_split() && K0 >= 800)
+        return hpnn_mlp3_front(X, ldx, K0, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct,
+                               Bp, n_valid, n_out, type, grid, stream);
 #define HPNN_FK(K_)                                                                                             \
     if (K0 == K_)                                                                                               \
     return launch_fused_k<K_ / 32>(X, ldx, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct, \
@@ -495,5 +505,6 @@ extern "C" int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, 
 
 /* MODE 9 timeline: out[8 waves][8 stages][8 marks] shader-clock ticks (block 0) */
 extern "C" int hpnn_mlp3_fused_trace(unsigned long long *out) {
+    if (front_split()) return hpnn_mlp3_front_trace(out);
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fz_trace), sizeof(g_fz_trace)) == hipSuccess ? 0 : -5;
 }
