@@ -253,25 +253,15 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         /* ====================== front waves 0-3 ====================== */
         /* W0 (neurons 32w .. 32w+31 x K0, the MFMA A operand) over both register files:
          * 128 AGPRs (w0[0][*] and the first W0_A1 fragments of w0[1]) and the rest in VGPRs
-         * beside the accumulators and the fragment prefetch.  Loaded by inline-asm loads
-         * straight into their final file (a compiler load would stage all 200 registers in
-         * VGPRs first); the explicit vmcnt(0) below orders every use after them. */
+         * beside the accumulators and the fragment prefetch.  Plain loads (the compiler
+         * tracks them), then pinned into their file. */
         constexpr int W0_A1 = 3;
         bf16x8 w0[2][KS];
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
-                const __bf16 *src = W0f + ((size_t)((2 * rw + i) * KS + ks) * 64 + lane) * 8;
-                if (i == 0 || ks < W0_A1)
-                    asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(w0[i][ks]) : "v"(src) : "memory");
-                else
-                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w0[i][ks]) : "v"(src) : "memory");
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        /* the loads above write their registers asynchronously: keep every destination
-         * live (and unchanged) up to this wait, so that no other value is given one of
-         * them while a load is in flight (e.g. when a profiling mode leaves W0 unused) */
+            for (int ks = 0; ks < KS; ks++)
+                w0[i][ks] = *(const bf16x8 *)(W0f + ((size_t)((2 * rw + i) * KS + ks) * 64 + lane) * 8);
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -281,8 +271,8 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             }
         emark(1);
         f32x4 acc[2][2]; /* H1 tiles (neuron group 2w+i, sample group sg) */
-        constexpr int PD = 2;
-        auto front_chunk = [&](const char *imgX, auto cc) {
+        constexpr int PD = 1;
+        auto front_chunk = [&](const char *imgX, auto cc, auto pinc) {
             constexpr int c = decltype(cc)::value;
             constexpr int k0 = XP::ks0(c), k1 = XP::ks1(c), NSL = k1 - k0;
             if constexpr (c == 0) {
@@ -309,27 +299,27 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                 __builtin_amdgcn_sched_barrier(0);
             });
         };
-        auto fstage = [&](int t, auto FWc) {
+        auto fstage = [&](int t, auto FWc, auto PINc) {
             constexpr bool FW = decltype(FWc)::value && FRONT_ON;
             const char *imgX = lds + (t & 1) * LY::XST;
             char *H1w = lds + LY::OFF_H1 + (t & 1) * LY::IMG_H1;
             mark(t, 0);
             lds_barrier();
             mark(t, 1);
-            if constexpr (FW) front_chunk(imgX, C0{});
+            if constexpr (FW) front_chunk(imgX, C0{}, PINc);
             mark(t, 2);
             lds_barrier();
             mark(t, 3);
-            if constexpr (FW) front_chunk(imgX, C1{});
+            if constexpr (FW) front_chunk(imgX, C1{}, PINc);
             mark(t, 4);
             lds_barrier();
             mark(t, 5);
-            if constexpr (FW) front_chunk(imgX, C2{});
+            if constexpr (FW) front_chunk(imgX, C2{}, PINc);
             mark(t, 6);
             lds_barrier();
             mark(t, 7);
             if constexpr (FW) {
-                front_chunk(imgX, C3{});
+                front_chunk(imgX, C3{}, PINc);
 #pragma unroll
                 for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -341,8 +331,8 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                     }
             }
         };
-        for (int t = 0; t < nloc; t++) fstage(t, T1{});
-        fstage(nloc, F0{});
+        for (int t = 0; t < nloc; t++) fstage(t, T1{}, F0{});
+        fstage(nloc, F0{}, F0{});
         emark(2);
     } else {
         /* ====================== back waves 4-7 ====================== */
