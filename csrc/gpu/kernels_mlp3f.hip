@@ -1,31 +1,27 @@
 /*
  * mlp3_front: the n_in -> 128 -> 64 -> n_out(<=32) training step up to delta1 in ONE
- * persistent kernel (gfx950), with the waves split by role.
+ * persistent kernel (gfx950), with the waves split by role.  HPNN_FRONT=f selects it
+ * (kernels_mlp3x.hip's mlp3_fused is the default).
  *
  * Reference: the per-sample GEMV chain of ann_kernel_train / snn_kernel_train
  * (ann.c:883-888, 1279-1592; snn.c:280-335, 481-794; cuda_ann.cu:426-2093), batched.
  *
- * Why roles.  Layer 0 (H1 = f(X W0^T), K0 = 800) is 85 % of the step's MFMA work.  With
- * W0 in VGPRs as the MFMA A operand and X tiles in LDS as the B operand, a wave holding
- * 16 neurons reads one 1 KiB B fragment per 16x16x32 MFMA: four SIMDs then ask the LDS
- * for 256 B/clk, its whole bandwidth, before the back chain or the X DMA touch it
- * (mlp3_fused, kernels_mlp3x.hip, spent ~6900 cycles per 32-sample stage against ~1600
- * of MFMA per SIMD).  Here
- *   waves 0-3 ("front") each hold 32 neurons of W0 in VGPRs (2 A fragments x K0/32 =
- *              200 VGPRs at K0 = 800) and use every X fragment twice: half the LDS
- *              read traffic per MFMA;
- *              They also issue the X / label LDS-DMA (a few pieces per interval beside
- *              the MFMAs) and own every counted vmcnt wait;
- *   waves 4-7 ("back", one per SIMD beside a front wave) run the dependent back chain of
- *              the previous tile (H2, output layer + loss, delta2, delta1 -> HBM, G1/G2
- *              accumulated over all the block's tiles); its latency hides behind the
- *              partner front wave's MFMAs on the same SIMD.
- * A stage t = front of tile t + back of tile t-1, in 4 intervals separated by workgroup
- * barriers; interval j holds X chunk j of the front and phase j of the back chain
- * (P1 | P2 | P3+P5 | P4+P6).  X streams into a 2-tile LDS ring refilled chunk by chunk.
- * VM-counter discipline: in the loop only the front waves issue vector-memory operations
- * (X pieces and labels) in a fixed periodic order, so every wait is one exact counted
- * s_waitcnt; the back waves issue only the delta1 stores and never wait on them.
+ * One 512-thread workgroup per CU, 32-sample tiles:
+ *   waves 0-3 ("front") hold 32 neurons of W0 each as the MFMA A operand (the last k-step
+ *              in LDS, the rest over the AGPR and VGPR files) and use every X fragment
+ *              twice, which halves the LDS read traffic per MFMA of a 16-neuron split;
+ *   waves 4-7 ("back", one per SIMD beside a front wave) stage X (global loads into VGPRs
+ *              one stage ahead, ds_write into the tile image) and run the back chain:
+ *              P1 H2 = f(H1 W1^T) | P2 output + loss + delta3 | P3 delta2, P5 G2 | P4 delta1
+ *              -> HBM, P6 G1.
+ * A stage is 2 intervals (workgroup barriers).  Stage t: the front computes H1(t) (X chunk
+ * c in interval c); the back runs P1(t-1) + P3/P5(t-2) in interval 0 and P2(t-1) +
+ * P4/P6(t-2) in interval 1 -- two independent dependency chains per interval, so their
+ * latencies overlap, and the back chain of a tile spans two stages.
+ * The X image holds ONE tile: chunk 0 of tile t+1 is written in interval 1 of stage t
+ * (after the front has consumed chunk 0 of tile t), chunk 1 of tile t in interval 0 of
+ * stage t; each chunk is loaded into the back waves' VGPRs one interval before it is
+ * written.  Every global load is a compiler-visible load (no hand-counted vmcnt).
  */
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
@@ -45,47 +41,39 @@ namespace {
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 constexpr int FR = 32; /* samples per tile */
-constexpr int NCH = 4; /* X chunks (intervals) per tile */
-/* MODE >= 9 timeline (profiling only): block 0, waves 0..3, stages 0..7, 8 marks per stage */
-__device__ unsigned long long g_ff_trace[8][8][8]; /* [wave][stage < 7][mark]; [wave][7][0..3]: kernel marks */
+/* MODE >= 9 timeline (profiling only): [wave][stage < 7][4 marks per stage];
+ * [wave][7][0..2]: kernel marks (entry, prologue done, loop end) */
+__device__ unsigned long long g_ff_trace[8][8][8];
 
 template <int KS>
-struct FPlan {
+struct FPlan6 {
     static constexpr int S64 = KS / 2, TAIL = KS & 1, NS = S64 + TAIL; /* sub-tiles (64 / 32 cols) */
     static constexpr int PF = FR / 8;                                   /* pieces per full sub-tile */
-    /* first sub-tile of chunk c (weights in 1/13: intervals 0 and 3 carry the longer
-     * back phases) */
-    static constexpr int sb(int c) {
-        constexpr int cw[NCH + 1] = {0, 4, 7, 10, 13};
-        return (NS * cw[c] + 6) / 13;
-    }
+    static constexpr int SB1 = (NS + 1) / 2;                           /* first sub-tile of chunk 1 */
+    static constexpr int sb(int c) { return c == 0 ? 0 : c == 1 ? SB1 : NS; }
     static constexpr int piece0(int c) { return sb(c) * PF; }
     static constexpr int pieces(int c) {
         const int e = sb(c + 1);
         return ((e < S64 ? e : S64) - sb(c)) * PF + ((TAIL && e > S64) ? FR / 16 : 0);
     }
-    static constexpr int L(int c) { return (pieces(c) + 3) / 4; } /* per issuer wave (4 issuers) */
+    static constexpr int L(int c) { return (pieces(c) + 3) / 4; } /* per back wave */
     static constexpr int ks0(int c) { return 2 * sb(c); }
     static constexpr int ks1(int c) { return 2 * sb(c + 1) < KS ? 2 * sb(c + 1) : KS; }
-    /* X chunks issued after X(t) chunk j that may stay in flight at its wait */
-    static constexpr int newer(int j) {
-        int n = 0;
-        for (int m = 1; m <= 6; m++) n += L((j + m) % NCH);
-        return n;
-    }
 };
 
 template <int KS>
-struct FLay {
-    static constexpr int XST = FR * KS * 32 * 2;
-    static constexpr int OFF_W1 = 2 * XST;
+struct FLay6 {
+    static constexpr int XT = FR * KS * 32 * 2;            /* one X tile image */
+    static constexpr int OFF_W1 = XT;
     static constexpr int OFF_W2 = OFF_W1 + IMG_W1;
-    static constexpr int OFF_H1 = OFF_W2 + IMG_W2; /* x2 (front writes t, back reads t-1) */
+    static constexpr int OFF_W0L = OFF_W2 + IMG_W2;         /* last k-step of W0, 4 waves x 2 frags */
     static constexpr int IMG_H1 = FR * H1 * 2;
-    static constexpr int OFF_H2 = OFF_H1 + 2 * IMG_H1;
-    static constexpr int OFF_D3 = OFF_H2 + FR * H2 * 2;
+    static constexpr int OFF_H1 = OFF_W0L + 8 * 1024;       /* x3: tiles t (front), t-1, t-2 (back) */
+    static constexpr int IMG_H2 = FR * H2 * 2;
+    static constexpr int OFF_H2 = OFF_H1 + 3 * IMG_H1;      /* x2: tiles t-1 (P1/P2), t-2 (P3/P5) */
+    static constexpr int OFF_D3 = OFF_H2 + 2 * IMG_H2;
     static constexpr int OFF_D2 = OFF_D3 + FR * NO * 2;
-    static constexpr int OFF_LAB = OFF_D2 + FR * H2 * 2; /* 2 slots x 64 ints */
+    static constexpr int OFF_LAB = OFF_D2 + FR * H2 * 2;    /* 2 slots x 64 ints */
     static constexpr int OFF_RED = OFF_LAB + 2 * 256;
     static constexpr int TOTAL = OFF_RED + 128;
     static_assert(TOTAL <= 160 * 1024, "LDS");
@@ -125,11 +113,13 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                                                             float *__restrict__ gslab, float *__restrict__ loss_acc,
                                                             unsigned int *__restrict__ correct, int n_tiles,
                                                             int n_valid, int n_out) {
-    using LY = FLay<KS>;
-    using XP = FPlan<KS>;
+    using LY = FLay6<KS>;
+    using XP = FPlan6<KS>;
     constexpr int R = FR;
     constexpr int S64 = XP::S64;
-    constexpr int LB = LABELS ? 1 : 0;
+    constexpr int PF = XP::PF;
+    constexpr bool FRONT_ON = MODE != 2 && MODE != 3 && MODE != 11;
+    constexpr bool BACK_ON = MODE != 1 && MODE != 3 && MODE != 10;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -137,91 +127,16 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
     const int rw = wave & 3;     /* index within the role */
     const int r16 = lane & 15, q = lane >> 4;
     const LaneOff lo = lane_offsets(lane);
+    char *imgX = lds;
     char *imgW1 = lds + LY::OFF_W1, *imgW2 = lds + LY::OFF_W2;
-    char *imgH2 = lds + LY::OFF_H2, *imgD3 = lds + LY::OFF_D3, *imgD2 = lds + LY::OFF_D2;
+    char *imgD3 = lds + LY::OFF_D3, *imgD2 = lds + LY::OFF_D2;
     const int G = gridDim.x;
     const int nloc = (n_tiles - (int)blockIdx.x + G - 1) / G;
     const size_t ldx_b = (size_t)ldx * 2;
-    auto tile_of = [&](int u) { return (int)blockIdx.x + (u < nloc ? u : nloc - 1) * G; };
-
-    /* X staging (back waves): back wave w owns pieces p = w + 4 i (1 KiB each: 8 rows x 128 B of a
-     * 64-column sub-tile, or 16 rows x 64 B of the 32-column tail) of each chunk; a piece is
-     * loaded into VGPRs one stage ahead (global_load_dwordx4, 16 B per lane) and written
-     * into its LDS ring slot with ds_write_b128 at the image position LDS-DMA would give it.
-     * Plain loads are issued in a few cycles (an LDS-DMA piece costs the issuing wave
-     * ~60-180) and every vmcnt wait is the compiler's own. */
-    using C0 = std::integral_constant<int, 0>;
-    using C1 = std::integral_constant<int, 1>;
-    using C2 = std::integral_constant<int, 2>;
-    using C3 = std::integral_constant<int, 3>;
-    constexpr int PF = XP::PF;
-    constexpr int OFF1 = XP::L(0), OFF2 = OFF1 + XP::L(1), OFF3 = OFF2 + XP::L(2), NPW = OFF3 + XP::L(3);
-    auto poff = [](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        return c == 0 ? 0 : c == 1 ? OFF1 : c == 2 ? OFF2 : OFF3;
-    };
-    /* global byte offset (within the tile) and LDS image offset of piece p of a tile */
-    auto piece_addr = [&](int p, unsigned int &goff, int &loff) {
-        if (p < S64 * PF) {
-            const int sub = p / PF, rp = (p % PF) * 8;
-            const int r = rp + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
-            goff = (unsigned int)r * (unsigned int)ldx_b + (unsigned int)(sub * 64 + lc * 8) * 2u;
-            loff = sub * (R * 128) + rp * 128 + lane * 16;
-        } else {
-            const int rp = (p - S64 * PF) * 16; /* one 32-col tail sub-tile: pieces of 16 rows */
-            const int r = rp + (lane >> 2), cp = lane & 3;
-            const int col = S64 * 64 + ((cp ^ t32_g(r)) & 3) * 8;
-            goff = (unsigned int)r * (unsigned int)ldx_b + (unsigned int)col * 2u;
-            loff = S64 * (R * 128) + rp * 64 + lane * 16;
-        }
-    };
-    u32x4 xs[NPW]; /* this wave's pieces of the next tile */
-    auto load_piece = [&](int u, auto cc, int i) {
-        constexpr int c = decltype(cc)::value;
-        constexpr int P = XP::pieces(c), p0 = XP::piece0(c);
-        int p = rw + 4 * i;
-        p = p < P ? p : P - 1;
-        unsigned int goff;
-        int loff;
-        piece_addr(p0 + p, goff, loff);
-        xs[poff(cc) + i] = *(const u32x4 *)((const char *)(X + (size_t)tile_of(u) * R * ldx) + goff);
-    };
-    auto store_piece = [&](int u, auto cc, int i) {
-        constexpr int c = decltype(cc)::value;
-        constexpr int P = XP::pieces(c), p0 = XP::piece0(c);
-        int p = rw + 4 * i;
-        p = p < P ? p : P - 1;
-        unsigned int goff;
-        int loff;
-        piece_addr(p0 + p, goff, loff);
-        *(u32x4 *)(lds + (u & 1) * LY::XST + loff) = xs[poff(cc) + i];
-    };
-    auto load_chunk = [&](int u, auto cc) {
-#pragma unroll
-        for (int i = 0; i < XP::L(decltype(cc)::value); i++) load_piece(u, cc, i);
-    };
-    auto store_chunk = [&](int u, auto cc) {
-#pragma unroll
-        for (int i = 0; i < XP::L(decltype(cc)::value); i++) store_piece(u, cc, i);
-    };
-    /* labels of tile u: back wave 4 lanes 0..31 (register-staged like X) */
-    int lab_r = 0;
-    auto load_label = [&](int u) {
-        if constexpr (LABELS) lab_r = labels[clamp_sample_f(tile_of(u) * R + (lane & 31), n_valid)];
-    };
-    auto store_label = [&](int u) {
-        if constexpr (LABELS)
-            if (rw == 0 && lane < 32) ((int *)(lds + LY::OFF_LAB + (u & 1) * 256))[lane] = lab_r;
-    };
-    /* a back wave's delta1 stores: h1 tiles 2w, 2w+1 x sample groups 0, 1 */
-    auto store_d1 = [&](int s0, const bf16x4 (&o)[2][2]) {
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int sg = 0; sg < 2; sg++)
-                *(bf16x4 *)(D1 + (size_t)(s0 + sg * 16 + r16) * H1 + (2 * rw + i) * 16 + 4 * q) = o[i][sg];
-    };
-    auto mark = [&](int t, int i) {
+    auto tile_of = [&](int u) __attribute__((always_inline)) { return (int)blockIdx.x + (u < nloc ? u : nloc - 1) * G; };
+    auto h1img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_H1 + (u % 3) * LY::IMG_H1; };
+    auto h2img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_H2 + (u & 1) * LY::IMG_H2; };
+    auto mark = [&](int t, int i) __attribute__((always_inline)) {
         if constexpr (MODE >= 9) {
             if (blockIdx.x == 0 && t < 7) {
                 const unsigned long long m = __builtin_amdgcn_s_memtime();
@@ -229,8 +144,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             }
         }
     };
-
-    auto emark = [&](int i) { /* kernel-level marks (stage-7 row, marks 0..3) */
+    auto emark = [&](int i) __attribute__((always_inline)) {
         if constexpr (MODE >= 9) {
             if (blockIdx.x == 0) {
                 const unsigned long long m = __builtin_amdgcn_s_memtime();
@@ -239,47 +153,49 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         }
     };
     emark(0);
-    using T1 = std::true_type;
-    using F0 = std::false_type;
-    constexpr bool FRONT_ON = MODE != 2 && MODE != 3 && MODE != 11;
-    constexpr bool BACK_ON = MODE != 1 && MODE != 3 && MODE != 10;
     float my_loss = 0.f;
     unsigned int my_hit = 0;
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
 
-    /* The roles run separate loops with the same barrier sequence (4 per stage), so the
+    /* The roles run separate loops with the same barrier sequence (2 per stage), so the
      * register allocator gives the front's W0 and the back's staging / chain registers the
      * same physical registers.  Budget at 2 waves per SIMD: 128 VGPRs + 128 AGPRs. */
     if (!back) {
         /* ====================== front waves 0-3 ====================== */
-        /* W0 (neurons 32w .. 32w+31 x K0, the MFMA A operand) over both register files:
-         * 128 AGPRs (w0[0][*] and the first W0_A1 fragments of w0[1]) and the rest in VGPRs
-         * beside the accumulators and the fragment prefetch.  Plain loads (the compiler
-         * tracks them), then pinned into their file. */
-        constexpr int W0_A1 = 3;
-        bf16x8 w0[2][KS];
+        /* the last k-step's A fragments live in LDS (frees 8 VGPRs for the prefetch) */
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            glds16(W0f + ((size_t)((2 * rw + i) * KS + KS - 1) * 64 + lane) * 8,
+                   lds + LY::OFF_W0L + (rw * 2 + i) * 1024);
+        /* k-steps 0 .. KS-2 over both register files: 128 AGPRs (w0[0][*] and the first
+         * W0_A1 fragments of w0[1]) and the rest in VGPRs; plain loads, then pinned */
+        constexpr int KR = KS - 1, W0_A1 = 32 - KR - 4; /* 4 AGPR fragments left for the accumulators */
+        bf16x8 w0[2][KR];
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int ks = 0; ks < KS; ks++)
+            for (int ks = 0; ks < KR; ks++)
                 w0[i][ks] = *(const bf16x8 *)(W0f + ((size_t)((2 * rw + i) * KS + ks) * 64 + lane) * 8);
+        __builtin_amdgcn_s_waitcnt(0xF70); /* vmcnt(0): W0 (and the LDS-DMA above) complete */
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int ks = 0; ks < KS; ks++) {
+            for (int ks = 0; ks < KR; ks++) {
                 if (i == 0 || ks < W0_A1) asm volatile("" : "+a"(w0[i][ks]));
                 else asm volatile("" : "+v"(w0[i][ks]));
             }
         emark(1);
         f32x4 acc[2][2]; /* H1 tiles (neuron group 2w+i, sample group sg) */
-        constexpr int PD = 1;
-        auto front_chunk = [&](const char *imgX, auto cc, auto pinc) {
+        constexpr int PD = 2;
+        auto front_chunk = [&](auto cc) __attribute__((always_inline)) {
             constexpr int c = decltype(cc)::value;
             constexpr int k0 = XP::ks0(c), k1 = XP::ks1(c), NSL = k1 - k0;
             if constexpr (c == 0) {
 #pragma unroll
                 for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            bf16x8 bq[PD][2];
+            bf16x8 bq[PD][2], wl[2];
 #pragma unroll
             for (int d = 0; d < PD; d++) {
                 bq[d][0] = x_frag<R, S64>(imgX, 0, k0 + d, lane);
@@ -292,34 +208,37 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                     bq[j % PD][0] = x_frag<R, S64>(imgX, 0, ks + PD, lane);
                     bq[j % PD][1] = x_frag<R, S64>(imgX, 16, ks + PD, lane);
                 }
-                acc[0][0] = mfma(w0[0][ks], b0, acc[0][0]);
-                acc[1][0] = mfma(w0[1][ks], b0, acc[1][0]);
-                acc[0][1] = mfma(w0[0][ks], b1, acc[0][1]);
-                acc[1][1] = mfma(w0[1][ks], b1, acc[1][1]);
+                if constexpr (ks + 2 == KS) { /* the last k-step's A fragments, one step ahead */
+#pragma unroll
+                    for (int i = 0; i < 2; i++)
+                        wl[i] = *(const bf16x8 *)(lds + LY::OFF_W0L + ((rw * 2 + i) * 64 + lane) * 16);
+                }
+                if constexpr (ks < KR) {
+                    acc[0][0] = mfma(w0[0][ks], b0, acc[0][0]);
+                    acc[1][0] = mfma(w0[1][ks], b0, acc[1][0]);
+                    acc[0][1] = mfma(w0[0][ks], b1, acc[0][1]);
+                    acc[1][1] = mfma(w0[1][ks], b1, acc[1][1]);
+                } else {
+                    acc[0][0] = mfma(wl[0], b0, acc[0][0]);
+                    acc[1][0] = mfma(wl[1], b0, acc[1][0]);
+                    acc[0][1] = mfma(wl[0], b1, acc[0][1]);
+                    acc[1][1] = mfma(wl[1], b1, acc[1][1]);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             });
         };
-        auto fstage = [&](int t, auto FWc, auto PINc) {
+        auto fstage = [&](int t, auto FWc) __attribute__((always_inline)) {
             constexpr bool FW = decltype(FWc)::value && FRONT_ON;
-            const char *imgX = lds + (t & 1) * LY::XST;
-            char *H1w = lds + LY::OFF_H1 + (t & 1) * LY::IMG_H1;
             mark(t, 0);
             lds_barrier();
             mark(t, 1);
-            if constexpr (FW) front_chunk(imgX, C0{}, PINc);
+            if constexpr (FW) front_chunk(C0{});
             mark(t, 2);
             lds_barrier();
             mark(t, 3);
-            if constexpr (FW) front_chunk(imgX, C1{}, PINc);
-            mark(t, 4);
-            lds_barrier();
-            mark(t, 5);
-            if constexpr (FW) front_chunk(imgX, C2{}, PINc);
-            mark(t, 6);
-            lds_barrier();
-            mark(t, 7);
             if constexpr (FW) {
-                front_chunk(imgX, C3{}, PINc);
+                front_chunk(C1{});
+                char *H1w = h1img(t);
 #pragma unroll
                 for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -331,34 +250,84 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                     }
             }
         };
-        for (int t = 0; t < nloc; t++) fstage(t, T1{}, F0{});
-        fstage(nloc, F0{}, F0{});
+        for (int t = 0; t < nloc; t++) fstage(t, std::true_type{});
+        fstage(nloc, std::false_type{});
+        fstage(nloc + 1, std::false_type{});
         emark(2);
     } else {
         /* ====================== back waves 4-7 ====================== */
-        /* prologue: X(0) -> LDS by LDS-DMA, W1 / W2 -> LDS, labels(0), one full wait, then
-         * X(1) and labels(1) into the staging registers */
+        /* X staging: back wave w owns pieces p = w + 4 i (1 KiB each: 8 rows x 128 B of a
+         * 64-column sub-tile, or 16 rows x 64 B of the 32-column tail) of each chunk; loaded
+         * into VGPRs one stage ahead, written with ds_write_b128 where LDS-DMA would put it */
+        constexpr int NPW = XP::L(0) > XP::L(1) ? XP::L(0) : XP::L(1);
+        auto piece_addr = [&](int p, unsigned int &goff, int &loff) __attribute__((always_inline)) {
+            if (p < S64 * PF) {
+                const int sub = p / PF, rp = (p % PF) * 8;
+                const int r = rp + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
+                goff = (unsigned int)r * (unsigned int)ldx_b + (unsigned int)(sub * 64 + lc * 8) * 2u;
+                loff = sub * (R * 128) + rp * 128 + lane * 16;
+            } else {
+                const int rp = (p - S64 * PF) * 16; /* the 32-col tail sub-tile: pieces of 16 rows */
+                const int r = rp + (lane >> 2), cp = lane & 3;
+                const int col = S64 * 64 + ((cp ^ t32_g(r)) & 3) * 8;
+                goff = (unsigned int)r * (unsigned int)ldx_b + (unsigned int)col * 2u;
+                loff = S64 * (R * 128) + rp * 64 + lane * 16;
+            }
+        };
+        u32x4 xs[NPW]; /* this wave's pieces of the next chunk to write (one interval ahead) */
+        auto load_chunk = [&](int u, auto cc) __attribute__((always_inline)) {
+            constexpr int c = decltype(cc)::value;
+            constexpr int P = XP::pieces(c), p0 = XP::piece0(c);
+#pragma unroll
+            for (int i = 0; i < XP::L(c); i++) {
+                int p = rw + 4 * i;
+                p = p < P ? p : P - 1;
+                unsigned int goff;
+                int loff;
+                piece_addr(p0 + p, goff, loff);
+                xs[i] = *(const u32x4 *)((const char *)(X + (size_t)tile_of(u) * R * ldx) + goff);
+            }
+        };
+        auto store_chunk = [&](auto cc) __attribute__((always_inline)) {
+            constexpr int c = decltype(cc)::value;
+            constexpr int P = XP::pieces(c), p0 = XP::piece0(c);
+#pragma unroll
+            for (int i = 0; i < XP::L(c); i++) {
+                int p = rw + 4 * i;
+                p = p < P ? p : P - 1;
+                unsigned int goff;
+                int loff;
+                piece_addr(p0 + p, goff, loff);
+                *(u32x4 *)(imgX + loff) = xs[i];
+            }
+        };
+        /* labels of tile u: back wave 4, lanes 0..31 (register-staged like X) */
+        int lab_r = 0;
+        auto load_label = [&](int u) __attribute__((always_inline)) {
+            if constexpr (LABELS) lab_r = labels[clamp_sample_f(tile_of(u) * R + (lane & 31), n_valid)];
+        };
+        auto store_label = [&](int u) __attribute__((always_inline)) {
+            if constexpr (LABELS)
+                if (rw == 0 && lane < 32) ((int *)(lds + LY::OFF_LAB + (u & 1) * 256))[lane] = lab_r;
+        };
+
+        /* prologue: X(0) chunk 0 -> LDS by LDS-DMA, W1 / W2 -> LDS, one full wait, then
+         * chunk 1 of X(0) and chunk 0 of X(1) into the staging registers */
         {
-            constexpr int NP = XP::S64 * PF + (XP::TAIL ? R / 16 : 0);
+            constexpr int P = XP::pieces(0);
             const char *g = (const char *)(X + (size_t)tile_of(0) * R * ldx);
 #pragma unroll
-            for (int i = 0; i < (NP + 3) / 4; i++) {
+            for (int i = 0; i < XP::L(0); i++) {
                 int p = rw + 4 * i;
-                p = p < NP ? p : NP - 1;
-                glds_x_piece_sv<R, S64>(g, (unsigned int)ldx_b, lds, p, lane);
+                p = p < P ? p : P - 1;
+                glds_x_piece_sv<R, S64>(g, (unsigned int)ldx_b, imgX, p, lane);
             }
         }
         load_img4f<H2, H1>(W1, H1, imgW1, rw, lane);
         load_img4f<NO, H2>(W2, H2, imgW2, rw, lane);
-        load_label(0);
         __builtin_amdgcn_s_waitcnt(0xF70); /* vmcnt(0) */
         emark(1);
-        store_label(0);
-        load_chunk(1, C0{});
-        load_chunk(1, C1{});
-        load_chunk(1, C2{});
-        load_chunk(1, C3{});
-        load_label(1);
+        load_chunk(0, C1{});
 
         f32x4 g1acc[2][4], g2acc[2]; /* G1: h1 tiles 2w+i x h2 tiles 0..3; G2: h2 tile w x o tiles */
 #pragma unroll
@@ -370,128 +339,139 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         const int n_ot = n_out > 16 ? 2 : 1;
         const float inv_nout = 1.0f / (float)n_out;
 
-        auto bstage = [&](int t, auto BWc) {
-            constexpr bool BW = decltype(BWc)::value && BACK_ON;
-            const int tb = t - 1;
-            char *H1r = lds + LY::OFF_H1 + ((t + 1) & 1) * LY::IMG_H1; /* tile t-1 */
-            const int s0b = tile_of(tb < 0 ? 0 : tb) * R;
+        /* P1: H2(u) = f(H1(u) W1^T), h2 tile w, sample groups 0, 1 */
+        auto p1 = [&](int u) __attribute__((always_inline)) {
+            const char *H1r = h1img(u);
+            char *H2w = h2img(u);
+            f32x4 a[2];
+            a[0] = a[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < H1; k += 32) {
+                const bf16x8 wa = rd_row<H2>(imgW1, lo, rw * 16, k);
+                a[0] = mfma(wa, rd_row<R>(H1r, lo, 0, k), a[0]);
+                a[1] = mfma(wa, rd_row<R>(H1r, lo, 16, k), a[1]);
+            }
+#pragma unroll
+            for (int hs = 0; hs < 2; hs++) {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[hs][r]);
+                *(bf16x4 *)wr_ptr<R>(H2w, lo, hs * 16, rw * 16) = o;
+            }
+        };
+        /* P2: output layer + loss + delta3 of tile u, sample group = w (back waves 4, 5) */
+        auto p2 = [&](int u) __attribute__((always_inline)) {
+            const char *H2r = h2img(u);
+            const int sg = rw;
+            f32x4 z[2];
+            z[0] = z[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int s = tile_of(u) * R + sg * 16 + r16;
+            const int lab = LABELS ? ((const int *)(lds + LY::OFF_LAB + (u & 1) * 256))[sg * 16 + r16] : -1;
+            if (n_ot > 1) {
+#pragma unroll
+                for (int k = 0; k < H2; k += 32) {
+                    const bf16x8 b = rd_row<R>(H2r, lo, sg * 16, k);
+                    z[0] = mfma(rd_row<NO>(imgW2, lo, 0, k), b, z[0]);
+                    z[1] = mfma(rd_row<NO>(imgW2, lo, 16, k), b, z[1]);
+                }
+                output_layer<TYPE, LABELS, R, 2>(z, lab, T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
+                                                 sg * 16, lane, inv_nout, my_loss, my_hit);
+            } else {
+#pragma unroll
+                for (int k = 0; k < H2; k += 32)
+                    z[0] = mfma(rd_row<NO>(imgW2, lo, 0, k), rd_row<R>(H2r, lo, sg * 16, k), z[0]);
+                output_layer<TYPE, LABELS, R, 1>(z, lab, T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
+                                                 sg * 16, lane, inv_nout, my_loss, my_hit);
+            }
+        };
+        /* P3: delta2(u) = (delta3 W2) f'(H2); P5: G2 += delta3^T H2 */
+        auto p35 = [&](int u) __attribute__((always_inline)) {
+            char *H2r = h2img(u);
+            const bf16x8 wa = rd_tr<NO>(imgW2, lo, 0, rw * 16); /* A[h2][o] = W2[o][h2] */
+#pragma unroll
+            for (int hs = 0; hs < 2; hs++) {
+                const f32x4 a = mfma(wa, rd_row<R>(imgD3, lo, hs * 16, 0), f32x4{0.f, 0.f, 0.f, 0.f});
+                const bf16x4 h = *(const bf16x4 *)wr_ptr<R>(H2r, lo, hs * 16, rw * 16);
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)h[r]));
+                *(bf16x4 *)wr_ptr<R>(imgD2, lo, hs * 16, rw * 16) = o;
+            }
+            const bf16x8 h2t = rd_tr<R>(H2r, lo, 0, rw * 16);
+            g2acc[0] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 0), g2acc[0]);
+            if (n_ot > 1) g2acc[1] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 16), g2acc[1]);
+        };
+        /* P4: delta1(u) = (delta2 W1) f'(H1) -> HBM; P6: G1 += delta2^T H1 */
+        auto p46 = [&](int u) __attribute__((always_inline)) {
+            char *H1r = h1img(u);
+            const int s0 = tile_of(u) * R;
+            f32x4 a4[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) a4[i][0] = a4[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < H2; k += 32) {
+                const bf16x8 d0 = rd_row<R>(imgD2, lo, 0, k), d1 = rd_row<R>(imgD2, lo, 16, k);
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const bf16x8 a = rd_tr<H2>(imgW1, lo, k, (2 * rw + i) * 16); /* A[h1][h2] = W1[h2][h1] */
+                    a4[i][0] = mfma(a, d0, a4[i][0]);
+                    a4[i][1] = mfma(a, d1, a4[i][1]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int sg = 0; sg < 2; sg++) {
+                    const bf16x4 hv = *(const bf16x4 *)wr_ptr<R>(H1r, lo, sg * 16, (2 * rw + i) * 16);
+                    bf16x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) o[r] = (__bf16)(a4[i][sg][r] * dbipolar((float)hv[r]));
+                    *(bf16x4 *)(D1 + (size_t)(s0 + sg * 16 + r16) * H1 + (2 * rw + i) * 16 + 4 * q) = o;
+                }
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const bf16x8 a = rd_tr<R>(H1r, lo, 0, (2 * rw + i) * 16);
+#pragma unroll
+                for (int t2 = 0; t2 < 4; t2++) g1acc[i][t2] = mfma(a, rd_tr<R>(imgD2, lo, 0, t2 * 16), g1acc[i][t2]);
+            }
+        };
 
-            /* ---- interval 0: P1: H2 = f(H1 W1^T), h2 tile w, sample groups 0, 1 ---- */
+        /* stage t: B12 = P1 / P2 of tile t-1 valid, B34 = P3..P6 of tile t-2 valid */
+        auto bstage = [&](int t, auto B12c, auto B34c) __attribute__((always_inline)) {
+            constexpr bool B12 = decltype(B12c)::value && BACK_ON;
+            constexpr bool B34 = decltype(B34c)::value && BACK_ON;
+            /* ---- interval 0 ---- */
             mark(t, 0);
             lds_barrier();
             mark(t, 1);
-            store_chunk(t + 1, C0{});
-            load_chunk(t + 2, C0{});
-            if constexpr (BW) {
-                f32x4 a[2];
-                a[0] = a[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < H1; k += 32) {
-                    const bf16x8 wa = rd_row<H2>(imgW1, lo, rw * 16, k);
-                    a[0] = mfma(wa, rd_row<R>(H1r, lo, 0, k), a[0]);
-                    a[1] = mfma(wa, rd_row<R>(H1r, lo, 16, k), a[1]);
-                }
-#pragma unroll
-                for (int hs = 0; hs < 2; hs++) {
-                    bf16x4 o;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[hs][r]);
-                    *(bf16x4 *)wr_ptr<R>(imgH2, lo, hs * 16, rw * 16) = o;
-                }
-            }
-            /* ---- interval 1: P2: output layer + loss + delta3 (back waves 4, 5) ---- */
+            store_chunk(C1{}); /* chunk 1 of tile t (loaded one interval ago) */
+            load_chunk(t + 1, C0{});
+            if (t >= 1) store_label(t - 1);
+            load_label(t);
+            if constexpr (B12) p1(t - 1);
+            if constexpr (B34) p35(t - 2);
+            /* ---- interval 1 ---- */
             mark(t, 2);
             lds_barrier();
             mark(t, 3);
-            store_chunk(t + 1, C1{});
-            load_chunk(t + 2, C1{});
-            if (BW && rw < 2) {
-                const int sg = rw;
-                f32x4 z[2];
-                z[0] = z[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const int s = s0b + sg * 16 + r16;
-                const int lab = LABELS ? ((const int *)(lds + LY::OFF_LAB + (tb & 1) * 256))[sg * 16 + r16] : -1;
-                if (n_ot > 1) {
-#pragma unroll
-                    for (int k = 0; k < H2; k += 32) {
-                        const bf16x8 b = rd_row<R>(imgH2, lo, sg * 16, k);
-                        z[0] = mfma(rd_row<NO>(imgW2, lo, 0, k), b, z[0]);
-                        z[1] = mfma(rd_row<NO>(imgW2, lo, 16, k), b, z[1]);
-                    }
-                    output_layer<TYPE, LABELS, R, 2>(z, lab, T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
-                                                     sg * 16, lane, inv_nout, my_loss, my_hit);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < H2; k += 32)
-                        z[0] = mfma(rd_row<NO>(imgW2, lo, 0, k), rd_row<R>(imgH2, lo, sg * 16, k), z[0]);
-                    output_layer<TYPE, LABELS, R, 1>(z, lab, T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
-                                                     sg * 16, lane, inv_nout, my_loss, my_hit);
-                }
+            store_chunk(C0{}); /* chunk 0 of tile t+1 */
+            load_chunk(t + 1, C1{});
+            if constexpr (B12) {
+                if (rw < 2) p2(t - 1);
             }
-            /* ---- interval 2: P3: delta2 = (delta3 W2) f'(H2); P5: G2 += delta3^T H2 ---- */
-            mark(t, 4);
-            lds_barrier();
-            mark(t, 5);
-            store_chunk(t + 1, C2{});
-            load_chunk(t + 2, C2{});
-            if constexpr (BW) {
-                const bf16x8 wa = rd_tr<NO>(imgW2, lo, 0, rw * 16); /* A[h2][o] = W2[o][h2] */
-#pragma unroll
-                for (int hs = 0; hs < 2; hs++) {
-                    const f32x4 a = mfma(wa, rd_row<R>(imgD3, lo, hs * 16, 0), f32x4{0.f, 0.f, 0.f, 0.f});
-                    const bf16x4 h = *(const bf16x4 *)wr_ptr<R>(imgH2, lo, hs * 16, rw * 16);
-                    bf16x4 o;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)h[r]));
-                    *(bf16x4 *)wr_ptr<R>(imgD2, lo, hs * 16, rw * 16) = o;
-                }
-                const bf16x8 h2t = rd_tr<R>(imgH2, lo, 0, rw * 16);
-                g2acc[0] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 0), g2acc[0]);
-                if (n_ot > 1) g2acc[1] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 16), g2acc[1]);
-            }
-            /* ---- interval 3: P4: delta1 = (delta2 W1) f'(H1) -> HBM; P6: G1 += delta2^T H1 ---- */
-            mark(t, 6);
-            lds_barrier();
-            mark(t, 7);
-            store_chunk(t + 1, C3{});
-            load_chunk(t + 2, C3{});
-            store_label(t + 1);
-            load_label(t + 2);
-            if constexpr (BW) {
-                f32x4 a4[2][2];
-#pragma unroll
-                for (int i = 0; i < 2; i++) a4[i][0] = a4[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < H2; k += 32) {
-                    const bf16x8 d0 = rd_row<R>(imgD2, lo, 0, k), d1 = rd_row<R>(imgD2, lo, 16, k);
-#pragma unroll
-                    for (int i = 0; i < 2; i++) {
-                        const bf16x8 a = rd_tr<H2>(imgW1, lo, k, (2 * rw + i) * 16); /* A[h1][h2] = W1[h2][h1] */
-                        a4[i][0] = mfma(a, d0, a4[i][0]);
-                        a4[i][1] = mfma(a, d1, a4[i][1]);
-                    }
-                }
-                bf16x4 o[2][2];
-#pragma unroll
-                for (int i = 0; i < 2; i++)
-#pragma unroll
-                    for (int sg = 0; sg < 2; sg++) {
-                        const bf16x4 hv = *(const bf16x4 *)wr_ptr<R>(H1r, lo, sg * 16, (2 * rw + i) * 16);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) o[i][sg][r] = (__bf16)(a4[i][sg][r] * dbipolar((float)hv[r]));
-                    }
-                store_d1(s0b, o);
-#pragma unroll
-                for (int i = 0; i < 2; i++) {
-                    const bf16x8 a = rd_tr<R>(H1r, lo, 0, (2 * rw + i) * 16);
-#pragma unroll
-                    for (int t2 = 0; t2 < 4; t2++)
-                        g1acc[i][t2] = mfma(a, rd_tr<R>(imgD2, lo, 0, t2 * 16), g1acc[i][t2]);
-                }
-            }
+            if constexpr (B34) p46(t - 2);
         };
-        bstage(0, F0{});
-        for (int t = 1; t <= nloc; t++) bstage(t, T1{});
+        using T1 = std::true_type;
+        using F0 = std::false_type;
+        bstage(0, F0{}, F0{});
+        if (nloc >= 2) {
+            bstage(1, T1{}, F0{});
+            for (int t = 2; t < nloc; t++) bstage(t, T1{}, T1{});
+            bstage(nloc, T1{}, T1{});
+        } else {
+            bstage(1, T1{}, F0{});
+        }
+        bstage(nloc + 1, F0{}, T1{});
         emark(2);
 
         /* per-block gradient slab [G1 (H2 x H1) | G2 (NO x H2)] (layout of mlp3_fused) */
@@ -516,7 +496,6 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         sh[wave] = my_hit;
     }
     __syncthreads();
-    emark(3);
     if (tid == 0) {
         float a = 0.f;
         unsigned int h = 0;
@@ -538,10 +517,10 @@ int launch_front(const void *X, int ldx, const void *W0f, const void *W1, const 
         static bool attr = false;                                                                                 \
         if (!attr) {                                                                                              \
             (void)hipFuncSetAttribute((const void *)mlp3_front_kernel<TYPE, LABELS, KS, MD>,                      \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, FLay<KS>::TOTAL);               \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, FLay6<KS>::TOTAL);               \
             attr = true;                                                                                          \
         }                                                                                                         \
-        hipLaunchKernelGGL((mlp3_front_kernel<TYPE, LABELS, KS, MD>), dim3(grid), dim3(512), FLay<KS>::TOTAL,     \
+        hipLaunchKernelGGL((mlp3_front_kernel<TYPE, LABELS, KS, MD>), dim3(grid), dim3(512), FLay6<KS>::TOTAL,     \
                            stream, (const __bf16 *)X, ldx, (const __bf16 *)W0f, (const __bf16 *)W1,               \
                            (const __bf16 *)W2, labels, T, ldt, t_hi, t_lo, (__bf16 *)D1, gslab, loss_acc, correct, \
                            Bp / FR, n_valid, n_out);                                                              \

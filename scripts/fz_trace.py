@@ -33,8 +33,14 @@ for w in range(NW):
         works.append(wk.mean().item())
     st = (tr[w, 3:7, 1] - tr[w, 2:6, 1]).mean().item()
     print(f"w{w}: work I0..I3 = " + " ".join(f"{x:6.0f}" for x in works) + f"   stage = {st:6.0f}")
-if os.environ.get("HPNN_FRONT", "") == "f":  # mlp3_front: kernel-level marks in the stage-7 row of every wave
+if os.environ.get("HPNN_FRONT", "") == "f":  # mlp3_front: 2 intervals per stage, kernel marks
     raw = torch.tensor(native().mlp3_fused_trace(), dtype=torch.float64).view(8, 8, 8)
+    print("mlp3_front: per-wave work of interval 0 / 1 and stage length (stages 2-5 mean)")
+    for w in range(8):
+        i0 = (raw[w, 2:6, 2] - raw[w, 2:6, 1]).mean().item()
+        i1 = (raw[w, 3:7, 0] - raw[w, 2:6, 3]).mean().item()
+        st = (raw[w, 3:7, 1] - raw[w, 2:6, 1]).mean().item()
+        print(f"w{w}: I0 {i0:6.0f}  I1 {i1:6.0f}  stage {st:6.0f}")
     t0 = raw[:, 7, 0].min()
     for w in range(8):
         e = raw[w, 7, :3] - t0
