@@ -395,22 +395,21 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
 #undef HPNN_NT
 }
 
-template <int TM, int TN, int RING = 73728, int MAXST = 6>
+template <int TM, int TN, int RING = 73728, int MAXST = 6, int BKR = 32, int WM = 2, int WN = 2>
 int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s, const TnTail &tail) {
     const int tiles_n = N / TN, tiles_m = M / TM;
     const int units = Bt / 64;
-    /* 32-row stages, ring of ~72 KiB (2 workgroups per CU), or the deep ring (~144 KiB,
-     * one workgroup per CU: twice the bytes in flight per CU for a grid of <= 1 GEMM
-     * workgroup per CU, where the stream is latency-bound by the ring depth) */
-    constexpr int BKR = 32;
+    /* BKR-row stages (default 32), ring of ~72 KiB (2 workgroups per CU), or the deep ring
+     * (~144 KiB, one workgroup per CU: twice the bytes in flight per CU for a grid of <= 1
+     * GEMM workgroup per CU, where the stream is latency-bound by the ring depth) */
     constexpr int STAGE = BKR * (TM + TN) * 2;
     constexpr int ST = (RING / STAGE) < 2 ? 2 : ((RING / STAGE) > MAXST ? MAXST : (RING / STAGE));
     const int tiles = tiles_m * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST>), dim3(tiles * splits + tail.blocks), dim3(256), 0, s,
-                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, tiles,
-                       xcd_map, tail);
+    hipLaunchKernelGGL((gemm_tn_pipe_kernel<TM, TN, BKR, ST, WM, WN>), dim3(tiles * splits + tail.blocks),
+                       dim3(WM * WN * 64), 0, s, (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units,
+                       splits, tiles_n, tiles, xcd_map, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -434,6 +433,20 @@ int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int
                 hipStream_t s, const TnTail &t) {
     const int dm = tn_deep_mode();
     const long wgs = (long)(N / 128) * (M / TM) * splits;
+    /* HPNN_TN_VAR (experiments, TM = 160 / N % 128 == 0): 1 = 8 waves, 32-row stages, 72 KiB
+     * ring; 2 = 8 waves, 64-row stages, 144 KiB; 3 = 4 waves, 64-row stages, 144 KiB;
+     * 4 = 8 waves, 32-row stages, 144 KiB; 5 = 8 waves, 64-row stages, 72 KiB.  MNIST G0
+     * (800 x 128 over 65536 rows, 48 splits), scripts/g0_sweep.py: default 29.6-29.8 us,
+     * 1: 31.8, 2: 30.4, 3: 28.6-29.0, 4: 33.6, 5: 28.9; D stored pre-tiled for linear
+     * 1 KiB LDS-DMA pieces (a DT template flag, timing probe): 27.9-30.1 -- none a clear win */
+    static const int var = [] { const char *e = getenv("HPNN_TN_VAR"); return e ? atoi(e) : 0; }();
+    if constexpr (TM == 160) {
+        if (N % 128 == 0 && var == 1) return launch_tn_t<TM, 128, 73728, 6, 32, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+        if (N % 128 == 0 && var == 2) return launch_tn_t<TM, 128, 147456, 6, 64, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+        if (N % 128 == 0 && var == 3) return launch_tn_t<TM, 128, 147456, 6, 64, 2, 2>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+        if (N % 128 == 0 && var == 4) return launch_tn_t<TM, 128, 147456, 8, 32, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+        if (N % 128 == 0 && var == 5) return launch_tn_t<TM, 128, 73728, 6, 64, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
+    }
     if (N % 128 == 0 && (dm == 1 || (dm < 0 && wgs <= HPNN_TN_DEEP_MAX_WG)))
         return launch_tn_t<TM, 128, 147456, 8>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     if (N % 128 == 0) return launch_tn_t<TM, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);

@@ -68,12 +68,12 @@ struct FLay6 {
     static constexpr int OFF_W2 = OFF_W1 + IMG_W1;
     static constexpr int OFF_W0L = OFF_W2 + IMG_W2;         /* last k-step of W0, 4 waves x 2 frags */
     static constexpr int IMG_H1 = FR * H1 * 2;
-    static constexpr int OFF_H1 = OFF_W0L + 8 * 1024;       /* x3: tiles t (front), t-1, t-2 (back) */
+    static constexpr int OFF_H1 = OFF_W0L + 8 * 1024;       /* x4: tiles t (front), t-1, t-2, t-3 (back) */
     static constexpr int IMG_H2 = FR * H2 * 2;
-    static constexpr int OFF_H2 = OFF_H1 + 3 * IMG_H1;      /* x2: tiles t-1 (P1/P2), t-2 (P3/P5) */
+    static constexpr int OFF_H2 = OFF_H1 + 4 * IMG_H1;      /* x2: tiles t-1 (P1/P2), t-2 (P3/P5) */
     static constexpr int OFF_D3 = OFF_H2 + 2 * IMG_H2;
-    static constexpr int OFF_D2 = OFF_D3 + FR * NO * 2;
-    static constexpr int OFF_LAB = OFF_D2 + FR * H2 * 2;    /* 2 slots x 64 ints */
+    static constexpr int OFF_D2 = OFF_D3 + FR * NO * 2;     /* x2: tiles t-2 (P3 -> P4), t-3 (P6) */
+    static constexpr int OFF_LAB = OFF_D2 + 2 * FR * H2 * 2; /* 2 slots x 64 ints */
     static constexpr int OFF_RED = OFF_LAB + 2 * 256;
     static constexpr int TOTAL = OFF_RED + 128;
     static_assert(TOTAL <= 160 * 1024, "LDS");
@@ -129,12 +129,13 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
     const LaneOff lo = lane_offsets(lane);
     char *imgX = lds;
     char *imgW1 = lds + LY::OFF_W1, *imgW2 = lds + LY::OFF_W2;
-    char *imgD3 = lds + LY::OFF_D3, *imgD2 = lds + LY::OFF_D2;
+    char *imgD3 = lds + LY::OFF_D3;
     const int G = gridDim.x;
     const int nloc = (n_tiles - (int)blockIdx.x + G - 1) / G;
     const size_t ldx_b = (size_t)ldx * 2;
     auto tile_of = [&](int u) __attribute__((always_inline)) { return (int)blockIdx.x + (u < nloc ? u : nloc - 1) * G; };
-    auto h1img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_H1 + (u % 3) * LY::IMG_H1; };
+    auto h1img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_H1 + (u & 3) * LY::IMG_H1; };
+    auto d2img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_D2 + (u & 1) * (FR * H2 * 2); };
     auto h2img = [&](int u) __attribute__((always_inline)) { return lds + LY::OFF_H2 + (u & 1) * LY::IMG_H2; };
     auto mark = [&](int t, int i) __attribute__((always_inline)) {
         if constexpr (MODE >= 9) {
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         for (int t = 0; t < nloc; t++) fstage(t, std::true_type{});
         fstage(nloc, std::false_type{});
         fstage(nloc + 1, std::false_type{});
+        fstage(nloc + 2, std::false_type{});
         emark(2);
     } else {
         /* ====================== back waves 4-7 ====================== */
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
         /* P3: delta2(u) = (delta3 W2) f'(H2); P5: G2 += delta3^T H2 */
         auto p35 = [&](int u) __attribute__((always_inline)) {
             char *H2r = h2img(u);
+            char *imgD2 = d2img(u);
             const bf16x8 wa = rd_tr<NO>(imgW2, lo, 0, rw * 16); /* A[h2][o] = W2[o][h2] */
 #pragma unroll
             for (int hs = 0; hs < 2; hs++) {
@@ -401,9 +404,10 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             g2acc[0] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 0), g2acc[0]);
             if (n_ot > 1) g2acc[1] = mfma(h2t, rd_tr<R>(imgD3, lo, 0, 16), g2acc[1]);
         };
-        /* P4: delta1(u) = (delta2 W1) f'(H1) -> HBM; P6: G1 += delta2^T H1 */
-        auto p46 = [&](int u) __attribute__((always_inline)) {
+        /* P4: delta1(u) = (delta2 W1) f'(H1) -> HBM */
+        auto p4 = [&](int u) __attribute__((always_inline)) {
             char *H1r = h1img(u);
+            const char *imgD2 = d2img(u);
             const int s0 = tile_of(u) * R;
             f32x4 a4[2][2];
 #pragma unroll
@@ -428,6 +432,11 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
                     for (int r = 0; r < 4; r++) o[r] = (__bf16)(a4[i][sg][r] * dbipolar((float)hv[r]));
                     *(bf16x4 *)(D1 + (size_t)(s0 + sg * 16 + r16) * H1 + (2 * rw + i) * 16 + 4 * q) = o;
                 }
+        };
+        /* P6: G1 += delta2(u)^T H1(u) */
+        auto p6 = [&](int u) __attribute__((always_inline)) {
+            char *H1r = h1img(u);
+            char *imgD2 = d2img(u);
 #pragma unroll
             for (int i = 0; i < 2; i++) {
                 const bf16x8 a = rd_tr<R>(H1r, lo, 0, (2 * rw + i) * 16);
@@ -436,11 +445,13 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             }
         };
 
-        /* stage t: B12 = P1 / P2 of tile t-1 valid, B34 = P3..P6 of tile t-2 valid */
-        auto bstage = [&](int t, auto B12c, auto B34c) __attribute__((always_inline)) {
+        /* stage t: B12 = P1 / P2 of tile t-1, B34 = P3 / P5 / P4 of tile t-2, B6 = P6 of
+         * tile t-3 (each flag: that tile exists) */
+        auto bstage = [&](int t, auto B12c, auto B34c, auto B6c) __attribute__((always_inline)) {
             constexpr bool B12 = decltype(B12c)::value && BACK_ON;
             constexpr bool B34 = decltype(B34c)::value && BACK_ON;
-            /* ---- interval 0 ---- */
+            constexpr bool B6 = decltype(B6c)::value && BACK_ON;
+            /* ---- interval 0: P1(t-1) | P3, P5(t-2) | P6(t-3) ---- */
             mark(t, 0);
             lds_barrier();
             mark(t, 1);
@@ -450,7 +461,8 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             load_label(t);
             if constexpr (B12) p1(t - 1);
             if constexpr (B34) p35(t - 2);
-            /* ---- interval 1 ---- */
+            if constexpr (B6) p6(t - 3);
+            /* ---- interval 1: P2(t-1) (waves 4, 5) | P4(t-2) ---- */
             mark(t, 2);
             lds_barrier();
             mark(t, 3);
@@ -459,19 +471,27 @@ __global__ __launch_bounds__(512, 1) void mlp3_front_kernel(const __bf16 *__rest
             if constexpr (B12) {
                 if (rw < 2) p2(t - 1);
             }
-            if constexpr (B34) p46(t - 2);
+            if constexpr (B34) p4(t - 2);
         };
         using T1 = std::true_type;
         using F0 = std::false_type;
-        bstage(0, F0{}, F0{});
-        if (nloc >= 2) {
-            bstage(1, T1{}, F0{});
-            for (int t = 2; t < nloc; t++) bstage(t, T1{}, T1{});
-            bstage(nloc, T1{}, T1{});
+        /* tiles 0 .. nloc-1; stage t runs P1/P2 of t-1, P3-P5 of t-2, P6 of t-3 */
+        bstage(0, F0{}, F0{}, F0{});
+        if (nloc >= 3) {
+            bstage(1, T1{}, F0{}, F0{});
+            bstage(2, T1{}, T1{}, F0{});
+            for (int t = 3; t < nloc; t++) bstage(t, T1{}, T1{}, T1{});
+            bstage(nloc, T1{}, T1{}, T1{});
+            bstage(nloc + 1, F0{}, T1{}, T1{});
+        } else if (nloc == 2) {
+            bstage(1, T1{}, F0{}, F0{});
+            bstage(2, T1{}, T1{}, F0{});
+            bstage(3, F0{}, T1{}, T1{});
         } else {
-            bstage(1, T1{}, F0{});
+            bstage(1, T1{}, F0{}, F0{});
+            bstage(2, F0{}, T1{}, F0{});
         }
-        bstage(nloc + 1, F0{}, T1{});
+        bstage(nloc + 2, F0{}, F0{}, T1{});
         emark(2);
 
         /* per-block gradient slab [G1 (H2 x H1) | G2 (NO x H2)] (layout of mlp3_fused) */
