@@ -1,23 +1,37 @@
 /*
- * One-shot xGMI all-reduce (include/libhpnn/xar.h).
+ * xGMI all-reduce (include/libhpnn/xar.h): one-shot and two-shot, one launch per call.
  *
  * Each rank owns two fine-grained (uncached) device allocations that every peer maps
- * through hipIpc: a data buffer (max_bytes) and a signal block (barrier flags).  One
- * kernel launch per all-reduce; workgroup b owns float4 slice b of the buffer:
- *   1. copy its slice of `in` into this rank's data buffer;
- *   2. barrier "start": write epoch e into start[b][rank] of every peer's signal block,
- *      wait until start[b][p] >= e for every p in this rank's block;
- *   3. out[slice] = sum_{p = 0..world-1} data_p[slice] (fixed rank order: every rank
- *      computes the same bits);
- *   4. barrier "end" (same protocol): no rank refills its data slice while a peer may
- *      still read it.
- * Epochs are per workgroup, kept in this rank's signal block and advanced by the kernel,
- * so launches captured in a HIP graph replay correctly; all ranks issue the same
- * sequence of all-reduces, so the epochs agree.  Every wait is bounded by a wall-clock
- * timeout: a missing peer sets the error word, never hangs the GPU.
+ * through hipIpc: a data buffer of two halves (max_bytes each, used alternately by
+ * consecutive calls) and a signal block (barrier flags).  Workgroup b of every rank
+ * owns the same element set on every rank.
  *
- * Fine-grained memory keeps peer reads coherent without cache maintenance; the
- * system-scope fences order the data stores before the flag stores.
+ * one-shot (every rank reads every peer's whole buffer; best for 2 ranks, where both
+ * algorithms move the same bytes per link, and for tiny buffers):
+ *   1. copy its elements of `in` into this rank's data half (local slab sums included);
+ *   2. barrier A: write epoch e into A[b][rank] of every peer, wait for A[b][p] >= e;
+ *   3. out = sum_{p = 0..W-1} data_p (fixed rank order: identical bits on every rank).
+ * two-shot (reduce-scatter + all-gather through the same buffers; with W ranks each
+ * link carries 2/W of the buffer instead of all of it: 4x fewer link bytes at W = 8):
+ *   1. copy in as above (block b owns sub-slice b of EVERY rank's shard);
+ *   2. barrier A;
+ *   3. this rank's shard: s = sum_p data_p[shard] in rank order, written to out and
+ *      back into this rank's data half (peers only read their own shards in step 3);
+ *   4. barrier B: every shard is reduced;
+ *   5. out[shard q] = data_q[shard q] for every peer q.
+ * No closing barrier: call e+2 reuses the data half of call e only after passing its
+ * barrier A of call e+1, which no peer signals before its call-e kernel (all its reads
+ * of that half) has completed.
+ * Epochs are per workgroup (every call runs the full fixed grid, so they stay equal),
+ * kept in this rank's signal block and advanced by the kernel,
+ * so launches captured in a HIP graph replay correctly; all ranks issue the same
+ * sequence of all-reduces (same sizes, same mode), so the epochs and halves agree.  Every
+ * wait is bounded by a wall-clock timeout: a missing peer sets the error word, never
+ * hangs the GPU.
+ *
+ * Fine-grained uncached memory keeps peer reads coherent without cache maintenance:
+ * waiting for the data stores' acknowledgements orders them before the flag stores (no
+ * L2 writeback), and an acquire invalidate precedes the peer reads.
  * Replaces the reference's hub copies through GPU0 (cuda_ann.cu EXP model).
  */
 #include <hip/hip_runtime.h>
@@ -29,8 +43,7 @@
 namespace {
 
 struct Signal {
-    unsigned int start[HPNN_XAR_MAX_BLOCKS][HPNN_XAR_MAX_RANKS];
-    unsigned int end[HPNN_XAR_MAX_BLOCKS][HPNN_XAR_MAX_RANKS];
+    unsigned int flag[2][HPNN_XAR_MAX_BLOCKS][HPNN_XAR_MAX_RANKS]; /* barriers A, B */
     unsigned int epoch[HPNN_XAR_MAX_BLOCKS];
     unsigned int error;
 };
@@ -48,16 +61,24 @@ __device__ __forceinline__ unsigned int flag_load(unsigned int *p) {
 }
 
 /* threads 0..world-1 signal peer t and wait for peer t; bounded spin */
-__device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world, int b, unsigned int e, bool end,
-                                         unsigned long long timeout) {
-    __threadfence_system(); /* this thread's data stores before any flag store */
+__device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world, int b, unsigned int e, int which,
+                                         unsigned long long timeout, int light) {
+    /* release: this thread's data stores complete before any flag store.  Everything a
+     * peer reads lives in the uncached (MTYPE UC) buffer, which no L2 holds, so waiting
+     * for the store acknowledgements is enough; __threadfence_system() would also write
+     * back every dirty L2 line of the XCD (buffer_wbl2) -- measured 18.6 -> 8.5 us per
+     * 437 KB call at world 1 and 36.6 -> 12.5 us at world 2 (scripts/xar_bench.py);
+     * HPNN_XAR_FENCE=1 restores the full fence */
+    if (light)
+        __builtin_amdgcn_s_waitcnt(0);
+    else
+        __threadfence_system();
     __syncthreads();
     const int t = threadIdx.x;
     if (t < world) {
-        Signal *peer = P.sig[t];
-        flag_store(end ? &peer->end[b][rank] : &peer->start[b][rank], e);
+        flag_store(&P.sig[t]->flag[which][b][rank], e);
         Signal *me = P.sig[rank];
-        unsigned int *f = end ? &me->end[b][t] : &me->start[b][t];
+        unsigned int *f = &me->flag[which][b][t];
         const unsigned long long t0 = wall_clock64();
         while (flag_load(f) < e) {
             __builtin_amdgcn_s_sleep(1);
@@ -68,7 +89,10 @@ __device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world,
         }
     }
     __syncthreads();
-    __threadfence_system();
+    if (light) /* acquire: invalidate (no writeback) before reading peer data */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else
+        __threadfence_system();
 }
 
 /* the input of a call: up to HPNN_XAR_MAX_SEGS segments laid end to end in the output;
@@ -107,8 +131,30 @@ __device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
     return a;
 }
 
-__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in,
-                                                  float4 *__restrict__ out, long n4, unsigned long long timeout) {
+/* sum of element i over the first `world` data halves, rank order */
+__device__ __forceinline__ float4 sum_peers(const XarPeers &P, long half4, int world, long i) {
+    float4 v[HPNN_XAR_MAX_RANKS];
+#pragma unroll
+    for (int p = 0; p < HPNN_XAR_MAX_RANKS; p++)
+        if (p < world) v[p] = P.buf[p][half4 + i];
+    float4 s = v[0];
+#pragma unroll
+    for (int p = 1; p < HPNN_XAR_MAX_RANKS; p++)
+        if (p < world) {
+            s.x += v[p].x;
+            s.y += v[p].y;
+            s.z += v[p].z;
+            s.w += v[p].w;
+        }
+    return s;
+}
+
+/* TWO = false: one-shot, element slice b of the whole buffer per workgroup.
+ * TWO = true: shard s = [s * sh, min((s + 1) * sh, n4)), workgroup b owns
+ * [s * sh + b * per, ...+ per) of every shard */
+template <bool TWO>
+__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
+                                                  long n4, long half_stride4, unsigned long long timeout, int light) {
     const int b = blockIdx.x;
     Signal *me = P.sig[rank];
     __shared__ unsigned int s_ep;
@@ -119,28 +165,42 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
     }
     __syncthreads();
     const unsigned int e = s_ep;
-    const long per = (n4 + gridDim.x - 1) / gridDim.x;
-    const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
-    float4 *mine = P.buf[rank];
-    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
-    xbarrier(P, rank, world, b, e, false, timeout);
-    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        float4 v[HPNN_XAR_MAX_RANKS];
-#pragma unroll
-        for (int p = 0; p < HPNN_XAR_MAX_RANKS; p++)
-            if (p < world) v[p] = P.buf[p][i];
-        float4 s = v[0];
-#pragma unroll
-        for (int p = 1; p < HPNN_XAR_MAX_RANKS; p++)
-            if (p < world) {
-                s.x += v[p].x;
-                s.y += v[p].y;
-                s.z += v[p].z;
-                s.w += v[p].w;
-            }
-        out[i] = s;
+    const long half4 = (e & 1) ? half_stride4 : 0;
+    float4 *mine = P.buf[rank] + half4;
+    if constexpr (!TWO) {
+        const long per = (n4 + gridDim.x - 1) / gridDim.x;
+        const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
+        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
+        xbarrier(P, rank, world, b, e, 0, timeout, light);
+        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = sum_peers(P, half4, world, i);
+    } else {
+        const long sh = (n4 + world - 1) / world;
+        const long per = (sh + gridDim.x - 1) / gridDim.x;
+        auto range = [&](int s, long &lo, long &hi) {
+            const long s_end = (long)(s + 1) * sh < n4 ? (long)(s + 1) * sh : n4;
+            lo = (long)s * sh + (long)b * per;
+            hi = lo + per < s_end ? lo + per : s_end;
+        };
+        long lo, hi;
+        for (int s = 0; s < world; s++) {
+            range(s, lo, hi);
+            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
+        }
+        xbarrier(P, rank, world, b, e, 0, timeout, light);
+        range(rank, lo, hi);
+        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            const float4 v = sum_peers(P, half4, world, i);
+            mine[i] = v;
+            out[i] = v;
+        }
+        xbarrier(P, rank, world, b, e, 1, timeout, light);
+        for (int q = 1; q < world; q++) { /* start after this rank: spread the link load */
+            const int s = (rank + q) % world;
+            range(s, lo, hi);
+            const float4 *src = P.buf[s] + half4;
+            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = src[i];
+        }
     }
-    xbarrier(P, rank, world, b, e, true, timeout);
 }
 
 struct IpcHandles {
@@ -158,6 +218,9 @@ struct hpnn_xar {
     XarPeers peers = {};
     bool opened[HPNN_XAR_MAX_RANKS] = {};
     unsigned long long timeout = 0;
+    int mode = 0;     /* HPNN_XAR_MODE: 0 auto, 1 one-shot, 2 two-shot */
+    int light = 1;    /* HPNN_XAR_FENCE=1 -> 0: full system fences, see xbarrier */
+    int blocks = 128; /* HPNN_XAR_BLOCKS (same on every rank), <= HPNN_XAR_MAX_BLOCKS */
 };
 
 extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
@@ -167,7 +230,7 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     c->world = world;
     c->max_bytes = (max_bytes + 255) / 256 * 256;
     if (hipGetDevice(&c->device) != hipSuccess ||
-        hipExtMallocWithFlags(&c->buf, c->max_bytes, hipDeviceMallocUncached) != hipSuccess ||
+        hipExtMallocWithFlags(&c->buf, 2 * c->max_bytes, hipDeviceMallocUncached) != hipSuccess ||
         hipExtMallocWithFlags((void **)&c->sig, sizeof(Signal), hipDeviceMallocUncached) != hipSuccess ||
         hipMemset(c->sig, 0, sizeof(Signal)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         NN_ERROR(stderr, "xgmi all-reduce: device allocation failed\n");
@@ -179,6 +242,12 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     const char *e = getenv("HPNN_XAR_TIMEOUT_MS");
     const long ms = e ? atol(e) : 5000;
     c->timeout = (unsigned long long)(ms > 0 ? ms : 5000) * (unsigned long long)(khz > 0 ? khz : 100000);
+    const char *m = getenv("HPNN_XAR_MODE");
+    c->mode = m ? atoi(m) : 0;
+    const char *fe = getenv("HPNN_XAR_FENCE");
+    c->light = !(fe && fe[0] == '1');
+    const char *nb = getenv("HPNN_XAR_BLOCKS");
+    if (nb && atoi(nb) > 0) c->blocks = atoi(nb) < HPNN_XAR_MAX_BLOCKS ? atoi(nb) : HPNN_XAR_MAX_BLOCKS;
     c->peers.buf[rank] = (float4 *)c->buf;
     c->peers.sig[rank] = c->sig;
     return c;
@@ -224,11 +293,25 @@ static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipS
     for (int p = 0; p < c->world; p++)
         if (!c->peers.buf[p]) return -3; /* not opened */
     const long n4 = count / 4;
-    long blocks = (n4 + 127) / 128; /* ~half a float4 per thread: many CUs share the slab reads */
-    if (blocks > HPNN_XAR_MAX_BLOCKS) blocks = HPNN_XAR_MAX_BLOCKS;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(xar_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank, c->world, in,
-                       (float4 *)out, n4, c->timeout);
+    /* two-shot from 4 ranks and 64 KiB up (each link then carries 2/W of the buffer
+     * instead of all of it, for one extra barrier); the choice depends only on values
+     * every rank shares, so all ranks run the same protocol */
+    const bool two = c->mode == 2 || (c->mode == 0 && c->world >= 4 && count * 4 >= (64 << 10));
+    /* the grid is the same for every call: every workgroup then takes part in every call,
+     * so the per-workgroup epochs (and the data half they select) stay equal across the
+     * grid -- with a size-dependent grid a workgroup skipping a call would flip halves
+     * against the others and could refill elements a peer still reads.  128 workgroups:
+     * half the CUs, so when several ranks share one GPU (the 1-GPU tests) a rank's
+     * spinning workgroups never occupy every CU while a peer's full-CU kernel (the fused
+     * MNIST front) still has to run before that peer reaches its all-reduce */
+    const long blocks = c->blocks;
+    const long half4 = (long)(c->max_bytes / 16);
+    if (two)
+        hipLaunchKernelGGL(xar_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank, c->world,
+                           in, (float4 *)out, n4, half4, c->timeout, c->light);
+    else
+        hipLaunchKernelGGL(xar_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,
+                           c->world, in, (float4 *)out, n4, half4, c->timeout, c->light);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -1,15 +1,19 @@
 /*
- * libhpnn xGMI all-reduce: one-shot peer-to-peer sum all-reduce for small buffers
- * between the GPUs of one node (csrc/dist/xgmi_ar.hip).
+ * libhpnn xGMI all-reduce: peer-to-peer sum all-reduce for small buffers between the
+ * GPUs of one node (csrc/dist/xgmi_ar.hip).
  *
  * Why: MNIST's whole gradient is 437 KB.  A ring all-reduce (RCCL) of that size over
  * 8 MI355X is latency-bound -- 2(N-1) = 14 dependent hops -- while each GPU has a direct
  * xGMI link to every other GPU.  Here every rank publishes its buffer in device memory
- * that every peer maps (hipIpc handles), then one kernel per rank does, per workgroup
- * slice: copy in -> signal all peers -> wait for all peers -> read the slice from all
- * N buffers and sum them in rank order (identical bits on every rank, deterministic)
- * -> signal/wait again (so a buffer is never overwritten while a peer still reads it).
- * One launch, two flag barriers, 7 concurrent link reads instead of 14 ring hops.
+ * that every peer maps (hipIpc handles), and one kernel per rank runs either
+ *   one-shot: copy in -> flag barrier -> read the slice from all N buffers and sum them
+ *             in rank order (identical bits on every rank, deterministic); or
+ *   two-shot: copy in -> barrier -> reduce this rank's 1/N shard from all N buffers ->
+ *             barrier -> read the N-1 reduced shards from their owners (each xGMI link
+ *             carries 2/N of the buffer instead of all of it).
+ * Auto choice (HPNN_XAR_MODE=0): two-shot from 4 ranks and 64 KiB, else one-shot
+ * (HPNN_XAR_MODE=1 / 2 force one).  Consecutive calls alternate between two halves of
+ * the buffer, so no closing barrier is needed before a buffer is refilled.
  *
  * Graph capture: the barrier epochs live in device memory and are advanced by the
  * kernel itself, so a captured launch replays correctly any number of times.

@@ -1,11 +1,12 @@
-"""One-shot xGMI all-reduce (csrc/dist/xgmi_ar.hip) with two real processes.
+"""xGMI all-reduce (csrc/dist/xgmi_ar.hip), one-shot and two-shot, with 2-4 real processes.
 
 The GPU box has one MI355X, so both ranks run on device 0: the peer buffers are mapped
 through hipIpc exactly as on an 8-GPU node (the data path is then local HBM instead of
 an xGMI link, the protocol -- IPC mapping, flag barriers, epochs, fixed-order sum -- is
 the same).  Checked: sums of several bucket sizes against the host sum, in-place use,
-repeated calls, HIP-graph capture + replays, and the bounded barrier: a rank whose peer
-never arrives reports a timeout instead of hanging."""
+repeated calls (alternating buffer halves, mixed one-/two-shot calls in auto mode at 4
+ranks), slab-sum inputs, HIP-graph capture + replays, and the bounded barrier: a rank
+whose peer never arrives reports a timeout instead of hanging."""
 import os
 import socket
 
@@ -22,9 +23,10 @@ def _data(rank, n, it):
     return torch.randn(n, generator=g)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     try:
         os.environ["HPNN_XAR_TIMEOUT_MS"] = "400"
+        os.environ["HPNN_XAR_MODE"] = mode
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         from hpnn_amd._lib import native
@@ -51,6 +53,17 @@ def _worker(rank, world, port, q):
                 e = (out.cpu() - ref).abs().max().item()
                 if e > 1e-5:
                     errs.append(f"size {sz} it {it}: max err {e}")
+        # slab inputs: out = sum over ranks of [sum of 3 slabs of seg 0 | seg 1 (1 slab)]
+        sl = torch.stack([_data(rank, 4096, 50 + k) for k in range(3)]).cuda()
+        tl = _data(rank, 1000, 60).cuda()
+        out = torch.empty(5096, device="cuda")
+        n.xar_all_reduce_slabs_f32(x, [(sl.data_ptr(), sl.stride(0), 3, 4096), (tl.data_ptr(), 0, 1, 1000)],
+                                   out.data_ptr(), s)
+        torch.cuda.synchronize()
+        ref = torch.cat([sum(_data(r, 4096, 50 + k) for r in range(world) for k in range(3)),
+                         sum(_data(r, 1000, 60) for r in range(world))])
+        if (out.cpu() - ref).abs().max().item() > 1e-4:
+            errs.append("slab-sum all-reduce mismatch")
         # graph capture: the kernel advances its own barrier epochs on every replay
         buf = _data(rank, 9280, 99).cuda()
         base = buf.clone()
@@ -87,13 +100,14 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_xgmi_allreduce_two_processes(gpu):
+@pytest.mark.parametrize("world,mode", [(2, "1"), (2, "2"), (3, "2"), (4, "0")])
+def test_xgmi_allreduce_processes(gpu, world, mode):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=100) for _ in ps)
@@ -101,4 +115,4 @@ def test_xgmi_allreduce_two_processes(gpu):
         p.join(timeout=30)
         if p.is_alive():
             p.kill()
-    assert res == {0: [], 1: []}, res
+    assert res == {r: [] for r in range(world)}, res
