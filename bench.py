@@ -172,7 +172,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "hip_graph": bool(use_graph),
                 "grad_allreduce": ("none" if not dp.active else
-                                   ("xgmi-oneshot+rccl" if dp.native is not None and dp.native.xar else
+                                   ("xgmi+rccl" if dp.native is not None and dp.native.xar else
                                     ("rccl-native" if dp.native is not None else "torch.distributed"))),
                 "steps_per_graph": min(gsteps, args.steps) if use_graph else 0,
             },

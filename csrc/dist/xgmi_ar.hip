@@ -107,28 +107,49 @@ struct XarIn {
     int nseg;
 };
 
+__device__ __forceinline__ void add4(float4 &a, const float4 &b) {
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+}
+
+/* local sum of element i of the input: slabs s = k (mod 8) accumulate in acc[k], eight
+ * loads in flight per thread (the copy-in of a 48-slab weight gradient is latency-bound:
+ * 2 loads in flight took 15.2 us per MNIST step), combined in a fixed tree */
 __device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
     int j = 0;
     while (j + 1 < in.nseg && i >= in.end4[j]) j++;
     const long li = i - (j ? in.end4[j - 1] : 0);
     const float4 *p = in.src[j] + li;
     const long st = in.stride4[j];
-    float4 a = p[0];
-    if (in.S[j] > 1) {
-        float4 b = p[st];
-        int s = 2;
-        for (; s + 1 < in.S[j]; s += 2) {
-            const float4 x = p[(long)s * st], y = p[(long)(s + 1) * st];
-            a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-            b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    const int S = in.S[j];
+    if (S == 1) return p[0];
+    constexpr int U = 8;
+    float4 acc[U];
+    int s = 0;
+    if (S >= U) {
+#pragma unroll
+        for (int k = 0; k < U; k++) acc[k] = p[(long)k * st];
+        for (s = U; s + U <= S; s += U) {
+            float4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) v[k] = p[(long)(s + k) * st];
+#pragma unroll
+            for (int k = 0; k < U; k++) add4(acc[k], v[k]);
         }
-        if (s < in.S[j]) {
-            const float4 x = p[(long)s * st];
-            a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-        }
-        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < U; k++) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    return a;
+#pragma unroll
+    for (int k = 0; k < U; k++)
+        if (s + k < S) add4(acc[k], p[(long)(s + k) * st]);
+#pragma unroll
+    for (int w = 1; w < U; w *= 2)
+#pragma unroll
+        for (int k = 0; k < U; k += 2 * w) add4(acc[k], acc[k + w]);
+    return acc[0];
 }
 
 /* sum of element i over the first `world` data halves, rank order */

@@ -78,7 +78,9 @@ class NativeComm:
         if not self.h:
             raise RuntimeError("ncclCommInitRank failed (see stderr)")
         self.xar = 0
-        if self.world > 1 and _xar_wanted(self.world):
+        # HPNN_DP_FORCE=1 (one rank): attach it anyway, so the N > 1 step path (slab sums in
+        # the all-reduce's copy-in, then the update) can be timed on a single-GPU box
+        if (self.world > 1 or os.environ.get("HPNN_DP_FORCE", "0") == "1") and _xar_wanted(self.world):
             self._attach_xar(int(os.environ.get("HPNN_XAR_MAX_BYTES", str(4 << 20))))
 
     def _attach_xar(self, max_bytes):
