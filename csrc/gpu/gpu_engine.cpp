@@ -450,7 +450,7 @@ struct Batched {
         int r;
         if (fused_x) {
             r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab, acc,
-                                (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, s);
+                                (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, 0, s);
             r = r > 0 ? 0 : (r ? r : -1);
         } else {
             r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0], HPNN_EPI_ACT, 0,
@@ -554,7 +554,7 @@ struct Batched {
             const int slab_f = hpnn_mlp3_slab_floats();
             if (fused_x) {
                 r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab,
-                                    acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, s);
+                                    acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, 0, s);
                 r = r > 0 ? 0 : (r ? r : -1);
             } else {
                 r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0],

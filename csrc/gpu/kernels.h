@@ -58,6 +58,22 @@ int hpnn_gemm_tn_bf16_reduce(const void *D, int ldd, const void *H, int ldh, flo
                              int Bt, int splits, const float *rslab, int rS, long rstride, long rn, int rgroups,
                              float *rout, hipStream_t stream);
 
+/* hpnn_gemm_tn_bf16(_reduce) with register-staged operands (kernels_g0.hip): coalesced
+ * vector loads P steps ahead -> T32 LDS image -> transposed MFMA reads.  M % 160 or 128,
+ * N % 128, Bt % 64.  rslab == NULL: no tail reduction. */
+int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
+                    int splits, const float *rslab, int rS, long rstride, long rn, int rgroups, float *rout,
+                    hipStream_t stream);
+/* weight gradient of hpnn_gemm_tn_bf16 over FRAGMENT-MAJOR operands (kernels_g0.hip):
+ * Dg [Bt/32][N/16][64][8], Hg [Bt/32][M/16][64][8], lane l = 16 g + r of fragment (t, cb)
+ * holding A[32 t + 8 g + j][16 cb + r] (j < 8); slab[s][n][m] as hpnn_gemm_tn_bf16.
+ * Bt, M, N multiples of 32.  _reduce: plus hpnn_reduce_groups on appended workgroups. */
+int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits,
+                        hipStream_t stream);
+int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits,
+                               const float *rslab, int rS, long rstride, long rn, int rgroups, float *rout,
+                               hipStream_t stream);
+
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)
  *   loss_acc[slot] += sum of per-sample loss over valid rows (slot array, above)
@@ -126,11 +142,13 @@ int hpnn_mlp3_mid(const void *H1g, const void *W1, const void *W1t, const void *
  * plus per-block [G1 | G2] slabs (grid of them, same layout as hpnn_mlp3_mid).  W0 is
  * read once per workgroup into registers from its fragment-major copy W0f (see
  * hpnn_sgd_update_multi); K0 in {256, 512, 800, 832, 896}, Bp % 32 == 0.  grid <= 0:
- * one workgroup per CU.  Returns the grid used (> 0) or an error (< 0). */
+ * one workgroup per CU.  d1fm: delta1 written fragment-major ([Bp/32][8][64][8], the
+ * operand layout of hpnn_gemm_fm_direct) instead of row-major [Bp x 128].  Returns the
+ * grid used (> 0) or an error (< 0). */
 int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,
                     const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                     float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
-                    hipStream_t stream);
+                    int d1fm, hipStream_t stream);
 /* role-split variant of hpnn_mlp3_fused (kernels_mlp3f.hip, selected by HPNN_FRONT=f for
  * K0 >= 800): same arguments, outputs and slab layout; grid > 0 required */
 int hpnn_mlp3_front(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
                                                             float t_lo, __bf16 *__restrict__ D1,
                                                             float *__restrict__ gslab, float *__restrict__ loss_acc,
                                                             unsigned int *__restrict__ correct, int n_tiles,
-                                                            int n_valid, int n_out) {
+                                                            int n_valid, int n_out, int d1fm) {
     using LY = Lay<KS>;
     using XP = XPlan<KS>;
     constexpr int R = FR;
@@ -269,6 +269,39 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
             f32x4 a4[2][2];
 #pragma unroll
             for (int i = 0; i < 2; i++) a4[i][0] = a4[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (d1fm) {
+                /* fragment-major delta1 for the direct-load G0 GEMM (kernels_g0.hip):
+                 * chunk (tile, h1 block) = [g][r][j] = delta1[tile*32 + 8g + j][16 block + r].
+                 * Operands swapped: D[row = sample 4q + r][col = h1 r16], so every lane owns
+                 * 4 consecutive samples of one neuron = 8 contiguous bytes of its chunk;
+                 * f'(H1) of the same 4 samples comes from one transposed LDS read. */
+#pragma unroll
+                for (int k = 0; k < H2; k += 32) {
+                    const bf16x8 d0 = rd_row<R>(imgD2, lo, 0, k), d1 = rd_row<R>(imgD2, lo, 16, k);
+#pragma unroll
+                    for (int i = 0; i < 2; i++) {
+                        const bf16x8 a = rd_tr<H2>(imgW1, lo, k, (2 * iw + i) * 16);
+                        a4[i][0] = mfma(d0, a, a4[i][0]);
+                        a4[i][1] = mfma(d1, a, a4[i][1]);
+                    }
+                }
+                __bf16 *chunk0 = D1 + (size_t)(s0b / R) * (H1 / 16) * 512;
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int sg = 0; sg < 2; sg++) {
+                        const int h = (2 * iw + i) * 16;
+                        const s16x4 hr = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s16x4 *)(H1r + t32<R>(sg * 16 + 4 * q + (r16 >> 2), h + 4 * (r16 & 3))));
+                        const bf16x4 hv = __builtin_bit_cast(bf16x4, hr);
+                        bf16x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) o[r] = (__bf16)(a4[i][sg][r] * dbipolar((float)hv[r]));
+                        const int g = 2 * sg + (q >> 1);
+                        *(bf16x4 *)(chunk0 + (size_t)(2 * iw + i) * 512 + (g * 16 + r16) * 8 + 4 * (q & 1)) = o;
+                    }
+                return;
+            }
 #pragma unroll
             for (int k = 0; k < H2; k += 32) {
                 const bf16x8 d0 = rd_row<R>(imgD2, lo, 0, k), d1 = rd_row<R>(imgD2, lo, 16, k);
@@ -415,7 +448,7 @@ int fused_grid(int Bp, int grid) {
 template <int TYPE, bool LABELS, int KS>
 int launch_fused(const void *X, int ldx, const void *W0f, const void *W1, const void *W2, const int *labels,
                  const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab, float *loss_acc,
-                 unsigned int *correct, int Bp, int n_valid, int n_out, int grid, hipStream_t stream) {
+                 unsigned int *correct, int Bp, int n_valid, int n_out, int grid, int d1fm, hipStream_t stream) {
     static const int mode = [] { const char *e = getenv("HPNN_FZ_MODE"); return e ? atoi(e) : 0; }();
 #define HPNN_FZL(MD)                                                                                             \
     do {                                                                                                         \
@@ -428,7 +461,7 @@ int launch_fused(const void *X, int ldx, const void *W0f, const void *W1, const 
         hipLaunchKernelGGL((mlp3_fused_kernel<TYPE, LABELS, KS, MD>), dim3(grid), dim3(512), Lay<KS>::TOTAL,     \
                            stream, (const __bf16 *)X, ldx, (const __bf16 *)W0f, (const __bf16 *)W1,              \
                            (const __bf16 *)W2, labels, T, ldt, t_hi, t_lo, (__bf16 *)D1, gslab, loss_acc, correct, \
-                           Bp / FR, n_valid, n_out);                                                             \
+                           Bp / FR, n_valid, n_out, d1fm);                                                       \
     } while (0)
     if constexpr (TYPE == 2 && LABELS && KS == 25) {
         switch (mode) {
@@ -454,10 +487,11 @@ int launch_fused(const void *X, int ldx, const void *W0f, const void *W1, const 
 template <int KS>
 int launch_fused_k(const void *X, int ldx, const void *W0f, const void *W1, const void *W2, const int *labels,
                    const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab, float *loss_acc,
-                   unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid, hipStream_t stream) {
+                   unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid, int d1fm,
+                   hipStream_t stream) {
 #define HPNN_FZ(TY, LB)                                                                                         \
     return launch_fused<TY, LB, KS>(X, ldx, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct, \
-                                    Bp, n_valid, n_out, grid, stream)
+                                    Bp, n_valid, n_out, grid, d1fm, stream)
     if (labels) {
         if (type == 2) HPNN_FZ(2, true);
         if (type == 0) HPNN_FZ(0, true);
@@ -482,18 +516,18 @@ extern "C" int hpnn_mlp3_fused_grid(int Bp, int grid) { return Bp > 0 && Bp % FR
 extern "C" int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,
                                const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1,
                                float *gslab, float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out,
-                               int type, int grid, hipStream_t stream) {
+                               int type, int grid, int d1fm, hipStream_t stream) {
     if (Bp <= 0 || Bp % FR || n_out > NO || n_out < 1 || ldx % 8 || ldx < K0) return -2;
     if (!labels && !T) return -1;
     grid = fused_grid(Bp, grid);
-    /* HPNN_FRONT=f: the role-split kernel (kernels_mlp3f.hip) */
-    if (front_split() && K0 >= 800)
+    /* HPNN_FRONT=f: the role-split kernel (kernels_mlp3f.hip; row-major delta1 only) */
+    if (front_split() && K0 >= 800 && !d1fm)
         return hpnn_mlp3_front(X, ldx, K0, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct,
                                Bp, n_valid, n_out, type, grid, stream);
 #define HPNN_FK(K_)                                                                                             \
     if (K0 == K_)                                                                                               \
     return launch_fused_k<K_ / 32>(X, ldx, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct, \
-                                   Bp, n_valid, n_out, type, grid, stream)
+                                   Bp, n_valid, n_out, type, grid, d1fm, stream)
     HPNN_FK(800);
     HPNN_FK(256);
     HPNN_FK(512);

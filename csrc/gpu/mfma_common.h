@@ -222,5 +222,34 @@ __device__ __forceinline__ float wave_sum(float v) {
     return rows_sum(v);
 }
 
+/* Optional tail work of a TN launch: a grouped slab reduction (reduce_groups_kernel of
+ * kernels_mlp3.hip: out[g*ostride + i] = sum of slabs [g*SG, min(S, (g+1)*SG)), float4 i)
+ * run by extra workgroups appended to the GEMM grid.  The fused MNIST step reduces its
+ * [G1 | G2] block slabs this way: the workgroups fill the CUs the 240-tile GEMM leaves
+ * idle, and a launch (plus its serialized ~5 us) disappears from the step. */
+struct TnTail {
+    const float *slab;
+    float *out;
+    long stride, n4, ostride;
+    int S, SG, bx, blocks;
+};
+
+__device__ __forceinline__ void tn_tail_reduce(const TnTail &t, int v) {
+    const long e = (long)(v % t.bx) * 256 + threadIdx.x;
+    const int g = v / t.bx;
+    if (e >= t.n4) return;
+    const int s_end = min(t.S, (g + 1) * t.SG);
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    int s = g * t.SG;
+    for (; s + 3 < s_end; s += 4) {
+        a0 += ((const f32x4 *)(t.slab + (long)s * t.stride))[e];
+        a1 += ((const f32x4 *)(t.slab + (long)(s + 1) * t.stride))[e];
+        a2 += ((const f32x4 *)(t.slab + (long)(s + 2) * t.stride))[e];
+        a3 += ((const f32x4 *)(t.slab + (long)(s + 3) * t.stride))[e];
+    }
+    for (; s < s_end; s++) a0 += ((const f32x4 *)(t.slab + (long)s * t.stride))[e];
+    ((f32x4 *)(t.out + (long)g * t.ostride))[e] = (a0 + a1) + (a2 + a3);
+}
+
 }  // namespace hpnn
 #endif

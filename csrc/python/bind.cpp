@@ -96,10 +96,10 @@ PYBIND11_MODULE(_native, m) {
     m.def("mlp3_slab_floats", []() { return hpnn_mlp3_slab_floats(); });
     m.def("mlp3_fused", [](uptr X, int ldx, int K0, uptr W0f, uptr W1, uptr W2, uptr labels, uptr T, int ldt,
                            float t_hi, float t_lo, uptr D1, uptr gslab, uptr loss, uptr correct, int Bp, int n_valid,
-                           int n_out, int type, int grid, uptr stream) {
+                           int n_out, int type, int grid, int d1fm, uptr stream) {
         const int rc = hpnn_mlp3_fused(P(X), ldx, K0, P(W0f), P(W1), P(W2), (const int *)P(labels),
                                        (const float *)P(T), ldt, t_hi, t_lo, P(D1), (float *)P(gslab), (float *)P(loss),
-                                       (unsigned int *)P(correct), Bp, n_valid, n_out, type, grid, S(stream));
+                                       (unsigned int *)P(correct), Bp, n_valid, n_out, type, grid, d1fm, S(stream));
         if (rc <= 0) check(rc ? rc : -1, "mlp3_fused");
         return rc;
     });
@@ -109,6 +109,22 @@ PYBIND11_MODULE(_native, m) {
         return v;
     });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
+    m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, uptr slab, int ldg, int N, int M, int Bt, int splits,
+                           uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout, uptr stream) {
+        check(hpnn_gemm_tn_rs(P(D), ldd, P(H), ldh, (float *)P(slab), ldg, N, M, Bt, splits, (const float *)P(rslab),
+                              rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
+              "gemm_tn_rs");
+    });
+    m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, uptr slab, int ldg, int N, int M, int Bt, int splits, uptr stream) {
+        check(hpnn_gemm_fm_direct(P(Dg), P(Hg), (float *)P(slab), ldg, N, M, Bt, splits, S(stream)), "gemm_fm_direct");
+    });
+    m.def("gemm_fm_direct_reduce", [](uptr Dg, uptr Hg, uptr slab, int ldg, int N, int M, int Bt, int splits,
+                                      uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout, uptr stream) {
+        check(hpnn_gemm_fm_direct_reduce(P(Dg), P(Hg), (float *)P(slab), ldg, N, M, Bt, splits,
+                                         (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout),
+                                         S(stream)),
+              "gemm_fm_direct_reduce");
+    });
     m.def("gemm_tn_bf16_reduce", [](uptr D, int ldd, uptr H, int ldh, uptr slab, int ldg, int N, int M, int Bt,
                                     int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,
                                     uptr stream) {

@@ -28,6 +28,12 @@ from .. import ops
 _SIDE_REDUCE = os.environ.get("HPNN_SIDE_REDUCE", "0") == "1"
 # HPNN_TAIL_REDUCE=0: separate reduce_groups launch instead of the GEMM's tail workgroups
 _TAIL_REDUCE = os.environ.get("HPNN_TAIL_REDUCE", "1") == "1"
+# HPNN_G0_FM=1, fused "x" path: first-layer gradient from fragment-major operands
+# (csrc/gpu/kernels_g0.hip).  Off by default: in the training step the fragment-major
+# copy of X is cold (the fused front has just streamed the row-major X, which the
+# LDS-staged TN GEMM then re-reads partly from the MALL): 82-83 us/step vs 77.3-77.8
+# (G0 37.8 vs 34.1 us under rocprofv3, scripts/gpu_fm_prof.sh)
+_G0_FM = os.environ.get("HPNN_G0_FM", "0") == "1"
 
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
@@ -172,10 +178,26 @@ class MLP:
         return [self.W32[l][:self.sizes[l + 1], :self.sizes[l]].double().cpu() for l in range(self.L)]
 
     def prepare_input(self, X):
-        """float/double [n, n_in] -> padded BF16 [Bp, Kp0] device tensor."""
+        """float/double [n, n_in] -> padded BF16 [Bp, Kp0] device tensor.
+
+        On the fused MNIST-shape path ("x") the returned tensor also carries, as attribute
+        `hpnn_fm`, a fragment-major copy of the same values (ops.to_fragment_major): the
+        operand layout of the first-layer gradient kernel (csrc/gpu/kernels_g0.hip), made
+        once per prepared batch so that every training step on it streams 1 KiB fragments
+        instead of transposing X through LDS (HPNN_G0_FM=1; off by default, see _G0_FM)."""
         Xd = X.to(self.device)
         out = torch.empty(ops.pad_to(X.shape[0], 128), self.Kp[0], dtype=torch.bfloat16, device=self.device)
-        return ops.pack_bf16(Xd.contiguous(), out)
+        ops.pack_bf16(Xd.contiguous(), out)
+        if self.fused_mode == "x" and _G0_FM:
+            out.hpnn_fm = ops.to_fragment_major(out)
+        return out
+
+    def _fm_input(self, X):
+        """the fragment-major copy of a prepared batch X (prepare_input), or None"""
+        Xg = getattr(X, "hpnn_fm", None)
+        if Xg is None or X.shape[0] != self.Bp or Xg.numel() != X.shape[0] * self.Kp[0]:
+            return None
+        return Xg
 
     # ------------------------------------------------------------------ phases
     def forward(self, X):
@@ -198,7 +220,11 @@ class MLP:
 
     def grad_layer(self, l, X, reduce=False):
         Hin = X if l == 0 else self.H[l - 1]
-        ops.gemm_tn(self.D[l], Hin, splits=self.S[l], out=self.slab[l])
+        Xg = self._fm_input(X) if l == 0 and self.fused_mode == "x" else None
+        if Xg is not None:  # delta1 came fragment-major from the fused front
+            ops.gemm_fm_direct(self.D[0], Xg, self.Np[0], self.Kp[0], splits=self.S[0], out=self.slab[0])
+        else:
+            ops.gemm_tn(self.D[l], Hin, splits=self.S[l], out=self.slab[l])
         if reduce:
             ops.reduce_slabs(self.slab[l], self.G[l])
 
@@ -260,11 +286,21 @@ class MLP:
                   correct=self.stats[0, 1:2])
         if self.fused_mode == "x":
             ops.mlp3_fused(X, self.Wb[0], self.W0f, self.Wb[1], self.Wb[2], self.D[0], self.midslab, self.n_out,
-                           self.type, **kw)
+                           self.type, d1_fm=self._fm_input(X) is not None, **kw)
         else:
             ops.gemm_nt(X, self.Wb[0], ops.EPI_ACT, out=self.H[0])
             ops.mlp3_mid(self.H[0], self.Wb[1], self.Wt[1], self.Wb[2], self.Wt[2], self.D[0], self.midslab,
                          self.n_out, self.type, **kw)
+
+    def _g0_reduce(self, X, groups):
+        """first-layer gradient slabs (self.slab[0]) + the first [G1|G2] reduction pass
+        (into groups) in one launch, after _fused_front on the same X"""
+        Xg = self._fm_input(X)
+        if Xg is not None:
+            ops.gemm_fm_direct_reduce(self.D[0], Xg, self.Np[0], self.Kp[0], self.S[0], self.slab[0], self.midslab,
+                                      self.mid_groups, groups)
+        else:
+            ops.gemm_tn_reduce(self.D[0], X, self.S[0], self.slab[0], self.midslab, self.mid_groups, groups)
 
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         """One minibatch fwd + bwd + update on the current stream (no host sync)."""
@@ -277,7 +313,9 @@ class MLP:
             # then every layer's update
             self._fused_front(X, labels, T, n_valid)
             groups = self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB)
-            if self.device.type == "cuda" and _SIDE_REDUCE:
+            if self._fm_input(X) is not None:
+                self._g0_reduce(X, groups)
+            elif self.device.type == "cuda" and _SIDE_REDUCE:
                 main = torch.cuda.current_stream(self.device)
                 side = self._side_stream()
                 side.wait_stream(main)

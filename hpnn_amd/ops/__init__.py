@@ -89,6 +89,63 @@ def gemm_tn_reduce(D, H, splits, out, rslab, groups, rout):
     return rout
 
 
+def gemm_tn_rs(D, H, splits=1, out=None, rslab=None, groups=1, rout=None):
+    """gemm_tn (and optionally reduce_groups(rslab, groups, rout) on tail workgroups) with
+    register-staged operands (csrc/gpu/kernels_g0.hip gemm_tn_rs_kernel)"""
+    Bt, N = D.shape
+    M = H.shape[1]
+    if out is None:
+        out = torch.empty(splits, N, M, dtype=torch.float32, device=D.device)
+    if _cpu(D):
+        gemm_tn(D, H, splits=splits, out=out)
+        if rslab is not None:
+            reduce_groups(rslab, groups, rout)
+        return out
+    native().gemm_tn_rs(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), out.data_ptr(), out.stride(1), N, M, Bt,
+                        splits, _ptr(rslab), rslab.shape[0] if rslab is not None else 0,
+                        rslab.stride(0) if rslab is not None else 0, rslab[0].numel() if rslab is not None else 0,
+                        groups, _ptr(rout), _stream())
+    return out
+
+
+def to_fragment_major(A):
+    """[Bt, M] (batch rows) -> fragment-major [Bt/32, M/16, 64, 8]: lane l = 16 g + r of
+    fragment (t, rb) holds A[t*32 + 8g + j, rb*16 + r], j < 8 (the MFMA operand layout of a
+    k = batch product, one contiguous 1 KiB per 16 x 32 fragment)"""
+    Bt, M = A.shape
+    return A.reshape(Bt // 32, 4, 8, M // 16, 16).permute(0, 3, 1, 4, 2).contiguous()
+
+
+def from_fragment_major(Ag, rows, cols):
+    """inverse of to_fragment_major"""
+    return Ag.view(rows // 32, cols // 16, 4, 16, 8).permute(0, 2, 4, 1, 3).reshape(rows, cols)
+
+
+def gemm_fm_direct(Dg, Hg, N, M, splits=1, out=None):
+    """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m] (gemm_tn) with D, H
+    given fragment-major (to_fragment_major), direct-to-register loads
+    (csrc/gpu/kernels_g0.hip)"""
+    Bt = Dg.numel() // N
+    if out is None:
+        out = torch.empty(splits, N, M, dtype=torch.float32, device=Dg.device)
+    if _cpu(Dg):
+        return gemm_tn(from_fragment_major(Dg, Bt, N), from_fragment_major(Hg, Bt, M), splits=splits, out=out)
+    native().gemm_fm_direct(Dg.data_ptr(), Hg.data_ptr(), out.data_ptr(), out.stride(1), N, M, Bt, splits, _stream())
+    return out
+
+
+def gemm_fm_direct_reduce(Dg, Hg, N, M, splits, out, rslab, groups, rout):
+    """gemm_fm_direct and reduce_groups(rslab, groups, rout) in ONE launch"""
+    if _cpu(Dg):
+        gemm_fm_direct(Dg, Hg, N, M, splits=splits, out=out)
+        return reduce_groups(rslab, groups, rout)
+    Bt = Dg.numel() // N
+    native().gemm_fm_direct_reduce(Dg.data_ptr(), Hg.data_ptr(), out.data_ptr(), out.stride(1), N, M, Bt, splits,
+                                   rslab.data_ptr(), rslab.shape[0], rslab.stride(0), rslab[0].numel(), groups,
+                                   rout.data_ptr(), _stream())
+    return rout
+
+
 def output_delta(Z, n_out, net_type, D, labels=None, T=None, t_hi=1.0, t_lo=0.0, n_valid=None, O=None,
                  loss_acc=None, correct=None):
     """Output layer: activation/softmax, loss sum, delta (bf16) and argmax hits."""
@@ -162,22 +219,26 @@ def mlp3_fused_grid(Bp, device=None):
 
 
 def mlp3_fused(X, W0, W0f, W1, W2, D1, gslab, n_out, net_type, labels=None, T=None, t_hi=1.0, t_lo=0.0,
-               n_valid=None, loss_acc=None, correct=None):
+               n_valid=None, loss_acc=None, correct=None, d1_fm=False):
     """Whole n_in-128-64-(<=32) step up to delta1 in one persistent kernel
     (csrc/gpu/kernels_mlp3.hip, mlp3_fused_kernel): X [Bp, K0] -> delta1 into D1
     [Bp, 128], per-block [G1 | G2] slabs into gslab [grid, MLP3_SLAB], loss/hits.
     W0f: fragment-major BF16 copy of W0 (frag_major); W0 (row-major) is only used by
-    the CPU emulation."""
+    the CPU emulation.  d1_fm: D1 receives delta1 fragment-major (to_fragment_major
+    layout, the operand of gemm_fm_direct) instead of row-major."""
     Bp, K0 = X.shape[0], W0.shape[1]
     n_valid = Bp if n_valid is None else int(n_valid)
     if _cpu(X):
         H1 = bipolar(X[:, :K0].float() @ W0.float().t()).bfloat16()
-        return _cpu_mlp3_mid(H1, W1, None, W2, None, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid,
-                             loss_acc, correct)
+        out = _cpu_mlp3_mid(H1, W1, None, W2, None, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid,
+                            loss_acc, correct)
+        if d1_fm:
+            D1.view(-1).copy_(to_fragment_major(D1.clone()).view(-1))
+        return out
     native().mlp3_fused(X.data_ptr(), X.stride(0), K0, W0f.data_ptr(), W1.data_ptr(), W2.data_ptr(), _ptr(labels),
                         _ptr(T), T.stride(0) if T is not None else 0, float(t_hi), float(t_lo), D1.data_ptr(),
                         gslab.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid, n_out, net_type,
-                        gslab.shape[0], _stream())
+                        gslab.shape[0], int(bool(d1_fm)), _stream())
     return D1
 
 

@@ -104,7 +104,7 @@ class DataParallel:
         m = self.m
         m._fused_front(X, labels, T, n_valid)
         groups = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
-        ops.gemm_tn_reduce(m.D[0], X, m.S[0], m.slab[0], m.midslab, m.mid_groups, groups)
+        m._g0_reduce(X, groups)
         n0 = m.G[0].numel()
         self.native.all_reduce_slabs(m.grad_flat, [(m.slab[0].view(m.S[0], n0), m.S[0], n0),
                                                    (groups, m.mid_groups, m.grad_flat.numel() - n0)])

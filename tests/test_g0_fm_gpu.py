@@ -1,0 +1,97 @@
+"""First-layer weight gradient over fragment-major operands (csrc/gpu/kernels_g0.hip) and
+the fused front's fragment-major delta1 (kernels_mlp3x.hip, d1fm).
+
+Numerics against a plain PyTorch fp32 reference of the same product; the fragment-major
+delta1 against the row-major one of the same kernel; a training step on the
+fragment-major path against the LDS-staged TN path (same math, other summation order)."""
+import pytest
+import torch
+
+from hpnn_amd import ops
+from hpnn_amd.models import MLP
+
+
+def _bf(*shape, scale=1.0):
+    return ((torch.rand(*shape, device="cuda") - 0.5) * scale).bfloat16()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Bt,N,M,S", [(65536, 128, 800, 48), (4096, 128, 800, 5), (2048, 64, 64, 7),
+                                      (1024, 32, 96, 3), (8192, 128, 832, 16)])
+def test_gemm_fm_direct_matches_fp32(gpu, Bt, N, M, S):
+    torch.manual_seed(Bt + N + M)
+    D, H = _bf(Bt, N, scale=0.25), _bf(Bt, M)
+    slab = ops.gemm_fm_direct(ops.to_fragment_major(D), ops.to_fragment_major(H), N, M, splits=S)
+    torch.cuda.synchronize()
+    ref = D.float().t() @ H.float()
+    got = slab.sum(0)
+    err = (got - ref).abs().max().item()
+    assert err < 1e-5 * Bt ** 0.5 * 4 + 1e-4, err
+    # per-split slabs: split s covers batch rows [s*U/S, (s+1)*U/S) of 32-row units
+    U = Bt // 32
+    s = S - 1
+    a, b = 32 * (s * U // S), 32 * ((s + 1) * U // S)
+    ref_s = D[a:b].float().t() @ H[a:b].float()
+    assert (slab[s] - ref_s).abs().max().item() < 1e-3
+
+
+@pytest.mark.gpu
+def test_gemm_fm_direct_with_tail_reduce(gpu):
+    torch.manual_seed(5)
+    Bt, N, M, S = 16384, 128, 800, 16
+    D, H = _bf(Bt, N, scale=0.25), _bf(Bt, M)
+    rslab = torch.randn(40, ops.MLP3_SLAB, device="cuda")
+    groups = 8
+    rout = torch.empty(groups, ops.MLP3_SLAB, device="cuda")
+    slab = torch.empty(S, N, M, device="cuda")
+    ops.gemm_fm_direct_reduce(ops.to_fragment_major(D), ops.to_fragment_major(H), N, M, S, slab, rslab, groups, rout)
+    torch.cuda.synchronize()
+    assert (slab.sum(0) - D.float().t() @ H.float()).abs().max().item() < 2e-3
+    SG = (40 + groups - 1) // groups
+    for g in range(groups):
+        ref = rslab[g * SG:min(40, (g + 1) * SG)].sum(0)
+        assert (rout[g] - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("net", ["SNN", "ANN"])
+def test_fused_front_fragment_major_delta1(gpu, net):
+    torch.manual_seed(7)
+    B = 8192
+    m = MLP([784, 128, 64, 10], net, batch=B, seed=2, fused="x")
+    X = m.prepare_input(torch.rand(B, 784))
+    X.hpnn_fm = ops.to_fragment_major(X)  # what prepare_input attaches with HPNN_G0_FM=1
+    assert m._fm_input(X) is not None
+    lab = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
+    Xrm = X.clone()  # no fragment-major copy attached: row-major delta1
+    assert m._fm_input(Xrm) is None
+    m._fused_front(Xrm, lab, None, B - 3)
+    d_rm = m.D[0].clone()
+    s_rm = m.midslab.clone()
+    m._fused_front(X, lab, None, B - 3)
+    d_fm = ops.from_fragment_major(m.D[0].view(-1), B, 128)
+    torch.cuda.synchronize()
+    diff = (d_fm.float() - d_rm.float()).abs()
+    # same products, operands swapped in the MFMA: at most one bf16 rounding step apart
+    assert diff.max().item() <= 2 ** -7 * d_rm.float().abs().max().item() + 1e-6
+    assert (diff > 0).float().mean().item() < 0.01
+    assert torch.equal(m.midslab, s_rm)
+
+
+@pytest.mark.gpu
+def test_train_step_fragment_major_matches_tn(gpu):
+    torch.manual_seed(9)
+    B = 16384
+    ms = [MLP([784, 128, 64, 10], "SNN", batch=B, seed=3, momentum=True, fused="x") for _ in range(2)]
+    xs = [torch.rand(B, 784) for _ in range(3)]
+    labs = [torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda") for _ in range(3)]
+    for i, m in enumerate(ms):
+        for x, lab in zip(xs, labs):
+            X = m.prepare_input(x)
+            if i == 0:
+                X.hpnn_fm = ops.to_fragment_major(X)  # fragment-major G0 path (HPNN_G0_FM=1)
+            m.train_step(X, labels=lab, lr=0.05, alpha=0.2)
+    torch.cuda.synchronize()
+    for l in range(3):
+        e = (ms[0].W32[l] - ms[1].W32[l]).abs().max().item()
+        assert e < 1e-5, (l, e)

@@ -2,6 +2,8 @@
 import pytest
 import torch
 
+from hpnn_amd import ops
+
 from hpnn_amd.models import MLP
 from hpnn_amd.models import reference as ref
 
@@ -79,7 +81,10 @@ def test_fused_matches_layerwise(gpu, net_type, B, n_valid, mode, n_in):
     lb, cb = ml.read_stats()
     assert la == pytest.approx(lb, rel=2e-2)
     assert abs(ca - cb) <= max(2, 0.01 * n_valid)
-    assert torch.equal(mf.D[0][n_valid:], torch.zeros_like(mf.D[0][n_valid:]))
+    D1 = mf.D[0]
+    if mf._fm_input(Xd) is not None:  # delta1 fragment-major (first-layer gradient kernel operand)
+        D1 = ops.from_fragment_major(D1.view(-1), mf.Bp, 128)
+    assert torch.equal(D1[n_valid:], torch.zeros_like(D1[n_valid:]))
 
 
 @pytest.mark.parametrize("net_type", ["SNN", "ANN"])
@@ -120,7 +125,10 @@ def test_fused_x_kernel_vs_emulation(gpu):
     st = torch.zeros(64, 16)
     ops.mlp3_fused(X.cpu(), m.Wb[0].cpu(), None, m.Wb[1].cpu(), m.Wb[2].cpu(), D1, slab, 10, ops.TYPE_SNN,
                    labels=lab.cpu(), n_valid=B - 5, loss_acc=st[0, 0:1], correct=st[0, 1:2])
-    d = (m.D[0].cpu().float() - D1.float()).abs().max().item()
+    got_d1 = m.D[0].cpu()
+    if m._fm_input(X) is not None:  # delta1 was written fragment-major for the G0 kernel
+        got_d1 = ops.from_fragment_major(got_d1.view(-1), B, 128)
+    d = (got_d1.float() - D1.float()).abs().max().item()
     assert d < 2e-2 * (D1.float().abs().max().item() + 1e-6), d
     got = m.midslab.sum(0).cpu()
     ref_ = slab[0]
