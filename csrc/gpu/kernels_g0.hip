@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void gemm_tn_rs_kernel(const __bf16 *__restric
 #pragma unroll
             for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], fd[j], acc[i][j], 0, 0, 0);
     };
-    static_assert(P == 3, "the loop below is unrolled by lcm(P, 3) = 3");
+    static_assert(P % 3 == 0, "the loop below is unrolled by P (slots) = a multiple of 3 (LDS buffers)");
     if (KT > 0) {
 #pragma unroll
         for (int sl = 0; sl < P; sl++) load(sl, sl);
@@ -246,18 +246,19 @@ __global__ __launch_bounds__(256) void gemm_tn_rs_kernel(const __bf16 *__restric
         store(0, 0);
         __builtin_amdgcn_sched_barrier(0);
         load(0, P);
-        for (int t = 0; t < KT; t += 3) {
+        for (int t = 0; t < KT; t += P) {
 #pragma unroll
-            for (int u = 0; u < 3; u++) {
-                /* step t+u: stage step t+u+1 (slot / buffer (u+1) % 3), refill that slot with
-                 * step t+u+1+P, one barrier, MFMAs on buffer u */
+            for (int u = 0; u < P; u++) {
+                /* step t+u: stage step t+u+1 (register slot (u+1) % P -> LDS buffer
+                 * (u+1) % 3), refill that slot with step t+u+1+P, one barrier, MFMAs on
+                 * buffer u % 3 */
                 __builtin_amdgcn_sched_barrier(0);
-                store((u + 1) % 3, (u + 1) % 3);
+                store((u + 1) % P, (u + 1) % 3);
                 __builtin_amdgcn_sched_barrier(0);
-                load((u + 1) % 3, t + u + 1 + P);
+                load((u + 1) % P, t + u + 1 + P);
                 __builtin_amdgcn_sched_barrier(0);
                 __syncthreads();
-                if (t + u < KT) compute(u);
+                if (t + u < KT) compute(u % 3);
             }
         }
     }
@@ -270,13 +271,13 @@ __global__ __launch_bounds__(256) void gemm_tn_rs_kernel(const __bf16 *__restric
             *(f32x4 *)(out + (size_t)(n0 + wn * WTN + j * 16 + r16) * ldg + m0 + wm * WTM + i * 16 + 4 * q) = acc[i][j];
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int P = 3>
 int launch_rs(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
               hipStream_t s, const TnTail &tail) {
     if (M % TM || N % TN || Bt % 64 || splits > Bt / 64) return -2;
     const int tiles_n = N / TN, tiles = (M / TM) * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-    hipLaunchKernelGGL((gemm_tn_rs_kernel<TM, TN, 3>), dim3(tiles * splits + tail.blocks), dim3(256), 0, s,
+    hipLaunchKernelGGL((gemm_tn_rs_kernel<TM, TN, P>), dim3(tiles * splits + tail.blocks), dim3(256), 0, s,
                        (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, Bt / 64, splits, tiles_n, tiles,
                        xcd_map, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -327,7 +328,12 @@ extern "C" int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, f
         const int bx = (int)((n4 + 255) / 256);
         t = {rslab, rout, rstride, n4, rn, rS, (rS + rgroups - 1) / rgroups, bx, bx * rgroups};
     }
-    if (M % 160 == 0 && N % 128 == 0) return launch_rs<160, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    static const int pd = [] { const char *e = getenv("HPNN_RS_P"); return e ? atoi(e) : 3; }();
+    if (M % 160 == 0 && N % 128 == 0) {
+        if (pd == 6) return launch_rs<160, 128, 6>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+        if (pd == 9) return launch_rs<160, 128, 9>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+        return launch_rs<160, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    }
     if (M % 128 == 0 && N % 128 == 0) return launch_rs<128, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     return -2;
 }

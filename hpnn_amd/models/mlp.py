@@ -34,6 +34,10 @@ _TAIL_REDUCE = os.environ.get("HPNN_TAIL_REDUCE", "1") == "1"
 # LDS-staged TN GEMM then re-reads partly from the MALL): 82-83 us/step vs 77.3-77.8
 # (G0 37.8 vs 34.1 us under rocprofv3, scripts/gpu_fm_prof.sh)
 _G0_FM = os.environ.get("HPNN_G0_FM", "0") == "1"
+# HPNN_G0_RS=1: first-layer gradient with the register-staged TN kernel (kernels_g0.hip):
+# 75.46-76.57 us/step vs 75.73-77.32 with the LDS-DMA TN kernel (scripts/gpu_ab_g0.sh),
+# within noise of each other
+_G0_RS = os.environ.get("HPNN_G0_RS", "0") == "1"
 
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
@@ -299,6 +303,9 @@ class MLP:
         if Xg is not None:
             ops.gemm_fm_direct_reduce(self.D[0], Xg, self.Np[0], self.Kp[0], self.S[0], self.slab[0], self.midslab,
                                       self.mid_groups, groups)
+        elif _G0_RS and (self.Kp[0] % 128 == 0 or self.Kp[0] % 160 == 0):
+            ops.gemm_tn_rs(self.D[0], X, self.S[0], self.slab[0], rslab=self.midslab, groups=self.mid_groups,
+                           rout=groups)
         else:
             ops.gemm_tn_reduce(self.D[0], X, self.S[0], self.slab[0], self.midslab, self.mid_groups, groups)
 
@@ -313,7 +320,7 @@ class MLP:
             # then every layer's update
             self._fused_front(X, labels, T, n_valid)
             groups = self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB)
-            if self._fm_input(X) is not None:
+            if self._fm_input(X) is not None or _G0_RS:
                 self._g0_reduce(X, groups)
             elif self.device.type == "cuda" and _SIDE_REDUCE:
                 main = torch.cuda.current_stream(self.device)

@@ -95,3 +95,19 @@ def test_train_step_fragment_major_matches_tn(gpu):
     for l in range(3):
         e = (ms[0].W32[l] - ms[1].W32[l]).abs().max().item()
         assert e < 1e-5, (l, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Bt,N,M,S", [(65536, 128, 800, 48), (8192, 128, 512, 8), (4096, 128, 256, 3)])
+def test_gemm_tn_register_staged_matches_fp32(gpu, Bt, N, M, S):
+    torch.manual_seed(Bt + M)
+    D, H = _bf(Bt, N, scale=0.25), _bf(Bt, M)
+    rslab = torch.randn(20, ops.MLP3_SLAB, device="cuda")
+    rout = torch.empty(4, ops.MLP3_SLAB, device="cuda")
+    slab = ops.gemm_tn_rs(D, H, splits=S, rslab=rslab, groups=4, rout=rout)
+    ref_slab = ops.gemm_tn(D, H, splits=S)
+    torch.cuda.synchronize()
+    assert (slab.sum(0) - D.float().t() @ H.float()).abs().max().item() < 1e-5 * Bt ** 0.5 * 4 + 1e-4
+    assert (slab - ref_slab).abs().max().item() < 1e-3  # same split boundaries as the TN kernel
+    for g in range(4):
+        assert (rout[g] - rslab[5 * g:5 * g + 5].sum(0)).abs().max().item() < 1e-4
