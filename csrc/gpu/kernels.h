@@ -60,10 +60,11 @@ int hpnn_gemm_tn_bf16_reduce(const void *D, int ldd, const void *H, int ldh, flo
 
 /* hpnn_gemm_tn_bf16(_reduce) with register-staged operands (kernels_g0.hip): coalesced
  * vector loads P steps ahead -> T32 LDS image -> transposed MFMA reads.  M % 160 or 128,
- * N % 128, Bt % 64.  rslab == NULL: no tail reduction. */
-int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
-                    int splits, const float *rslab, int rS, long rstride, long rn, int rgroups, float *rout,
-                    hipStream_t stream);
+ * N % 128, Bt % 64.  h_u8: H is uint8 [Bt x ldh] (ldh % 16 == 0) used as bf16(h * hscale)
+ * (exact for pixel values 0..255 with hscale 1).  rslab == NULL: no tail reduction. */
+int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, int h_u8, float hscale, float *slab, int ldg,
+                    int N, int M, int Bt, int splits, const float *rslab, int rS, long rstride, long rn, int rgroups,
+                    float *rout, hipStream_t stream);
 /* weight gradient of hpnn_gemm_tn_bf16 over FRAGMENT-MAJOR operands (kernels_g0.hip):
  * Dg [Bt/32][N/16][64][8], Hg [Bt/32][M/16][64][8], lane l = 16 g + r of fragment (t, cb)
  * holding A[32 t + 8 g + j][16 cb + r] (j < 8); slab[s][n][m] as hpnn_gemm_tn_bf16.

@@ -40,10 +40,12 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8 &a, const bf16x8 &b, const f3
 
 /* byte offset of element (r, col) in a T32 image with R rows */
 __device__ __forceinline__ int t32_g(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
-template <int R>
+/* PAD: bytes between consecutive 32-column sub-tiles beyond R * 64 (a padded image lets
+ * 16 lanes writing one row across 4 sub-tiles hit 4 different bank groups) */
+template <int R, int PAD = 0>
 __device__ __forceinline__ int t32(int r, int col) {
     const int sub = col >> 5, c = col & 31;
-    return sub * (R * 64) + r * 64 + ((((c >> 3) ^ t32_g(r)) & 3) << 4) + (c & 7) * 2;
+    return sub * (R * 64 + PAD) + r * 64 + ((((c >> 3) ^ t32_g(r)) & 3) << 4) + (c & 7) * 2;
 }
 
 /* row-read fragment: 8 consecutive columns [col0 + 8(l>>4), +8) of row r0 + (l&15) */
@@ -53,12 +55,12 @@ __device__ __forceinline__ bf16x8 frag_row(const char *img, int r0, int col0, in
 }
 
 /* transposed fragment: column c0 + (l&15), rows kbase + 8(l>>4) + 0..7 */
-template <int R>
+template <int R, int PAD = 0>
 __device__ __forceinline__ bf16x8 frag_tr(const char *img, int kbase, int c0, int lane) {
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int row = kbase + 8 * g + q;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R>(row, c0 + 4 * p)));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R>(row + 4, c0 + 4 * p)));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R, PAD>(row, c0 + 4 * p)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + t32<R, PAD>(row + 4, c0 + 4 * p)));
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
 }

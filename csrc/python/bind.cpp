@@ -109,10 +109,11 @@ PYBIND11_MODULE(_native, m) {
         return v;
     });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
-    m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, uptr slab, int ldg, int N, int M, int Bt, int splits,
-                           uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout, uptr stream) {
-        check(hpnn_gemm_tn_rs(P(D), ldd, P(H), ldh, (float *)P(slab), ldg, N, M, Bt, splits, (const float *)P(rslab),
-                              rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
+    m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, int h_u8, float hscale, uptr slab, int ldg, int N, int M,
+                           int Bt, int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,
+                           uptr stream) {
+        check(hpnn_gemm_tn_rs(P(D), ldd, P(H), ldh, h_u8, hscale, (float *)P(slab), ldg, N, M, Bt, splits,
+                              (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
               "gemm_tn_rs");
     });
     m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, uptr slab, int ldg, int N, int M, int Bt, int splits, uptr stream) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""MNIST first-layer weight gradient (800 x 128 over 65536 rows) with the three TN kernels:
-LDS-DMA pipe (ops.gemm_tn), register-staged (ops.gemm_tn_rs), fragment-major direct loads
-(ops.gemm_fm_direct).  "hot": the same operands every call (they stay in the 256 MB MALL);
+"""MNIST first-layer weight gradient (800 x 128 over 65536 rows) with the TN kernels:
+LDS-DMA pipe (ops.gemm_tn), register-staged (ops.gemm_tn_rs; rs-u8: the input as 8-bit
+pixels, converted while staging), fragment-major direct loads (ops.gemm_fm_direct).  "hot": the same operands every call (they stay in the 256 MB MALL);
 "cold": cycling over 4 operand sets (420 MB, from HBM).  usage: g0_direct.py [splits]"""
 import os
 import sys
@@ -27,7 +27,8 @@ def t(fn, n, reps=48):
 B, M, N = 65536, 800, 128
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 48
 dev = torch.device("cuda")
-Xs = [torch.rand(B, M, device=dev).bfloat16() for _ in range(4)]
+Xu = [torch.randint(0, 256, (B, M), device=dev, dtype=torch.uint8) for _ in range(4)]  # pixel values
+Xs = [x.bfloat16() for x in Xu]  # exact
 Ds = [((torch.rand(B, N, device=dev) - 0.5) / 8).bfloat16() for _ in range(4)]
 Xg = [ops.to_fragment_major(x) for x in Xs]
 Dg = [ops.to_fragment_major(d) for d in Ds]
@@ -35,7 +36,8 @@ out = torch.empty(S, N, M, device=dev)
 ref = Ds[0].float().t() @ Xs[0].float()
 for name, fn in [("tn", lambda i: ops.gemm_tn(Ds[i], Xs[i], splits=S, out=out)),
                  ("rs", lambda i: ops.gemm_tn_rs(Ds[i], Xs[i], splits=S, out=out)),
-                 ("fm", lambda i: ops.gemm_fm_direct(Dg[i], Xg[i], N, M, splits=S, out=out))]:
+                 ("fm", lambda i: ops.gemm_fm_direct(Dg[i], Xg[i], N, M, splits=S, out=out)),
+                 ("rs-u8", lambda i: ops.gemm_tn_rs(Ds[i], Xu[i], splits=S, out=out))]:
     hot, cold = t(fn, 1), t(fn, 4)
     fn(0)
     err = (out.sum(0) - ref).abs().max().item()
