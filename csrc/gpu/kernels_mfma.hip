@@ -342,7 +342,10 @@ int launch_nt_bn(const void *A, int lda, const void *B, int ldb, void *C, int ld
 /* large GEMMs: 256x256 tiles, 8 waves (2 x 4, each 128x64), 2-stage ring of 64 KiB
  * stages, one workgroup per CU (HPNN_NT_BIG=0 disables).  8192x4096x4096: 974 / 1004
  * TFLOP/s (forward / backward epilogue) vs 870 / 918 with the 128x128 4-wave tile;
- * measured and rejected: BK=32 with 4 stages (913), s_setprio around the MFMA block (910) */
+ * measured and rejected: BK=32 with 4 stages (913), s_setprio around the MFMA block (910),
+ * register-staged operands instead of LDS-DMA, same tiling (916 / 961 vs 926 / 1001 on
+ * the same box), 4 waves with 128x128 wave tiles and 256 AGPR accumulators (693 / 570:
+ * one wave per SIMD leaves the LDS reads and the MFMAs of a k-step serialized) */
 template <int EPI, bool CF32>
 int launch_nt_big(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
                   int N, int K, hipStream_t s) {
