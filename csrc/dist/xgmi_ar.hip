@@ -170,12 +170,62 @@ __device__ __forceinline__ float4 sum_peers(const XarPeers &P, long half4, int w
     return s;
 }
 
+/* optimizer step fused after the exchange (hpnn_xar_all_reduce_slabs_update_f32) */
+struct XarUpd {
+    float *W32[HPNN_XAR_MAX_LAYERS], *V32[HPNN_XAR_MAX_LAYERS];
+    __bf16 *Wb[HPNN_XAR_MAX_LAYERS], *Wt[HPNN_XAR_MAX_LAYERS], *Wf[HPNN_XAR_MAX_LAYERS];
+    int N[HPNN_XAR_MAX_LAYERS], K[HPNN_XAR_MAX_LAYERS];
+    long end4[HPNN_XAR_MAX_LAYERS]; /* exclusive prefix ends in float4 */
+    int nl;
+    float lr, alpha, scale;
+    int momentum;
+};
+
+/* float4 i of the reduced gradient = 4 consecutive k of one row n of one layer: the
+ * step of sgd_tile (kernels_misc.hip) on those 4 weights */
+__device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g) {
+    int l = 0;
+    while (l + 1 < u.nl && i >= u.end4[l]) l++;
+    const long e = (i - (l ? u.end4[l - 1] : 0)) * 4;
+    const int K = u.K[l], N = u.N[l];
+    const int n = (int)(e / K), k = (int)(e % K);
+    float4 w = *(const float4 *)(u.W32[l] + e);
+    float gv[4] = {g.x, g.y, g.z, g.w}, wv[4] = {w.x, w.y, w.z, w.w};
+    if (u.momentum) {
+        float4 v = *(const float4 *)(u.V32[l] + e);
+        float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            vv[r] += u.lr * (gv[r] * u.scale);
+            wv[r] += vv[r];
+            vv[r] *= u.alpha;
+        }
+        *(float4 *)(u.V32[l] + e) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) wv[r] += u.lr * (gv[r] * u.scale);
+    }
+    *(float4 *)(u.W32[l] + e) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 wb;
+#pragma unroll
+    for (int r = 0; r < 4; r++) wb[r] = (__bf16)wv[r];
+    *(bf16x4 *)(u.Wb[l] + e) = wb;
+    if (u.Wf[l]) {
+        const size_t fo = (((size_t)(n >> 4) * (K / 32) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+        *(bf16x4 *)(u.Wf[l] + fo) = wb;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) u.Wt[l][(size_t)(k + r) * N + n] = wb[r];
+}
+
 /* TWO = false: one-shot, element slice b of the whole buffer per workgroup.
  * TWO = true: shard s = [s * sh, min((s + 1) * sh, n4)), workgroup b owns
  * [s * sh + b * per, ...+ per) of every shard */
-template <bool TWO>
+template <bool TWO, bool UPD>
 __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
-                                                  long n4, long half_stride4, unsigned long long timeout, int light) {
+                                                  long n4, long half_stride4, unsigned long long timeout, int light,
+                                                  XarUpd upd) {
     const int b = blockIdx.x;
     Signal *me = P.sig[rank];
     __shared__ unsigned int s_ep;
@@ -193,7 +243,11 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
         const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
         for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
         xbarrier(P, rank, world, b, e, 0, timeout, light);
-        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = sum_peers(P, half4, world, i);
+        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            const float4 v = sum_peers(P, half4, world, i);
+            out[i] = v;
+            if constexpr (UPD) xar_update4(upd, i, v);
+        }
     } else {
         const long sh = (n4 + world - 1) / world;
         const long per = (sh + gridDim.x - 1) / gridDim.x;
@@ -213,13 +267,18 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
             const float4 v = sum_peers(P, half4, world, i);
             mine[i] = v;
             out[i] = v;
+            if constexpr (UPD) xar_update4(upd, i, v);
         }
         xbarrier(P, rank, world, b, e, 1, timeout, light);
         for (int q = 1; q < world; q++) { /* start after this rank: spread the link load */
             const int s = (rank + q) % world;
             range(s, lo, hi);
             const float4 *src = P.buf[s] + half4;
-            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = src[i];
+            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+                const float4 v = src[i];
+                out[i] = v;
+                if constexpr (UPD) xar_update4(upd, i, v);
+            }
         }
     }
 }
@@ -308,7 +367,8 @@ extern "C" int hpnn_xar_open(hpnn_xar *c, const void *all) {
 
 extern "C" size_t hpnn_xar_max_bytes(const hpnn_xar *c) { return c ? c->max_bytes : 0; }
 
-static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipStream_t stream) {
+static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipStream_t stream,
+                      const XarUpd *upd = nullptr) {
     if (!c || count <= 0 || (count & 3) || (size_t)count * 4 > c->max_bytes) return -1;
     if ((uintptr_t)out & 15) return -1;
     for (int p = 0; p < c->world; p++)
@@ -327,12 +387,19 @@ static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipS
      * MNIST front) still has to run before that peer reaches its all-reduce */
     const long blocks = c->blocks;
     const long half4 = (long)(c->max_bytes / 16);
-    if (two)
-        hipLaunchKernelGGL(xar_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank, c->world,
-                           in, (float4 *)out, n4, half4, c->timeout, c->light);
-    else
-        hipLaunchKernelGGL(xar_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,
-                           c->world, in, (float4 *)out, n4, half4, c->timeout, c->light);
+    XarUpd none = {};
+    const XarUpd &u = upd ? *upd : none;
+#define HPNN_XARL(T_, U_)                                                                                          \
+    hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,       \
+                       c->world, in, (float4 *)out, n4, half4, c->timeout, c->light, u)
+    if (two) {
+        if (upd) HPNN_XARL(true, true);
+        else HPNN_XARL(true, false);
+    } else {
+        if (upd) HPNN_XARL(false, true);
+        else HPNN_XARL(false, false);
+    }
+#undef HPNN_XARL
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -364,6 +431,48 @@ extern "C" int hpnn_xar_all_reduce_slabs_f32(hpnn_xar *c, const hpnn_xar_seg *se
     }
     x.nseg = nseg;
     return xar_launch(c, x, out, tot, stream);
+}
+
+extern "C" int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
+                                                    const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha,
+                                                    float scale, int momentum, hipStream_t stream) {
+    if (!segs || nseg < 1 || nseg > HPNN_XAR_MAX_SEGS || !layers || nl < 1 || nl > HPNN_XAR_MAX_LAYERS) return -1;
+    XarIn x = {};
+    long tot = 0;
+    for (int j = 0; j < nseg; j++) {
+        const hpnn_xar_seg &g = segs[j];
+        if (!g.src || g.S < 1 || g.count <= 0 || (g.count & 3) || (g.stride & 3) || ((uintptr_t)g.src & 15))
+            return -1;
+        x.src[j] = (const float4 *)g.src;
+        x.stride4[j] = g.stride / 4;
+        x.S[j] = g.S;
+        tot += g.count;
+        x.end4[j] = tot / 4;
+    }
+    x.nseg = nseg;
+    XarUpd u = {};
+    long lt = 0;
+    for (int l = 0; l < nl; l++) {
+        const hpnn_xar_upd_layer &L = layers[l];
+        if (!L.W32 || !L.Wbf || !L.Wt || (momentum && !L.V32) || L.N <= 0 || L.K <= 0 || L.K % 4) return -1;
+        if (L.Wf && (L.N % 16 || L.K % 32)) return -1;
+        u.W32[l] = L.W32;
+        u.V32[l] = L.V32;
+        u.Wb[l] = (__bf16 *)L.Wbf;
+        u.Wt[l] = (__bf16 *)L.Wt;
+        u.Wf[l] = (__bf16 *)L.Wf;
+        u.N[l] = L.N;
+        u.K[l] = L.K;
+        lt += (long)L.N * L.K;
+        u.end4[l] = lt / 4;
+    }
+    if (lt != tot) return -2; /* the layers must tile the reduced vector exactly */
+    u.nl = nl;
+    u.lr = lr;
+    u.alpha = alpha;
+    u.scale = scale;
+    u.momentum = momentum;
+    return xar_launch(c, x, out, tot, stream, &u);
 }
 
 extern "C" int hpnn_xar_status(hpnn_xar *c) {

@@ -240,6 +240,22 @@ PYBIND11_MODULE(_native, m) {
         check(hpnn_xar_all_reduce_slabs_f32((hpnn_xar *)c, v.data(), (int)v.size(), (float *)P(out), S(stream)),
               "xar_all_reduce_slabs_f32");
     });
+    m.def("xar_all_reduce_slabs_update_f32",
+          [](uptr c, std::vector<std::tuple<uptr, long, int, long>> segs, uptr out,
+             std::vector<std::tuple<uptr, uptr, uptr, uptr, uptr, int, int>> layers, float lr, float alpha, float scale,
+             int momentum, uptr stream) {
+              std::vector<hpnn_xar_seg> v;
+              for (auto &t : segs)
+                  v.push_back({(const float *)P(std::get<0>(t)), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+              std::vector<hpnn_xar_upd_layer> L;
+              for (auto &t : layers)
+                  L.push_back({(float *)P(std::get<0>(t)), (float *)P(std::get<1>(t)), P(std::get<2>(t)),
+                               P(std::get<3>(t)), P(std::get<4>(t)), std::get<5>(t), std::get<6>(t)});
+              check(hpnn_xar_all_reduce_slabs_update_f32((hpnn_xar *)c, v.data(), (int)v.size(), (float *)P(out),
+                                                         L.data(), (int)L.size(), lr, alpha, scale, momentum,
+                                                         S(stream)),
+                    "xar_all_reduce_slabs_update_f32");
+          });
     m.def("xar_status", [](uptr c) { return hpnn_xar_status((hpnn_xar *)c); });
     m.def("xar_destroy", [](uptr c) { hpnn_xar_destroy((hpnn_xar *)c); });
     m.def("comm_set_xar", [](uptr c, uptr x, size_t max_bytes) {

@@ -157,6 +157,18 @@ class NativeComm:
                                           out.data_ptr(), _stream())
         return out
 
+    def all_reduce_slabs_update(self, out, segs, layers, lr, alpha, scale, momentum):
+        """all_reduce_slabs followed, in the same launch, by every layer's optimizer step
+        on the reduced gradient (include/libhpnn/xar.h hpnn_xar_all_reduce_slabs_update_f32);
+        layers: [(W32, V32 or None, Wbf, Wt, Wf or None)] tiling `out` in order"""
+        def p(t):
+            return 0 if t is None else t.data_ptr()
+        native().xar_all_reduce_slabs_update_f32(
+            self.xar, [(t.data_ptr(), t.stride(0), S, n) for t, S, n in segs], out.data_ptr(),
+            [(p(w), p(v), p(wb), p(wt), p(wf), w.shape[0], w.shape[1]) for w, v, wb, wt, wf in layers],
+            float(lr), float(alpha), float(scale), int(bool(momentum)), _stream())
+        return out
+
     # -- failure detection ----------------------------------------------------------
     def check(self):
         """raise if the communicator saw an asynchronous error (peer died, link down) or an

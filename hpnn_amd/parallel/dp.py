@@ -13,10 +13,15 @@ lower layers.  The optimizer kernels then wait (stream-side, no host sync) for t
 bucket.  Small consecutive layers are merged into one bucket (`bucket_bytes`) because a
 37 KB all-reduce is latency-bound on xGMI.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from .. import ops
+
+# HPNN_XAR_UPD=0: separate optimizer launch after the xGMI all-reduce (fused MNIST path)
+_XAR_UPD = os.environ.get("HPNN_XAR_UPD", "1") == "1"
 
 
 class DataParallel:
@@ -97,18 +102,26 @@ class DataParallel:
         return m.grad_flat[start // 4:end // 4]
 
     def _fused_xgmi_step(self, X, labels, T, n_valid, lr, alpha):
-        """MNIST fused path on the xGMI all-reduce: 4 launches per step -- fused front, G0
+        """MNIST fused path on the xGMI all-reduce: 3 launches per step -- fused front, G0
         GEMM (+ first [G1|G2] reduction pass on its tail workgroups), ONE all-reduce whose
-        copy-in phase also sums the local split-K slabs of G0 and the [G1|G2] groups, the
-        update of every layer from the reduced gradients"""
+        copy-in phase also sums the local split-K slabs of G0 and the [G1|G2] groups and
+        which then applies every layer's update to the reduced gradients"""
         m = self.m
         m._fused_front(X, labels, T, n_valid)
         groups = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
         m._g0_reduce(X, groups)
         n0 = m.G[0].numel()
-        self.native.all_reduce_slabs(m.grad_flat, [(m.slab[0].view(m.S[0], n0), m.S[0], n0),
-                                                   (groups, m.mid_groups, m.grad_flat.numel() - n0)])
-        m.update_all(lr, alpha, 1.0 / (n_valid * self.world), m.G)
+        segs = [(m.slab[0].view(m.S[0], n0), m.S[0], n0), (groups, m.mid_groups, m.grad_flat.numel() - n0)]
+        scale = 1.0 / (n_valid * self.world)
+        if _XAR_UPD:
+            # exchange + every layer's optimizer step in ONE launch (the update kernel and
+            # its launch gap leave the data-parallel step)
+            self.native.all_reduce_slabs_update(
+                m.grad_flat, segs, [(m.W32[l], m.V32[l], m.Wb[l], m.Wt[l], m.W0f if l == 0 else None)
+                                    for l in range(m.L)], lr, alpha, scale, m.momentum)
+        else:
+            self.native.all_reduce_slabs(m.grad_flat, segs)
+            m.update_all(lr, alpha, scale, m.G)
 
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         m = self.m

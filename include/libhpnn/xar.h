@@ -60,6 +60,24 @@ typedef struct {
     long count;  /* floats */
 } hpnn_xar_seg;
 int hpnn_xar_all_reduce_slabs_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out, hipStream_t stream);
+/* the same all-reduce followed, in the same kernel, by every layer's optimizer step on the
+ * reduced gradient (the math of hpnn_sgd_update_multi: g * scale, BP or BPM with momentum
+ * alpha, FP32 master W32 / V32, BF16 copies Wbf [N x K], Wt [K x N] and, optionally,
+ * the fragment-major Wf).  Layer l covers floats [sum_{j<l} N_j K_j, + N_l K_l) of the
+ * output; the layers must cover it exactly.  Saves the separate update launch of a
+ * data-parallel step; every rank applies the same bits. */
+#define HPNN_XAR_MAX_LAYERS 8
+typedef struct {
+    float *W32;
+    float *V32; /* NULL without momentum */
+    void *Wbf;
+    void *Wt;
+    void *Wf; /* may be NULL */
+    int N, K;
+} hpnn_xar_upd_layer;
+int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
+                                         const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha, float scale,
+                                         int momentum, hipStream_t stream);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
 int hpnn_xar_status(hpnn_xar *c);
 void hpnn_xar_destroy(hpnn_xar *c);
