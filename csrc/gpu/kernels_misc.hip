@@ -233,6 +233,132 @@ __global__ __launch_bounds__(256) void output_delta_reg_kernel(const float *__re
     block_reduce_store(my_loss, my_hit, loss_acc, correct);
 }
 
+/* wide outputs up to 256 classes (RRUFF: 230), FOUR rows per wave: 16 lanes per row,
+ * lane i of a row group owning columns [16 i, 16 i + 16) (four float4 loads, two 16-byte
+ * delta stores).  The five row reductions (max, sum, loss, two argmax) run over 16 lanes
+ * (4 shuffle steps instead of 6) and for 4 rows at once; the one-row-per-wave kernel above
+ * spent ~17 us on 16384 x 230 in these dependent reductions.  Needs ldz, ldd (and ldo)
+ * multiples of 16, ldd <= 256. */
+__device__ __forceinline__ float g16_max(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 16));
+    return v;
+}
+__device__ __forceinline__ float g16_sum(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+    return v;
+}
+__device__ __forceinline__ void g16_argmax(float &v, int &i) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 16);
+        const int oi = __shfl_xor(i, o, 16);
+        if (oi >= 0 && (i < 0 || ov > v || (ov == v && oi < i))) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void output_delta_q_kernel(const float *__restrict__ Z, int ldz,
+                                                             const float *__restrict__ T, int ldt,
+                                                             const int *__restrict__ labels, float t_hi, float t_lo,
+                                                             __bf16 *__restrict__ D, int ldd, float *__restrict__ O,
+                                                             int ldo, float *__restrict__ loss_acc,
+                                                             unsigned int *__restrict__ correct, int B, int n_valid,
+                                                             int n_out, int type) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gi = lane & 15, c0 = 16 * gi;
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    for (int row0 = (blockIdx.x * 4 + wave) * 4; row0 < B; row0 += gridDim.x * 16) {
+        const int row = row0 + (lane >> 4);
+        const bool in = row < B, valid = row < n_valid;
+        const int lab = (labels && valid) ? labels[row] : -1;
+        float z[16];
+        if (in && c0 < ldz) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float4 v = *(const float4 *)(Z + (size_t)row * ldz + c0 + 4 * j);
+                z[4 * j] = v.x;
+                z[4 * j + 1] = v.y;
+                z[4 * j + 2] = v.z;
+                z[4 * j + 3] = v.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (!in || c0 + j >= n_out) z[j] = -INFINITY;
+        float inv = 0.f, zmax = 0.f;
+        if (type == 2) {
+            zmax = z[0];
+#pragma unroll
+            for (int j = 1; j < 16; j++) zmax = fmaxf(zmax, z[j]);
+            zmax = g16_max(zmax);
+            float denom = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; j++) { /* z[j] <- e^{z - max}: computed once */
+                z[j] = c0 + j < n_out ? __expf(z[j] - zmax) : 0.f;
+                denom += z[j];
+            }
+            denom = g16_sum(denom);
+            /* reference: e^{z-1} / (TINY + sum e^{z-1}); shifted by m=zmax */
+            denom += __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
+            inv = 1.0f / denom;
+        }
+        float bo = -INFINITY, bt = -INFINITY, l = 0.f;
+        int io = -1, it = -1;
+        typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+        bf16x8 dv[2];
+        float ov[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int c = c0 + j;
+            float d = 0.f, o = 0.f;
+            if (in && c < n_out) {
+                if (type == 2) o = z[j] * inv;
+                else if (type == 0) o = 2.0f / (1.0f + __expf(-z[j])) - 1.0f;
+                else o = z[j];
+                if (valid) {
+                    const float t = labels ? (c == lab ? t_hi : t_lo) : T[(size_t)row * ldt + c];
+                    if (type == 2) {
+                        if (t != 0.f && o > 0.f) l += t * logf(o + TINY); /* one-hot: one log per row */
+                        d = t - o;
+                    } else if (type == 0) {
+                        l += (t - o) * (t - o);
+                        d = (t - o) * (-0.5f * (o * o - 1.0f));
+                    } else {
+                        l += (t - o) * (t - o);
+                        d = t - o;
+                    }
+                    if (o > bo) { bo = o; io = c; }
+                    if (t > bt) { bt = t; it = c; }
+                }
+            }
+            ov[j] = o;
+            dv[j >> 3][j & 7] = (__bf16)d;
+        }
+        if (in && c0 < ldd) {
+            *(bf16x8 *)(D + (size_t)row * ldd + c0) = dv[0];
+            *(bf16x8 *)(D + (size_t)row * ldd + c0 + 8) = dv[1];
+        }
+        if (O && in && c0 < ldo) {
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if (c0 + j < n_out) O[(size_t)row * ldo + c0 + j] = ov[j];
+        }
+        l = g16_sum(l);
+        g16_argmax(bo, io);
+        g16_argmax(bt, it);
+        if (valid && gi == 0) {
+            my_loss += (type == 2) ? -l / (float)n_out : 0.5f * l;
+            my_hit += (io == it) ? 1u : 0u;
+        }
+    }
+    block_reduce_store(my_loss, my_hit, loss_acc, correct);
+}
+
 /* wide outputs: one WAVE per sample row, grid-stride */
 __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restrict__ Z, int ldz,
                                                            const float *__restrict__ T, int ldt,
@@ -613,6 +739,12 @@ inline int grid_for(long n, int bs) {
 
 }  // namespace
 
+/* HPNN_OD_WAVE=1: one row per wave for wide outputs (the kernel before output_delta_q) */
+static bool od_wave_mode() {
+    static const bool v = [] { const char *e = getenv("HPNN_OD_WAVE"); return e && e[0] == '1'; }();
+    return v;
+}
+
 extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ldt, const int *labels, float t_hi,
                                  float t_lo, void *D, int ldd, float *O, int ldo, float *loss_acc,
                                  unsigned int *correct, int B, int n_valid, int n_out, int type,
@@ -623,6 +755,12 @@ extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ld
         const int grid = (B + 255) / 256 < 256 ? (B + 255) / 256 : 256;
         hipLaunchKernelGGL(output_delta_rows_kernel<32>, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels,
                            t_hi, t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
+    } else if (n_out > 64 && ldz % 16 == 0 && ldd % 16 == 0 && ldd <= 256 && ldz >= ldd && (!O || ldo % 16 == 0) &&
+               !od_wave_mode()) {
+        /* four rows per wave (16 lanes per row): the grid covers the batch */
+        const int grid = (B + 15) / 16 < 4096 ? (B + 15) / 16 : 4096;
+        hipLaunchKernelGGL(output_delta_q_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi, t_lo,
+                           (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
     } else if (n_out <= 256) {
         /* one row per wave: the grid covers the batch (up to 16 waves per CU) */
         const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
