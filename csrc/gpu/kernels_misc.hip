@@ -359,6 +359,112 @@ __global__ __launch_bounds__(256) void output_delta_q_kernel(const float *__rest
     block_reduce_store(my_loss, my_hit, loss_acc, correct);
 }
 
+/* very wide outputs (> 256 classes, e.g. the synthetic 4096-wide ANN): one wave per row,
+ * every lane handling 4 consecutive columns per step (float4 Z / T loads, 8-byte delta
+ * stores); needs ldz and ldd multiples of 4.  The scalar kernel below moved
+ * 256 B per wave instruction and ran the 8192 x 4096 output at ~2 TB/s. */
+__global__ __launch_bounds__(256) void output_delta_v4_kernel(const float *__restrict__ Z, int ldz,
+                                                              const float *__restrict__ T, int ldt,
+                                                              const int *__restrict__ labels, float t_hi, float t_lo,
+                                                              __bf16 *__restrict__ D, int ldd, float *__restrict__ O,
+                                                              int ldo, float *__restrict__ loss_acc,
+                                                              unsigned int *__restrict__ correct, int B, int n_valid,
+                                                              int n_out, int type) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    const int cend = ldd > n_out ? ldd : n_out;
+    for (int row = blockIdx.x * 4 + wave; row < B; row += gridDim.x * 4) {
+        const bool valid = row < n_valid;
+        const int lab = (labels && valid) ? labels[row] : -1;
+        const float *zr = Z + (size_t)row * ldz;
+        float zmax = -INFINITY, denom = 0.f;
+        if (type == 2) {
+            for (int c = 4 * lane; c < n_out; c += 256) {
+                const float4 v = *(const float4 *)(zr + c);
+                const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (c + r < n_out) zmax = fmaxf(zmax, e[r]);
+            }
+            zmax = wave_max(zmax);
+            for (int c = 4 * lane; c < n_out; c += 256) {
+                const float4 v = *(const float4 *)(zr + c);
+                const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (c + r < n_out) denom += __expf(e[r] - zmax);
+            }
+            denom = wave_sum(denom);
+            denom += __expf(fminf(logf(TINY) + 1.0f - zmax, 80.f));
+        }
+        const float inv = type == 2 ? 1.0f / denom : 0.f;
+        float bo = -INFINITY, bt = -INFINITY, l = 0.f;
+        int io = -1, it = -1;
+        for (int c = 4 * lane; c < cend; c += 256) {
+            float e[4] = {0.f, 0.f, 0.f, 0.f}, tv[4] = {t_lo, t_lo, t_lo, t_lo};
+            if (c < n_out) {
+                const float4 v = *(const float4 *)(zr + c);
+                e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+                if (!labels && valid) {
+                    const float *tr = T + (size_t)row * ldt + c;
+                    if ((ldt & 3) == 0) {
+                        const float4 w = *(const float4 *)tr;
+                        tv[0] = w.x; tv[1] = w.y; tv[2] = w.z; tv[3] = w.w;
+                    } else { /* unaligned target rows: scalar loads, same values */
+#pragma unroll
+                        for (int r = 0; r < 4; r++) tv[r] = c + r < n_out ? tr[r] : t_lo;
+                    }
+                }
+            }
+            bf16x4 dv;
+            float ov[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int cc = c + r;
+                float d = 0.f, o = 0.f;
+                if (cc < n_out) {
+                    if (type == 2) o = __expf(e[r] - zmax) * inv;
+                    else if (type == 0) o = 2.0f / (1.0f + __expf(-e[r])) - 1.0f;
+                    else o = e[r];
+                    if (valid) {
+                        const float t = labels ? (cc == lab ? t_hi : t_lo) : tv[r];
+                        if (type == 2) {
+                            if (t != 0.f && o > 0.f) l += t * logf(o + TINY);
+                            d = t - o;
+                        } else if (type == 0) {
+                            l += (t - o) * (t - o);
+                            d = (t - o) * (-0.5f * (o * o - 1.0f));
+                        } else {
+                            l += (t - o) * (t - o);
+                            d = t - o;
+                        }
+                        if (o > bo) { bo = o; io = cc; }
+                        if (t > bt) { bt = t; it = cc; }
+                    }
+                }
+                ov[r] = o;
+                dv[r] = (__bf16)d;
+            }
+            if (c < ldd) *(bf16x4 *)(D + (size_t)row * ldd + c) = dv;
+            if (O && c < n_out) {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (c + r < n_out) O[(size_t)row * ldo + c + r] = ov[r];
+            }
+        }
+        l = wave_sum(l);
+        wave_argmax(bo, io);
+        wave_argmax(bt, it);
+        if (valid && lane == 0) {
+            my_loss += (type == 2) ? -l / (float)n_out : 0.5f * l;
+            my_hit += (io == it) ? 1u : 0u;
+        }
+    }
+    block_reduce_store(my_loss, my_hit, loss_acc, correct);
+}
+
 /* wide outputs: one WAVE per sample row, grid-stride */
 __global__ __launch_bounds__(256) void output_delta_kernel(const float *__restrict__ Z, int ldz,
                                                            const float *__restrict__ T, int ldt,
@@ -772,6 +878,10 @@ extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ld
         else if (n_out <= 192) HPNN_OD(3);
         else HPNN_OD(4);
 #undef HPNN_OD
+    } else if (ldz % 4 == 0 && ldd % 4 == 0 && !od_wave_mode()) {
+        const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
+        hipLaunchKernelGGL(output_delta_v4_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
+                           t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);
     } else {
         const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
         hipLaunchKernelGGL(output_delta_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,

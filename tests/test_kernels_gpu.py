@@ -218,7 +218,8 @@ def test_gemm_tn_integer_exact(gpu):
 
 @pytest.mark.parametrize("net_type", [ops.TYPE_SNN, ops.TYPE_ANN, ops.TYPE_LNN])
 @pytest.mark.parametrize("n_out,ldz,B", [(10, 32, 256), (230, 256, 256), (64, 64, 256), (100, 128, 256),
-                                        (150, 160, 256), (256, 256, 256), (300, 320, 256), (230, 256, 20000)])
+                                        (150, 160, 256), (256, 256, 256), (300, 320, 256), (230, 256, 20000),
+                                        (4096, 4096, 512), (1001, 1024, 300)])
 def test_output_delta(gpu, net_type, n_out, ldz, B):
     n_valid = B - 56
     torch.manual_seed(n_out + net_type)
