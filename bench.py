@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--graph", type=int, default=1,
                     help="capture the steps in HIP graphs (0: eager, 2: also with torch.distributed collectives)")
     ap.add_argument("--graph-steps", type=int, default=20, help="training steps per graph replay")
+    ap.add_argument("--input", choices=["u8", "float"], default="u8",
+                    help="synthetic images as 8-bit pixels (MNIST's format; the net sees pixel/255 in BF16) "
+                         "or as uniform floats in [0, 1)")
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
@@ -58,7 +61,10 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     Xs, Ls = [], []
     for _ in range(args.datasets):
-        X = torch.rand(m.Bp, sizes[0], device=dev, generator=g)
+        if args.input == "u8":
+            X = torch.randint(0, 256, (m.Bp, sizes[0]), device=dev, generator=g, dtype=torch.uint8)
+        else:
+            X = torch.rand(m.Bp, sizes[0], device=dev, generator=g)
         Xs.append(m.prepare_input(X))
         Ls.append(torch.randint(0, sizes[-1], (m.Bp,), device=dev, generator=g, dtype=torch.int32))
     torch.cuda.synchronize()
@@ -163,7 +169,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (uniform [0,1) pixels, uniform labels; random-init weights, reference init rule)",
+            "data": ("synthetic (uniform 8-bit pixels 0..255 -> pixel/255 in BF16 as MNIST images, uniform labels; "
+                     "random-init weights, reference init rule)" if args.input == "u8" else
+                     "synthetic (uniform [0,1) pixels, uniform labels; random-init weights, reference init rule)"),
             "config": {
                 "model": "mnist_snn 784-128-64-10 (SNN, BPM momentum 0.2, lr 0.01, batched mode)",
                 "global_batch": m.Bp * world,

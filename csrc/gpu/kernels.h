@@ -68,12 +68,13 @@ int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, int h_u8, fl
 /* weight gradient of hpnn_gemm_tn_bf16 over FRAGMENT-MAJOR operands (kernels_g0.hip):
  * Dg [Bt/32][N/16][64][8], Hg [Bt/32][M/16][64][8], lane l = 16 g + r of fragment (t, cb)
  * holding A[32 t + 8 g + j][16 cb + r] (j < 8); slab[s][n][m] as hpnn_gemm_tn_bf16.
- * Bt, M, N multiples of 32.  _reduce: plus hpnn_reduce_groups on appended workgroups. */
-int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits,
-                        hipStream_t stream);
-int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits,
-                               const float *rslab, int rS, long rstride, long rn, int rgroups, float *rout,
-                               hipStream_t stream);
+ * Bt, M, N multiples of 32.  h_u8: Hg holds unsigned bytes in the same layout, used as
+ * bf16(h * hscale) (pixel data).  _reduce: plus hpnn_reduce_groups on appended workgroups. */
+int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N, int M,
+                        int Bt, int splits, hipStream_t stream);
+int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
+                               int M, int Bt, int splits, const float *rslab, int rS, long rstride, long rn,
+                               int rgroups, float *rout, hipStream_t stream);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)

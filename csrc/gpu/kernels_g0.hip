@@ -32,6 +32,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 #include "mfma_common.h"
 
@@ -41,10 +43,22 @@ using hpnn::bf16x8;
 using hpnn::f32x4;
 using hpnn::TnTail;
 
-/* Dg: [Bt/32][N/16][64][8], Hg: [Bt/32][M/16][64][8]; nbd = N / 16, nbh = M / 16 */
-template <int WF, int WH, int PD, int KW>
+/* 8 unsigned bytes -> bf16x8 of (byte * scale) (exact for pixel values with scale 1) */
+__device__ __forceinline__ bf16x8 u8x8_bf16(uint2 v, float scale) {
+    bf16x8 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        r[e] = (__bf16)((float)((v.x >> (8 * e)) & 0xffu) * scale);
+        r[4 + e] = (__bf16)((float)((v.y >> (8 * e)) & 0xffu) * scale);
+    }
+    return r;
+}
+
+/* Dg: [Bt/32][N/16][64][8], Hg: [Bt/32][M/16][64][8]; nbd = N / 16, nbh = M / 16.
+ * HU8: Hg holds unsigned bytes (8 per lane per fragment), used as bf16(h * hscale) */
+template <int WF, int WH, int PD, int KW, bool HU8 = false>
 __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
-                                                                  const __bf16 *__restrict__ Hg, int nbh,
+                                                                  const void *__restrict__ Hg, int nbh, float hscale,
                                                                   float *__restrict__ slab, int ldg, int N, int ksteps,
                                                                   int splits, int tiles_n, int tiles, int xcd_map,
                                                                   TnTail tail) {
@@ -71,9 +85,11 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
     /* this wave group's k-steps: k0 + kg, k0 + kg + KW, ... */
     const int nk = (k1 - k0 - kg + KW - 1) / KW;
     const int r16 = lane & 15;
-    const __bf16 *pa = Hg + ((size_t)(k0 + kg) * nbh + m0 / 16) * 512 + lane * 8;
+    constexpr int ES = HU8 ? 1 : 2; /* bytes per H element */
+    using HT = typename std::conditional<HU8, uint2, bf16x8>::type;
+    const char *pa = (const char *)Hg + (((size_t)(k0 + kg) * nbh + m0 / 16) * 512 + lane * 8) * ES;
     const __bf16 *pb = Dg + ((size_t)(k0 + kg) * nbd + n0 / 16) * 512 + lane * 8;
-    const size_t step_a = (size_t)KW * nbh * 512, step_b = (size_t)KW * nbd * 512; /* this group's next k-step */
+    const size_t step_a = (size_t)KW * nbh * 512 * ES, step_b = (size_t)KW * nbd * 512; /* this group's next k-step */
 
     f32x4 acc[WF][WH];
 #pragma unroll
@@ -81,20 +97,25 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
 #pragma unroll
         for (int j = 0; j < WH; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    bf16x8 ra[R][WF], rb[R][WH];
+    HT ra[R][WF];
+    bf16x8 rb[R][WH];
     auto load = [&](int slot_, int t) __attribute__((always_inline)) {
         const int tc = t < nk - 1 ? t : nk - 1; /* clamped: the ring tail re-reads the last step */
 #pragma unroll
-        for (int i = 0; i < WF; i++) ra[slot_][i] = *(const bf16x8 *)(pa + i * 512 + (size_t)tc * step_a);
+        for (int i = 0; i < WF; i++) ra[slot_][i] = *(const HT *)(pa + i * 512 * ES + (size_t)tc * step_a);
 #pragma unroll
         for (int j = 0; j < WH; j++) rb[slot_][j] = *(const bf16x8 *)(pb + j * 512 + (size_t)tc * step_b);
     };
     auto mma = [&](int slot_) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < WF; i++)
+        for (int i = 0; i < WF; i++) {
+            bf16x8 a;
+            if constexpr (HU8) a = u8x8_bf16(ra[slot_][i], hscale);
+            else a = ra[slot_][i];
 #pragma unroll
             for (int j = 0; j < WH; j++)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[slot_][i], rb[slot_][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, rb[slot_][j], acc[i][j], 0, 0, 0);
+        }
     };
     if (nk > 0) {
 #pragma unroll
@@ -321,20 +342,20 @@ int launch_rs(const void *D, int ldd, const void *H, int ldh, float hscale, floa
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-template <int WF, int WH, int PD, int KW>
-int launch_fm(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits, hipStream_t s,
-              const TnTail &tail) {
+template <int WF, int WH, int PD, int KW, bool HU8 = false>
+int launch_fm(const void *Dg, const void *Hg, float hscale, float *slab, int ldg, int N, int M, int Bt, int splits,
+              hipStream_t s, const TnTail &tail) {
     constexpr int TMF = 32 * WF, TNH = 32 * WH;
     const int tiles_n = N / TNH, tiles = (M / TMF) * tiles_n;
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-    hipLaunchKernelGGL((gemm_fm_direct_kernel<WF, WH, PD, KW>), dim3(tiles * splits + tail.blocks), dim3(256 * KW), 0,
-                       s, (const __bf16 *)Dg, N / 16, (const __bf16 *)Hg, M / 16, slab, ldg, N, Bt / 32, splits,
-                       tiles_n, tiles, xcd_map, tail);
+    hipLaunchKernelGGL((gemm_fm_direct_kernel<WF, WH, PD, KW, HU8>), dim3(tiles * splits + tail.blocks),
+                       dim3(256 * KW), 0, s, (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32,
+                       splits, tiles_n, tiles, xcd_map, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int fm_dispatch(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt, int splits, hipStream_t s,
-                const TnTail &t) {
+int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N, int M, int Bt,
+                int splits, hipStream_t s, const TnTail &t) {
     if (N <= 0 || M <= 0 || Bt <= 0 || splits <= 0) return -1;
     if (Bt % 32 || splits > Bt / 32 || M % 32 || N % 32) return -2;
     if (ldg % 4 || ldg < M) return -3;
@@ -342,14 +363,22 @@ int fm_dispatch(const void *Dg, const void *Hg, float *slab, int ldg, int N, int
      * (two k-interleaved groups) with 2 / 1 in flight; measured 23.8 / 25.1 / 24.3 us vs
      * 23.8 us for the default (2 in flight, 4 waves) */
     static const int var = [] { const char *e = getenv("HPNN_G0D"); return e ? atoi(e) : 0; }();
+#define HPNN_FM(...)                                                                                              \
+    return h_u8 ? launch_fm<__VA_ARGS__, true>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)                  \
+                : launch_fm<__VA_ARGS__, false>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)
     if (M % 160 == 0 && N % 128 == 0) {
-        if (var == 1) return launch_fm<5, 4, 3, 1>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
-        if (var == 2) return launch_fm<5, 4, 2, 2>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
-        if (var == 3) return launch_fm<5, 4, 1, 2>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
-        return launch_fm<5, 4, 2, 1>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
+        if (var == 1) { HPNN_FM(5, 4, 3, 1); }
+        if (var == 2) { HPNN_FM(5, 4, 2, 2); }
+        if (var == 3) { HPNN_FM(5, 4, 1, 2); }
+        if (var == 4) { HPNN_FM(5, 4, 2, 1); }
+        /* 8-bit H: 8 waves (two k-interleaved groups) hide the byte -> bf16 conversion
+         * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves */
+        if (h_u8) { HPNN_FM(5, 4, 1, 2); }
+        HPNN_FM(5, 4, 2, 1);
     }
-    if (M % 64 == 0 && N % 64 == 0) return launch_fm<2, 2, 2, 1>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
-    return launch_fm<1, 1, 3, 1>(Dg, Hg, slab, ldg, N, M, Bt, splits, s, t);
+    if (M % 64 == 0 && N % 64 == 0) { HPNN_FM(2, 2, 2, 1); }
+    HPNN_FM(1, 1, 3, 1);
+#undef HPNN_FM
 }
 
 }  // namespace
@@ -379,18 +408,18 @@ extern "C" int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, i
     return -2;
 }
 
-extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M, int Bt,
-                                   int splits, hipStream_t stream) {
+extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
+                                   int M, int Bt, int splits, hipStream_t stream) {
     const TnTail none = {nullptr, nullptr, 0, 0, 0, 0, 1, 1, 0};
-    return fm_dispatch(Dg, Hg, slab, ldg, N, M, Bt, splits, stream, none);
+    return fm_dispatch(Dg, Hg, h_u8, hscale, slab, ldg, N, M, Bt, splits, stream, none);
 }
 
-extern "C" int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, float *slab, int ldg, int N, int M,
-                                          int Bt, int splits, const float *rslab, int rS, long rstride, long rn,
-                                          int rgroups, float *rout, hipStream_t stream) {
+extern "C" int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab,
+                                          int ldg, int N, int M, int Bt, int splits, const float *rslab, int rS,
+                                          long rstride, long rn, int rgroups, float *rout, hipStream_t stream) {
     if (rn % 4 || rstride % 4 || rS < 1 || rgroups < 1 || rgroups > rS || !rslab || !rout) return -2;
     const long n4 = rn / 4;
     const int bx = (int)((n4 + 255) / 256);
     const TnTail t = {rslab, rout, rstride, n4, rn, rS, (rS + rgroups - 1) / rgroups, bx, bx * rgroups};
-    return fm_dispatch(Dg, Hg, slab, ldg, N, M, Bt, splits, stream, t);
+    return fm_dispatch(Dg, Hg, h_u8, hscale, slab, ldg, N, M, Bt, splits, stream, t);
 }

@@ -116,12 +116,15 @@ PYBIND11_MODULE(_native, m) {
                               (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
               "gemm_tn_rs");
     });
-    m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, uptr slab, int ldg, int N, int M, int Bt, int splits, uptr stream) {
-        check(hpnn_gemm_fm_direct(P(Dg), P(Hg), (float *)P(slab), ldg, N, M, Bt, splits, S(stream)), "gemm_fm_direct");
+    m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, int h_u8, float hscale, uptr slab, int ldg, int N, int M, int Bt,
+                               int splits, uptr stream) {
+        check(hpnn_gemm_fm_direct(P(Dg), P(Hg), h_u8, hscale, (float *)P(slab), ldg, N, M, Bt, splits, S(stream)),
+              "gemm_fm_direct");
     });
-    m.def("gemm_fm_direct_reduce", [](uptr Dg, uptr Hg, uptr slab, int ldg, int N, int M, int Bt, int splits,
-                                      uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout, uptr stream) {
-        check(hpnn_gemm_fm_direct_reduce(P(Dg), P(Hg), (float *)P(slab), ldg, N, M, Bt, splits,
+    m.def("gemm_fm_direct_reduce", [](uptr Dg, uptr Hg, int h_u8, float hscale, uptr slab, int ldg, int N, int M,
+                                      int Bt, int splits, uptr rslab, int rS, long rstride, long rn, int rgroups,
+                                      uptr rout, uptr stream) {
+        check(hpnn_gemm_fm_direct_reduce(P(Dg), P(Hg), h_u8, hscale, (float *)P(slab), ldg, N, M, Bt, splits,
                                          (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout),
                                          S(stream)),
               "gemm_fm_direct_reduce");

@@ -34,6 +34,12 @@ _TAIL_REDUCE = os.environ.get("HPNN_TAIL_REDUCE", "1") == "1"
 # LDS-staged TN GEMM then re-reads partly from the MALL): 82-83 us/step vs 77.3-77.8
 # (G0 37.8 vs 34.1 us under rocprofv3, scripts/gpu_fm_prof.sh)
 _G0_FM = os.environ.get("HPNN_G0_FM", "0") == "1"
+# uint8 (pixel) input on the fused path: fragment-major 8-bit copy for the G0 kernel
+# (HPNN_G0_FM_U8=0 disables: LDS-staged TN GEMM on the BF16 batch)
+_G0_FM_U8 = os.environ.get("HPNN_G0_FM_U8", "1") == "1"
+# the value a uint8 input means (1/255: MNIST pixels normalised to [0, 1])
+PIXEL_SCALE = float(torch.tensor(float(os.environ.get("HPNN_PIXEL_SCALE", str(1.0 / 255.0))),
+                                 dtype=torch.float32).item())
 # HPNN_G0_RS=1: first-layer gradient with the register-staged TN kernel (kernels_g0.hip):
 # 75.46-76.57 us/step vs 75.73-77.32 with the LDS-DMA TN kernel (scripts/gpu_ab_g0.sh),
 # within noise of each other
@@ -182,18 +188,32 @@ class MLP:
         return [self.W32[l][:self.sizes[l + 1], :self.sizes[l]].double().cpu() for l in range(self.L)]
 
     def prepare_input(self, X):
-        """float/double [n, n_in] -> padded BF16 [Bp, Kp0] device tensor.
+        """[n, n_in] -> padded BF16 [Bp, Kp0] device tensor.
 
-        On the fused MNIST-shape path ("x") the returned tensor also carries, as attribute
-        `hpnn_fm`, a fragment-major copy of the same values (ops.to_fragment_major): the
-        operand layout of the first-layer gradient kernel (csrc/gpu/kernels_g0.hip), made
-        once per prepared batch so that every training step on it streams 1 KiB fragments
-        instead of transposing X through LDS (HPNN_G0_FM=1; off by default, see _G0_FM)."""
+        X float/double: the values as given.  X uint8 (8-bit pixel data, e.g. MNIST images):
+        the network sees bf16(X * PIXEL_SCALE) (PIXEL_SCALE = 1/255, the usual [0, 1]
+        normalisation; HPNN_PIXEL_SCALE overrides, 1 = raw 0..255 values as the reference's
+        pmnist writes them), and on the fused MNIST-shape path ("x") the returned tensor
+        also carries the pixels themselves in fragment-major order (attribute `hpnn_fm`,
+        ops.to_fragment_major, one byte per value): the first-layer gradient kernel
+        (csrc/gpu/kernels_g0.hip) streams that copy -- half the bytes of the BF16 batch, no
+        LDS transposes -- and converts it exactly as above.  HPNN_G0_FM=1 attaches a
+        fragment-major BF16 copy for float input too (off by default, see _G0_FM)."""
         Xd = X.to(self.device)
-        out = torch.empty(ops.pad_to(X.shape[0], 128), self.Kp[0], dtype=torch.bfloat16, device=self.device)
+        rows = ops.pad_to(X.shape[0], 128)
+        out = torch.empty(rows, self.Kp[0], dtype=torch.bfloat16, device=self.device)
+        if Xd.dtype == torch.uint8:
+            u8 = torch.zeros(rows, self.Kp[0], dtype=torch.uint8, device=self.device)
+            u8[:X.shape[0], :X.shape[1]] = Xd
+            out.copy_((u8.float() * PIXEL_SCALE).bfloat16())  # the same rounding as the kernel's
+            if self.fused_mode == "x" and _G0_FM_U8:
+                out.hpnn_fm = ops.to_fragment_major(u8)
+                out.hpnn_fm_scale = PIXEL_SCALE
+            return out
         ops.pack_bf16(Xd.contiguous(), out)
         if self.fused_mode == "x" and _G0_FM:
             out.hpnn_fm = ops.to_fragment_major(out)
+            out.hpnn_fm_scale = 1.0
         return out
 
     def _fm_input(self, X):
@@ -226,7 +246,8 @@ class MLP:
         Hin = X if l == 0 else self.H[l - 1]
         Xg = self._fm_input(X) if l == 0 and self.fused_mode == "x" else None
         if Xg is not None:  # delta1 came fragment-major from the fused front
-            ops.gemm_fm_direct(self.D[0], Xg, self.Np[0], self.Kp[0], splits=self.S[0], out=self.slab[0])
+            ops.gemm_fm_direct(self.D[0], Xg, self.Np[0], self.Kp[0], splits=self.S[0], out=self.slab[0],
+                               hscale=getattr(X, "hpnn_fm_scale", 1.0))
         else:
             ops.gemm_tn(self.D[l], Hin, splits=self.S[l], out=self.slab[l])
         if reduce:
@@ -302,7 +323,7 @@ class MLP:
         Xg = self._fm_input(X)
         if Xg is not None:
             ops.gemm_fm_direct_reduce(self.D[0], Xg, self.Np[0], self.Kp[0], self.S[0], self.slab[0], self.midslab,
-                                      self.mid_groups, groups)
+                                      self.mid_groups, groups, hscale=getattr(X, "hpnn_fm_scale", 1.0))
         elif _G0_RS and (self.Kp[0] % 128 == 0 or self.Kp[0] % 160 == 0):
             ops.gemm_tn_rs(self.D[0], X, self.S[0], self.slab[0], rslab=self.midslab, groups=self.mid_groups,
                            rout=groups)

@@ -123,28 +123,32 @@ def from_fragment_major(Ag, rows, cols):
     return Ag.view(rows // 32, cols // 16, 4, 16, 8).permute(0, 2, 4, 1, 3).reshape(rows, cols)
 
 
-def gemm_fm_direct(Dg, Hg, N, M, splits=1, out=None):
+def gemm_fm_direct(Dg, Hg, N, M, splits=1, out=None, hscale=1.0):
     """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m] (gemm_tn) with D, H
     given fragment-major (to_fragment_major), direct-to-register loads
-    (csrc/gpu/kernels_g0.hip)"""
+    (csrc/gpu/kernels_g0.hip).  Hg may be uint8 (pixel data): used as bf16(H * hscale)."""
     Bt = Dg.numel() // N
+    u8 = Hg.dtype == torch.uint8
     if out is None:
         out = torch.empty(splits, N, M, dtype=torch.float32, device=Dg.device)
     if _cpu(Dg):
-        return gemm_tn(from_fragment_major(Dg, Bt, N), from_fragment_major(Hg, Bt, M), splits=splits, out=out)
-    native().gemm_fm_direct(Dg.data_ptr(), Hg.data_ptr(), out.data_ptr(), out.stride(1), N, M, Bt, splits, _stream())
+        H = from_fragment_major(Hg, Bt, M)
+        return gemm_tn(from_fragment_major(Dg, Bt, N), (H.float() * hscale).bfloat16() if u8 else H, splits=splits,
+                       out=out)
+    native().gemm_fm_direct(Dg.data_ptr(), Hg.data_ptr(), int(u8), float(hscale), out.data_ptr(), out.stride(1), N, M,
+                            Bt, splits, _stream())
     return out
 
 
-def gemm_fm_direct_reduce(Dg, Hg, N, M, splits, out, rslab, groups, rout):
+def gemm_fm_direct_reduce(Dg, Hg, N, M, splits, out, rslab, groups, rout, hscale=1.0):
     """gemm_fm_direct and reduce_groups(rslab, groups, rout) in ONE launch"""
     if _cpu(Dg):
-        gemm_fm_direct(Dg, Hg, N, M, splits=splits, out=out)
+        gemm_fm_direct(Dg, Hg, N, M, splits=splits, out=out, hscale=hscale)
         return reduce_groups(rslab, groups, rout)
     Bt = Dg.numel() // N
-    native().gemm_fm_direct_reduce(Dg.data_ptr(), Hg.data_ptr(), out.data_ptr(), out.stride(1), N, M, Bt, splits,
-                                   rslab.data_ptr(), rslab.shape[0], rslab.stride(0), rslab[0].numel(), groups,
-                                   rout.data_ptr(), _stream())
+    native().gemm_fm_direct_reduce(Dg.data_ptr(), Hg.data_ptr(), int(Hg.dtype == torch.uint8), float(hscale),
+                                   out.data_ptr(), out.stride(1), N, M, Bt, splits, rslab.data_ptr(), rslab.shape[0],
+                                   rslab.stride(0), rslab[0].numel(), groups, rout.data_ptr(), _stream())
     return rout
 
 

@@ -32,12 +32,14 @@ Xs = [x.bfloat16() for x in Xu]  # exact
 Ds = [((torch.rand(B, N, device=dev) - 0.5) / 8).bfloat16() for _ in range(4)]
 Xg = [ops.to_fragment_major(x) for x in Xs]
 Dg = [ops.to_fragment_major(d) for d in Ds]
+Xgu = [ops.to_fragment_major(x) for x in Xu]
 out = torch.empty(S, N, M, device=dev)
 ref = Ds[0].float().t() @ Xs[0].float()
 for name, fn in [("tn", lambda i: ops.gemm_tn(Ds[i], Xs[i], splits=S, out=out)),
                  ("rs", lambda i: ops.gemm_tn_rs(Ds[i], Xs[i], splits=S, out=out)),
                  ("fm", lambda i: ops.gemm_fm_direct(Dg[i], Xg[i], N, M, splits=S, out=out)),
-                 ("rs-u8", lambda i: ops.gemm_tn_rs(Ds[i], Xu[i], splits=S, out=out))]:
+                 ("rs-u8", lambda i: ops.gemm_tn_rs(Ds[i], Xu[i], splits=S, out=out)),
+                 ("fm-u8", lambda i: ops.gemm_fm_direct(Dg[i], Xgu[i], N, M, splits=S, out=out))]:
     hot, cold = t(fn, 1), t(fn, 4)
     fn(0)
     err = (out.sum(0) - ref).abs().max().item()
