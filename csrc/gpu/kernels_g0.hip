@@ -12,8 +12,12 @@
  * snn_kernel_train (ann.c:1279-1592, cuda_ann.cu ger_acc), batched.
  *
  * Used for MNIST's first-layer gradient G0 = delta1^T X (800 x 128 over 65536 rows): the
- * fused front (kernels_mlp3x.hip, d1fm) writes delta1 in this layout, the input batch
- * has a fragment-major copy made once when it is prepared (MLP.prepare_input).
+ * fused front (kernels_mlp3x.hip, d1fm) writes delta1 in this layout, and an 8-bit pixel
+ * batch keeps a fragment-major copy of its bytes, made once when it is prepared
+ * (MLP.prepare_input): half the bytes of the BF16 batch, converted in registers to the
+ * same bf16(pixel * scale) values the front computes with (8 waves hide the conversion).
+ * In the step: 72.5-72.7 us with it vs 74.8-75.6 us for the LDS-DMA TN kernel on the
+ * BF16 batch (scripts/gpu_ab_input.sh); cold 26.5 us vs 34 in scripts/g0_direct.py.
  * Measured (scripts/g0_direct.py, 48 splits): LDS-staged TN kernel 31.2 us (its LDS-DMA
  * fill, ~27 GB/s per CU, is the bound); this kernel 23.8 us, ~5.1 TB/s of HBM reads --
  * it streams at the memory rate.  Rejected on the way: the same kernel on plain
@@ -371,6 +375,8 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
         if (var == 2) { HPNN_FM(5, 4, 2, 2); }
         if (var == 3) { HPNN_FM(5, 4, 1, 2); }
         if (var == 4) { HPNN_FM(5, 4, 2, 1); }
+        if (var == 5) { HPNN_FM(5, 4, 3, 2); } /* 8-bit H: 23.9 / 27.0 us, no gain */
+        if (var == 6) { HPNN_FM(5, 4, 5, 2); } /* 8-bit H: 24.0 / 27.6 us */
         /* 8-bit H: 8 waves (two k-interleaved groups) hide the byte -> bf16 conversion
          * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves */
         if (h_u8) { HPNN_FM(5, 4, 1, 2); }
