@@ -17,12 +17,14 @@ SIZES = [784, 128, 64, 10]
 B = 8192
 
 
-def _data(rank, step):
+def _data(rank, step, u8=False):
     g = torch.Generator().manual_seed(100 * rank + step)
-    return torch.rand(B, SIZES[0], generator=g), torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
+    x = (torch.randint(0, 256, (B, SIZES[0]), generator=g, dtype=torch.uint8) if u8
+         else torch.rand(B, SIZES[0], generator=g))
+    return x, torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
 
 
-def _worker(rank, world, port, graph, q):
+def _worker(rank, world, port, graph, q, u8=False):
     try:
         os.environ["LOCAL_WORLD_SIZE"] = str(world)
         os.environ["HPNN_XAR_TIMEOUT_MS"] = "2000"
@@ -37,8 +39,10 @@ def _worker(rank, world, port, graph, q):
         dp.broadcast_parameters()
         batches = []
         for step in range(3):
-            x, lab = _data(rank, step)
+            x, lab = _data(rank, step, u8)
             batches.append((m.prepare_input(x.to(dev)), lab.to(dev)))
+            if u8:  # 8-bit pixels: fragment-major byte copy for the first-layer gradient
+                assert m._fm_input(batches[-1][0]) is not None
         if graph:
             # step 0 eager, steps 1-2 from one captured graph replayed twice over the same inputs
             dp.train_step(batches[0][0], labels=batches[0][1], lr=0.05, alpha=0.2)
@@ -66,12 +70,12 @@ def _worker(rank, world, port, graph, q):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def _reference():
+def _reference(u8=False):
     from hpnn_amd.models import MLP
     dev = torch.device("cuda", 0)
     m = MLP(SIZES, "SNN", batch=2 * B, device=dev, momentum=True, seed=3)
     for step in (0, 1, 1):
-        xs, ls = zip(*[_data(r, step) for r in range(2)])
+        xs, ls = zip(*[_data(r, step, u8) for r in range(2)])
         X = m.prepare_input(torch.cat(xs).to(dev))
         m.train_step(X, labels=torch.cat(ls).to(dev), lr=0.05, alpha=0.2)
     torch.cuda.synchronize()
@@ -79,14 +83,14 @@ def _reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("graph", [False, True])
-def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph):
+@pytest.mark.parametrize("graph,u8", [(False, False), (True, False), (True, True)])
+def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph, u8):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, graph, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, graph, q, u8)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=110) for _ in ps)
@@ -97,6 +101,6 @@ def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph):
     for r in (0, 1):
         assert isinstance(res[r], torch.Tensor), res[r]
     assert torch.equal(res[0], res[1])  # deterministic, identical on every rank
-    ref = _reference()
+    ref = _reference(u8)
     err = (res[0] - ref).abs().max().item()
     assert err < 2e-6, err
