@@ -223,7 +223,7 @@ __device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g) {
  * TWO = true: shard s = [s * sh, min((s + 1) * sh, n4)), workgroup b owns
  * [s * sh + b * per, ...+ per) of every shard */
 template <bool TWO, bool UPD>
-__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
+__global__ __launch_bounds__(1024) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
                                                   long n4, long half_stride4, unsigned long long timeout, int light,
                                                   XarUpd upd) {
     const int b = blockIdx.x;
@@ -283,6 +283,20 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
     }
 }
 
+/* self-test pattern: rank r, element i -> (r + 1) * (i % 97 + 1) / 16; sums over <= 8
+ * ranks are small multiples of 1/16, exact in FP32 in any order */
+__global__ void xar_fill_kernel(float *__restrict__ v, long n, int rank) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        v[i] = (float)(rank + 1) * (float)(i % 97 + 1) * 0.0625f;
+}
+__global__ void xar_check_kernel(const float *__restrict__ v, long n, int world, unsigned int *__restrict__ bad) {
+    const float tri = (float)(world * (world + 1) / 2);
+    unsigned int nbad = 0;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        nbad += v[i] != tri * (float)(i % 97 + 1) * 0.0625f;
+    if (nbad) atomicAdd(bad, nbad);
+}
+
 struct IpcHandles {
     hipIpcMemHandle_t buf, sig;
 };
@@ -301,6 +315,7 @@ struct hpnn_xar {
     int mode = 0;     /* HPNN_XAR_MODE: 0 auto, 1 one-shot, 2 two-shot */
     int light = 1;    /* HPNN_XAR_FENCE=1 -> 0: full system fences, see xbarrier */
     int blocks = 128; /* HPNN_XAR_BLOCKS (same on every rank), <= HPNN_XAR_MAX_BLOCKS */
+    int threads = 256; /* HPNN_XAR_THREADS: 64..1024, multiple of 64 */
 };
 
 extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
@@ -328,6 +343,8 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     c->light = !(fe && fe[0] == '1');
     const char *nb = getenv("HPNN_XAR_BLOCKS");
     if (nb && atoi(nb) > 0) c->blocks = atoi(nb) < HPNN_XAR_MAX_BLOCKS ? atoi(nb) : HPNN_XAR_MAX_BLOCKS;
+    const char *nt = getenv("HPNN_XAR_THREADS");
+    if (nt && atoi(nt) >= 64 && atoi(nt) <= 1024 && atoi(nt) % 64 == 0) c->threads = atoi(nt);
     c->peers.buf[rank] = (float4 *)c->buf;
     c->peers.sig[rank] = c->sig;
     return c;
@@ -390,7 +407,7 @@ static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipS
     XarUpd none = {};
     const XarUpd &u = upd ? *upd : none;
 #define HPNN_XARL(T_, U_)                                                                                          \
-    hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,       \
+    hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3((unsigned)c->threads), 0, stream, c->peers, c->rank,       \
                        c->world, in, (float4 *)out, n4, half4, c->timeout, c->light, u)
     if (two) {
         if (upd) HPNN_XARL(true, true);
@@ -480,6 +497,39 @@ extern "C" int hpnn_xar_status(hpnn_xar *c) {
     unsigned int err = 0;
     if (hipMemcpy(&err, &c->sig->error, 4, hipMemcpyDeviceToHost) != hipSuccess) return -2;
     return err ? -1 : 0;
+}
+
+extern "C" int hpnn_xar_self_test(hpnn_xar *c, hipStream_t stream) {
+    if (!c) return -3;
+    /* one-shot size (4 KiB) and the whole buffer (two-shot from 4 ranks), each twice:
+     * consecutive calls use alternate halves */
+    const long full = (long)(c->max_bytes / 4) & ~3L, small = full < 1024 ? full : 1024;
+    float *v = nullptr;
+    unsigned int *bad = nullptr;
+    int rc = 0;
+    if (hipMalloc((void **)&v, (size_t)full * 4) != hipSuccess || hipMalloc((void **)&bad, 4) != hipSuccess ||
+        hipMemsetAsync(bad, 0, 4, stream) != hipSuccess)
+        rc = -3;
+    const long sizes[4] = {small, small, full, full};
+    for (int t = 0; t < 4 && rc == 0; t++) {
+        const long n = sizes[t];
+        hipLaunchKernelGGL(xar_fill_kernel, dim3(256), dim3(256), 0, stream, v, n, c->rank);
+        if (hpnn_xar_all_reduce_f32(c, v, v, n, stream) != 0) rc = -3;
+        hipLaunchKernelGGL(xar_check_kernel, dim3(256), dim3(256), 0, stream, v, n, c->world, bad);
+    }
+    unsigned int nbad = 0;
+    if (rc == 0 && (hipMemcpyAsync(&nbad, bad, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                    hipStreamSynchronize(stream) != hipSuccess))
+        rc = -3;
+    if (rc == 0 && hpnn_xar_status(c) != 0) rc = -2;
+    else if (rc == 0 && nbad) {
+        NN_ERROR(stderr, "xgmi all-reduce self-test: %u wrong elements on rank %d\n", nbad, c->rank);
+        rc = -1;
+    }
+    hipStreamSynchronize(stream);
+    if (v) hipFree(v);
+    if (bad) hipFree(bad);
+    return rc;
 }
 
 extern "C" void hpnn_xar_destroy(hpnn_xar *c) {

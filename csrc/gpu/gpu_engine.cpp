@@ -949,6 +949,13 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         std::vector<int> oks(W);
         if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return FALSE;
         for (int v : oks) use_xar = use_xar && v;
+        if (use_xar) { /* known sums over the real links before any gradient goes through */
+            const int rc = hpnn_xar_self_test(xar, s);
+            ok = rc == 0;
+            if (!ok) NN_WARN(stderr, "xGMI all-reduce self-test failed (%d) on rank %d\n", rc, R);
+            if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return FALSE;
+            for (int v : oks) use_xar = use_xar && v;
+        }
         if (!use_xar && xar) {
             hpnn_xar_destroy(xar);
             xar = nullptr;

@@ -260,6 +260,7 @@ PYBIND11_MODULE(_native, m) {
                     "xar_all_reduce_slabs_update_f32");
           });
     m.def("xar_status", [](uptr c) { return hpnn_xar_status((hpnn_xar *)c); });
+    m.def("xar_self_test", [](uptr c, uptr stream) { return hpnn_xar_self_test((hpnn_xar *)c, S(stream)); });
     m.def("xar_destroy", [](uptr c) { hpnn_xar_destroy((hpnn_xar *)c); });
     m.def("comm_set_xar", [](uptr c, uptr x, size_t max_bytes) {
         check(hpnn_comm_set_xar((hpnn_comm *)c, (hpnn_xar *)x, max_bytes), "comm_set_xar");

@@ -107,6 +107,15 @@ class NativeComm:
                 ok = False
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 1 and os.environ.get("HPNN_XAR_SELFTEST", "1") != "0":
+            # every rank mapped every peer: check on the real links that each rank receives
+            # exactly the known sums (a mapping / coherence fault shows here, not as silently
+            # wrong gradients later), then agree; any failure sends every rank to RCCL
+            rc = n.xar_self_test(x, _stream())
+            if rc != 0:
+                print(f"rank {self.rank}: xGMI all-reduce self-test failed ({rc}); using RCCL", flush=True)
+            flag.fill_(1 if rc == 0 else 0)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         if int(flag.item()) != 1:
             if x:
                 n.xar_destroy(x)

@@ -80,6 +80,15 @@ int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, 
                                          int momentum, hipStream_t stream);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
 int hpnn_xar_status(hpnn_xar *c);
+/* collective self-test, run by every rank right after hpnn_xar_open: all-reduces known
+ * rank-dependent vectors (every partial sum exact in FP32, so any summation order gives
+ * the same bits) at a one-shot size and at the full buffer size, twice each so both
+ * buffer halves are used, and compares the result on the device.  Returns 0 when this
+ * rank received exactly the expected sums, -1 on a wrong element (peer writes not visible
+ * over the links: coherence / mapping fault), -2 on a barrier timeout, -3 on a HIP error.
+ * Every rank must call it (it is a collective); callers then agree across ranks (MIN of
+ * the results) before the all-reduce is used. */
+int hpnn_xar_self_test(hpnn_xar *c, hipStream_t stream);
 void hpnn_xar_destroy(hpnn_xar *c);
 
 #ifdef __cplusplus

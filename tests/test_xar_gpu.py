@@ -4,7 +4,7 @@ The GPU box has one MI355X, so both ranks run on device 0: the peer buffers are 
 through hipIpc exactly as on an 8-GPU node (the data path is then local HBM instead of
 an xGMI link, the protocol -- IPC mapping, flag barriers, epochs, fixed-order sum -- is
 the same).  Checked: sums of several bucket sizes against the host sum, in-place use,
-repeated calls (alternating buffer halves, mixed one-/two-shot calls in auto mode at 4
+the attach-time self-test, repeated calls (alternating buffer halves, mixed one-/two-shot calls in auto mode at 4
 ranks), slab-sum inputs, HIP-graph capture + replays, and the bounded barrier: a rank
 whose peer never arrives reports a timeout instead of hanging."""
 import os
@@ -40,6 +40,10 @@ def _worker(rank, world, port, q, mode):
         dist.barrier()
         s = torch.cuda.current_stream().cuda_stream
         errs = []
+        # the attach-time self-test (known exact sums at a one-shot and the full size)
+        rc = n.xar_self_test(x, s)
+        if rc != 0:
+            errs.append(f"self-test returned {rc}")
         for it in range(3):
             for sz in SIZES:
                 a = _data(rank, sz, it).cuda()
