@@ -356,11 +356,18 @@ int launch_nt_big(const void *A, int lda, const void *B, int ldb, void *C, int l
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* large NT GEMMs on the 8-phase kernel (kernels_nt8.hip); HPNN_NT_8PH=0 keeps the 1-phase
+ * 256x256 kernel, hpnn_gemm_nt_set_8ph() switches at run time (A/B benchmarks) */
+int g_nt8 = [] { const char *e = getenv("HPNN_NT_8PH"); return !(e && e[0] == '0'); }();
+
 template <int EPI, bool CF32>
 int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
                   int N, int K, hipStream_t s) {
     const bool k64 = (K % 64) == 0;
     static const int big_off = [] { const char *e = getenv("HPNN_NT_BIG"); return e && e[0] == '0'; }();
+    if (!big_off && g_nt8 && K % 128 == 0 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 &&
+        K >= 512)
+        return hpnn_gemm_nt8_bf16(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, EPI, CF32 ? 1 : 0, s);
     if (!big_off && k64 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 && K >= 512)
         return launch_nt_big<EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s);
 #define HPNN_NT(BN_)                                                                                  \
@@ -460,6 +467,8 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
 }
 
 }  // namespace
+
+extern "C" void hpnn_gemm_nt_set_8ph(int on) { g_nt8 = on ? 1 : 0; }
 
 extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {

@@ -1,0 +1,268 @@
+/*
+ * 256x256-tile NT GEMM with an 8-phase software pipeline (gfx950, BF16 in, FP32 acc).
+ *
+ *   C[M x N] = epi(A[M x K] . B[N x K]^T)   -- the forward (bipolar epilogue) and the
+ *   delta (f'(h) epilogue) GEMMs of the large-layer path; same contract and epilogues
+ *   as gemm_nt_pipe_kernel (kernels_mfma.hip).  Reference: the per-slice cublasDgemv /
+ *   fw_mv_acc / dsigmoid_mul_delta_T of cuda_ann.cu:426-2093, batched.
+ *
+ * Why a second kernel: the 1-phase 256x256 kernel (one wait + barrier, all of a K-step's
+ * LDS reads and MFMAs, barrier) serialises each wave's LDS reads with its MFMAs and keeps
+ * only one K-step in flight; it tops out near 1 PFLOP/s on 8192x4096x4096.  Here:
+ *
+ *  - 8 waves (2 M x 4 N), wave tile 128 x 64 = 2 x 2 quadrants of 64 x 32 (16 MFMAs of
+ *    16x16x32 per quadrant per 64-wide K-tile);
+ *  - LDS: two K-tile buffers E / O (even / odd K-tiles) of four 16 KiB half-tiles
+ *    (A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255), 128 KiB total, filled by
+ *    LDS-DMA (global_load_lds_dwordx4) with the swizzle of nt_off<8> applied on the source
+ *    address (conflict-free ds_read_b128);
+ *  - one iteration = 2 K-tiles = 8 phases; phase p computes one quadrant:
+ *        [ds_reads of the quadrant's new operands; LDS-DMA issue; counted vmcnt]
+ *        s_barrier; lgkmcnt(0); setprio 1; 16 MFMAs; setprio 0; s_barrier
+ *    quadrant order (0,0) (0,1) (1,1) (1,0): 12, 4, 8 and 0 ds_read_b128 per phase;
+ *  - the waves of M-half 1 run one barrier behind those of M-half 0 (one extra barrier at
+ *    the start), so on every SIMD one wave issues MFMAs while the other reads LDS;
+ *  - prefetch: a half-tile is restaged two phases after its last read (the stagger makes
+ *    one phase unsafe) and waited for with a counted vmcnt one phase before its first
+ *    read, never vmcnt(0) in the steady state:
+ *        P1: A(o) -> O     P4: B(e+2) -> E, vmcnt(4)     P5: A(e+2) -> E
+ *        P8: B(o+2) -> O, vmcnt(4)                       (e = 2i, o = 2i + 1)
+ *  - XCD-aware block order: each XCD gets a contiguous run of output tiles (bijective for
+ *    any grid), so neighbouring tiles that share A / B panels share that XCD's L2.
+ * Requires M % 256 == 0, N % 256 == 0, K % 128 == 0.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "kernels.h"
+#include "mfma_common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int HALF = 16384;   /* bytes of one 128-row x 64-col BF16 half-tile */
+constexpr int KBUF = 4 * HALF; /* one K-tile: A0 A1 B0 B1 */
+
+/* swizzled byte offset of 16-byte chunk c of row r in a 128-B-row half-tile image */
+__device__ __forceinline__ int off8(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EPI, bool CF32>
+__global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict__ A, int lda,
+                                                       const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
+                                                       int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
+                                                       int tiles_n, int ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * KBUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3; /* wm = stagger group */
+    /* XCD-aware, bijective: blocks b, b+8, b+16, ... (one XCD) take consecutive tiles */
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int KT = K / 64;
+    const size_t lda_b = (size_t)lda * 2, ldb_b = (size_t)ldb * 2;
+    const char *Ag = (const char *)(A + (size_t)m0 * lda);
+    const char *Bg = (const char *)(B + (size_t)n0 * ldb);
+
+    /* LDS-DMA of half-tile h (0,1: A rows 128h..; 2,3: B rows 128(h-2)..) of K-tile kt
+     * into buffer kt & 1: 16 pieces of 8 rows, two per wave; wave-uniform base in SGPRs,
+     * one 32-bit per-lane offset (row, source-swizzled chunk) per piece */
+    unsigned int voa[2], vob[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int r = (wave * 2 + i) * 8 + (lane >> 3), cl = (lane & 7) ^ ((r >> 1) & 7);
+        voa[i] = (unsigned int)(r * lda_b + cl * 16);
+        vob[i] = (unsigned int)(r * ldb_b + cl * 16);
+    }
+    auto stage = [&](int h, int kt) __attribute__((always_inline)) {
+        char *dst = lds + (kt & 1) * KBUF + h * HALF;
+        const char *g = h < 2 ? Ag + (size_t)(h * 128) * lda_b : Bg + (size_t)((h - 2) * 128) * ldb_b;
+        g += (size_t)kt * 128;
+#pragma unroll
+        for (int i = 0; i < 2; i++) hpnn::glds16_sv(g, h < 2 ? voa[i] : vob[i], dst + (wave * 2 + i) * 1024);
+    };
+
+    f32x4 acc[2][2][4][2]; /* [mi][ni][j: 16-row frag][i: 16-col frag] */
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++) acc[a][b][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int r16 = lane & 15, q = lane >> 4;
+    bf16x8 ra[4][2], rb0[2][2], rb1[2][2]; /* [frag][k32 substep] */
+    auto read_a = [&](const char *buf, int mi) __attribute__((always_inline)) {
+        const char *img = buf + wm * HALF;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) ra[j][kk] = *(const bf16x8 *)(img + off8(mi * 64 + j * 16 + r16, kk * 4 + q));
+    };
+    auto read_b = [&](const char *buf, int ni, bf16x8 (&rb)[2][2]) __attribute__((always_inline)) {
+        const char *img = buf + (2 + (wn >> 1)) * HALF;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++)
+                rb[i][kk] = *(const bf16x8 *)(img + off8((wn & 1) * 64 + ni * 32 + i * 16 + r16, kk * 4 + q));
+    };
+    auto mma = [&](int mi, int ni, const bf16x8 (&rb)[2][2]) __attribute__((always_inline)) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+                    acc[mi][ni][j][i] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[i][kk], ra[j][kk], acc[mi][ni][j][i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+    };
+
+    /* prologue: K-tile 0 (A, B) -> E, B of K-tile 1 -> O; K-tile 0 landed everywhere */
+    stage(0, 0);
+    stage(1, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(2, 1);
+    stage(3, 1);
+    vm_wait<4>();
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier(); /* the stagger */
+
+    for (int e = 0; e < KT; e += 2) {
+        const int o = e + 1;
+        const bool ne = e + 2 < KT, no = o + 2 < KT;
+        const char *bE = lds + (e & 1) * KBUF, *bO = lds + (o & 1) * KBUF;
+        /* P1 */
+        read_a(bE, 0);
+        read_b(bE, 0, rb0);
+        stage(0, o);
+        stage(1, o);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 0, rb0);
+        /* P2 */
+        read_b(bE, 1, rb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 1, rb1);
+        /* P3 */
+        read_a(bE, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 1, rb1);
+        /* P4: restage E's B for K-tile e+2; K-tile o complete */
+        if (ne) {
+            stage(2, e + 2);
+            stage(3, e + 2);
+            vm_wait<4>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 0, rb0);
+        /* P5 */
+        read_a(bO, 0);
+        read_b(bO, 0, rb0);
+        if (ne) {
+            stage(0, e + 2);
+            stage(1, e + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 0, rb0);
+        /* P6 */
+        read_b(bO, 1, rb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 1, rb1);
+        /* P7 */
+        read_a(bO, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 1, rb1);
+        /* P8: restage O's B for K-tile o+2; K-tile e+2 complete */
+        if (no) {
+            stage(2, o + 2);
+            stage(3, o + 2);
+            vm_wait<4>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 0, rb0);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier(); /* pair the stagger barrier */
+
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+        for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int b = m0 + wm * 128 + mi * 64 + j * 16 + r16;
+                    const int f = n0 + wn * 64 + ni * 32 + i * 16 + 4 * q;
+                    f32x4 v = acc[mi][ni][j][i];
+                    if constexpr (EPI == HPNN_EPI_ACT) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) v[r] = hpnn::bipolar(v[r]);
+                    } else if constexpr (EPI == HPNN_EPI_DACT) {
+                        const bf16x4 h = *(const bf16x4 *)(aux + (size_t)b * ldaux + f);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float y = (float)h[r];
+                            v[r] *= -0.5f * (y * y - 1.0f);
+                        }
+                    }
+                    if constexpr (CF32) {
+                        *(f32x4 *)((float *)C + (size_t)b * ldc + f) = v;
+                    } else {
+                        bf16x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) o[r] = (__bf16)v[r];
+                        *(bf16x4 *)((__bf16 *)C + (size_t)b * ldc + f) = o;
+                    }
+                }
+}
+
+template <int EPI, bool CF32>
+int launch8(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M, int N,
+            int K, hipStream_t s) {
+    const int tiles_n = N / 256, ntiles = (M / 256) * tiles_n;
+    hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32>), dim3(ntiles), dim3(512), 0, s, (const __bf16 *)A, lda,
+                       (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n, ntiles);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace
+
+extern "C" int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
+                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 128) return -1;
+    if (lda % 8 || ldb % 8 || ldc % 4 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return -1;
+    if ((size_t)lda * 2 * 256 >= (1u << 31) || (size_t)ldb * 2 * 256 >= (1u << 31)) return -1; /* 32-bit offsets */
+    if (epi == HPNN_EPI_DACT && (!aux || ldaux % 4)) return -1;
+    if (c_f32) {
+        if (epi == HPNN_EPI_NONE) return launch8<HPNN_EPI_NONE, true>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+        if (epi == HPNN_EPI_ACT) return launch8<HPNN_EPI_ACT, true>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+        return launch8<HPNN_EPI_DACT, true>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+    }
+    if (epi == HPNN_EPI_NONE) return launch8<HPNN_EPI_NONE, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+    if (epi == HPNN_EPI_ACT) return launch8<HPNN_EPI_ACT, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+    return launch8<HPNN_EPI_DACT, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+}

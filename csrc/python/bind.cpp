@@ -62,6 +62,15 @@ PYBIND11_MODULE(_native, m) {
                                     B, n_valid, n_out, type, S(stream)),
                   "output_delta");
         });
+    m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
+    m.def(
+        "gemm_nt8_bf16",
+        [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M, int N, int K, int epi,
+           int c_f32, uptr stream) {
+            check(hpnn_gemm_nt8_bf16(P(A), lda, P(B), ldb, P(C), ldc, P(aux), ldaux, M, N, K, epi, c_f32, S(stream)),
+                  "gemm_nt8_bf16");
+        },
+        "C = epi(A . B^T), bf16 MFMA");
     m.def("reduce_slabs", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
         check(hpnn_reduce_slabs((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)), "reduce_slabs");
     });

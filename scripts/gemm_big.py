@@ -41,15 +41,20 @@ def main():
     dx = torch.empty(B, K, dtype=torch.bfloat16, device=dev)
     fl = 2.0 * B * N * K
     res = {}
-    res["nt_fwd_act"] = t(lambda: ops.gemm_nt(X, W, ops.EPI_ACT, out=out))
-    res["nt_bwd_dact"] = t(lambda: ops.gemm_nt(D, Wt, ops.EPI_DACT, aux=X, out=dx))
+    from hpnn_amd._lib import native
+    for rnd in range(2):  # interleaved A/B in one process: 1-phase vs 8-phase 256x256 NT kernel
+        for mode, tag in ((0, "1ph"), (1, "8ph")):
+            native().gemm_nt_set_8ph(mode)
+            res[f"nt_fwd_act_{tag}_r{rnd}"] = t(lambda: ops.gemm_nt(X, W, ops.EPI_ACT, out=out))
+            res[f"nt_bwd_dact_{tag}_r{rnd}"] = t(lambda: ops.gemm_nt(D, Wt, ops.EPI_DACT, aux=X, out=dx))
+    native().gemm_nt_set_8ph(1)
     S = 1
     slab = torch.empty(S, N, K, dtype=torch.float32, device=dev)
     res["tn_grad"] = t(lambda: ops.gemm_tn(D, X, splits=S, out=slab))
     res["torch_mm_nt"] = t(lambda: torch.matmul(X, W.t()))
     res["torch_mm_tn"] = t(lambda: torch.matmul(D.t(), X))
     for k, v in res.items():
-        print(f"{k:14s} {v:9.1f} us  {fl / v / 1e6:8.1f} TFLOP/s")
+        print(f"{k:22s} {v:9.1f} us  {fl / v / 1e6:8.1f} TFLOP/s")
 
 
 if __name__ == "__main__":

@@ -71,6 +71,39 @@ def test_gemm_nt_big_tile(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 384), (256, 1024, 1152),
+                                   (2304, 256, 640)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nt8(gpu, M, N, K, epi):
+    """the 8-phase 256x256 kernel (kernels_nt8.hip) called directly at small grids: one
+    iteration (K = 128, no restaging), odd iteration counts, a ragged XCD split (9 tiles),
+    padded row strides on every operand"""
+    from hpnn_amd._lib import native
+    torch.manual_seed(M + 3 * N + K + epi)
+    A = _rand(M, K + 64).bfloat16()[:, :K]
+    B = (_rand(N, K + 32) + torch.arange(N, device="cuda")[:, None] * 0.001).bfloat16()[:, :K]
+    aux = _rand(M, N + 32).bfloat16()[:, :N] if epi == ops.EPI_DACT else None
+    for f32 in (False, True):
+        C = torch.full((M, N + 64), float("nan"), dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")[:, :N]
+        native().gemm_nt8_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                               aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+                               M, N, K, epi, int(f32), torch.cuda.current_stream().cuda_stream)
+        R = ops.ref_gemm_nt(A, B, epi, aux)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (C.float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+
+
+def test_gemm_nt8_rejects_bad_shapes(gpu):
+    from hpnn_amd._lib import native
+    A = torch.zeros(256, 192, dtype=torch.bfloat16, device="cuda")
+    C = torch.zeros(256, 256, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(RuntimeError):
+        native().gemm_nt8_bf16(A.data_ptr(), 192, A.data_ptr(), 192, C.data_ptr(), 256, 0, 0, 256, 256, 192,
+                               ops.EPI_NONE, 0, torch.cuda.current_stream().cuda_stream)
+
+
 def test_gemm_nt_identity(gpu):
     """A = I checks the C layout with an asymmetric B (cdna guide section 3)."""
     M, N, K = 128, 64, 128
