@@ -42,10 +42,11 @@ int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, i
                       hipStream_t stream);
 
 /* weight-stationary variant for N <= 128, K in {512, 800, 1024}: returns 1 if no instance */
-/* the same product on the 8-phase 256x256-tile kernel (kernels_nt8.hip): M % 256 == 0,
+/* the same product on the 8-phase 256x256-tile kernel (kernels_8ph.hip): M % 256 == 0,
  * N % 256 == 0, K % 128 == 0, else -1.  hpnn_gemm_nt_bf16 routes large GEMMs here when
  * HPNN_NT_8PH is not 0. */
 void hpnn_gemm_nt_set_8ph(int on);
+void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
                        int M, int N, int K, int epi, int c_f32, hipStream_t stream);
 int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C, int ldc, int M, int N, int K,

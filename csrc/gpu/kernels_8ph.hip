@@ -240,6 +240,208 @@ __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict_
                 }
 }
 
+/* ---------------------------------------------------------------------- */
+/* TN: slab[s][n][m] = sum over the batch rows b of split s of D[b][n] H[b][m] */
+/* ---------------------------------------------------------------------- */
+/* The weight-gradient GEMM on the same 8-phase schedule.  The operands stay sample-major:
+ * a half-tile is 64 batch rows x 128 columns of H (m) or D (n), kept as a T32 image
+ * (mfma_common.h: 4 sub-tiles of [64][32], 64-byte rows, chunk permutation) and read
+ * column-wise with ds_read_b64_tr_b16 (frag_tr), so nothing is transposed in memory.
+ * Wave (wm, wn): m in [128 wm, +128) (H half wm), n in [64 wn, +64) (D half wn / 2);
+ * quadrant (mi, ni) = 4 H fragments x 2 D fragments x 2 k-substeps = 16 MFMAs.
+ * Split s covers the 64-row units [s U / S, (s + 1) U / S); every split must hold an even
+ * number of units (two K-tiles per iteration).  Appended workgroups run the TnTail
+ * reduction, as in gemm_tn_pipe_kernel. */
+__global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict__ D, int ldd,
+                                                       const __bf16 *__restrict__ H, int ldh,
+                                                       float *__restrict__ slab, int ldg, int N, int units,
+                                                       int splits, int tiles_n, int ntiles, hpnn::TnTail tail) {
+    if ((int)blockIdx.x >= ntiles * splits) {
+        if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - ntiles * splits);
+        return;
+    }
+    __shared__ __attribute__((aligned(16))) char lds[2 * KBUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int tile, split;
+    if (splits == 1) {
+        const int bid = blockIdx.x, xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+        tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        split = 0;
+    } else {
+        tile = blockIdx.x % ntiles;
+        split = blockIdx.x / ntiles;
+    }
+    const int tn = tile % tiles_n, tm = tile / tiles_n;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int u0 = (int)((long)split * units / splits), u1 = (int)((long)(split + 1) * units / splits);
+    const int KT = u1 - u0; /* 64-row K-tiles, even */
+    const size_t ldh_b = (size_t)ldh * 2, ldd_b = (size_t)ldd * 2;
+    const char *Hg = (const char *)(H + (size_t)u0 * 64 * ldh + m0);
+    const char *Dg = (const char *)(D + (size_t)u0 * 64 * ldd + n0);
+
+    unsigned int voh[2], vod[2];
+    int dsto[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int pc = wave * 2 + i, sub = pc >> 2, rp = (pc & 3) * 16;
+        const int r = rp + (lane >> 2), col = sub * 32 + (((lane & 3) ^ hpnn::t32_g(r)) & 3) * 8;
+        voh[i] = (unsigned int)(r * ldh_b + col * 2);
+        vod[i] = (unsigned int)(r * ldd_b + col * 2);
+        dsto[i] = sub * 4096 + rp * 64;
+    }
+    auto stage = [&](int h, int kt) __attribute__((always_inline)) {
+        char *dst = lds + (kt & 1) * KBUF + h * HALF;
+        const char *g = h < 2 ? Hg + (size_t)kt * 64 * ldh_b + h * 256 : Dg + (size_t)kt * 64 * ldd_b + (h - 2) * 256;
+#pragma unroll
+        for (int i = 0; i < 2; i++) hpnn::glds16_sv(g, h < 2 ? voh[i] : vod[i], dst + dsto[i]);
+    };
+
+    f32x4 acc[2][2][4][2]; /* [mi][ni][i: H frag][j: D frag] */
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    /* transposed fragment reads (hpnn::frag_tr on a T32 image with 64 rows), addresses
+     * split into a per-lane part -- it depends only on whether the fragment's first column
+     * is 0 or 16 mod 32 and on the low / high 4-row group -- and a compile-time constant
+     * (sub-tile, k-substep, buffer, half) folded into the ds_read offset */
+    int toff[2][2];
+    {
+        const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+        for (int cls = 0; cls < 2; cls++)
+#pragma unroll
+            for (int hl = 0; hl < 2; hl++) {
+                const int r = 8 * g + qq + 4 * hl;
+                toff[cls][hl] = r * 64 + ((((2 * cls + (p >> 1)) ^ hpnn::t32_g(r)) & 3) << 4) + (p & 1) * 8;
+            }
+    }
+    auto ftr = [&](const char *img, int kbase, int c0) __attribute__((always_inline)) {
+        const char *b = img + (c0 >> 5) * 4096 + kbase * 64;
+        const int cls = (c0 >> 4) & 1;
+        hpnn::s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((hpnn::lds_s16x4 *)(b + toff[cls][0]));
+        hpnn::s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((hpnn::lds_s16x4 *)(b + toff[cls][1]));
+        hpnn::s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    bf16x8 rh[4][2], rd0[2][2], rd1[2][2];
+    auto read_h = [&](const char *buf, int mi) __attribute__((always_inline)) {
+        const char *img = buf + wm * HALF;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) rh[i][kk] = ftr(img, kk * 32, mi * 64 + i * 16);
+    };
+    auto read_d = [&](const char *buf, int ni, bf16x8 (&rd)[2][2]) __attribute__((always_inline)) {
+        const char *img = buf + (2 + (wn >> 1)) * HALF;
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) rd[j][kk] = ftr(img, kk * 32, (wn & 1) * 64 + ni * 32 + j * 16);
+    };
+    auto mma = [&](int mi, int ni, const bf16x8 (&rd)[2][2]) __attribute__((always_inline)) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    acc[mi][ni][i][j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh[i][kk], rd[j][kk], acc[mi][ni][i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+    };
+
+    /* the schedule of gemm_nt8_kernel with H in the role of A and D in that of B */
+    stage(0, 0);
+    stage(1, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(2, 1);
+    stage(3, 1);
+    vm_wait<4>();
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+
+    for (int e = 0; e < KT; e += 2) {
+        const int o = e + 1;
+        const bool ne = e + 2 < KT, no = o + 2 < KT;
+        const char *bE = lds + (e & 1) * KBUF, *bO = lds + (o & 1) * KBUF;
+        read_h(bE, 0);
+        read_d(bE, 0, rd0);
+        stage(0, o);
+        stage(1, o);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 0, rd0);
+        read_d(bE, 1, rd1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 1, rd1);
+        read_h(bE, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 1, rd1);
+        if (ne) {
+            stage(2, e + 2);
+            stage(3, e + 2);
+            vm_wait<4>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 0, rd0);
+        read_h(bO, 0);
+        read_d(bO, 0, rd0);
+        if (ne) {
+            stage(0, e + 2);
+            stage(1, e + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 0, rd0);
+        read_d(bO, 1, rd1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0, 1, rd1);
+        read_h(bO, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 1, rd1);
+        if (no) {
+            stage(2, o + 2);
+            stage(3, o + 2);
+            vm_wait<4>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1, 0, rd0);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+
+    float *out = slab + (size_t)split * N * ldg;
+    const int r16 = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+        for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
+                    const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                    *(f32x4 *)(out + (size_t)n * ldg + m) = acc[mi][ni][i][j];
+                }
+}
+
 template <int EPI, bool CF32>
 int launch8(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M, int N,
             int K, hipStream_t s) {
@@ -265,4 +467,17 @@ extern "C" int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb
     if (epi == HPNN_EPI_NONE) return launch8<HPNN_EPI_NONE, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
     if (epi == HPNN_EPI_ACT) return launch8<HPNN_EPI_ACT, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
     return launch8<HPNN_EPI_DACT, false>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, stream);
+}
+
+/* TN entry for gemm_tn_dispatch (kernels_mfma.hip): -1 when the shape does not fit */
+int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
+                         int splits, hipStream_t stream, const hpnn::TnTail &tail) {
+    if (N % 256 || M % 256 || Bt % 128 || splits < 1 || ldd % 8 || ldh % 8 || ldg % 4) return -1;
+    const int units = Bt / 64;
+    if (units % splits || (units / splits) % 2) return -1;
+    if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
+    const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
+    hipLaunchKernelGGL(gemm_tn8_kernel, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream, (const __bf16 *)D,
+                       ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles, tail);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }

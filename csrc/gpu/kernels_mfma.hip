@@ -35,6 +35,10 @@
 #include "kernels.h"
 #include "mfma_common.h"
 
+/* kernels_8ph.hip */
+int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt,
+                         int splits, hipStream_t stream, const hpnn::TnTail &tail);
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -356,9 +360,11 @@ int launch_nt_big(const void *A, int lda, const void *B, int ldb, void *C, int l
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-/* large NT GEMMs on the 8-phase kernel (kernels_nt8.hip); HPNN_NT_8PH=0 keeps the 1-phase
+/* large NT GEMMs on the 8-phase kernel (kernels_8ph.hip); HPNN_NT_8PH=0 keeps the 1-phase
  * 256x256 kernel, hpnn_gemm_nt_set_8ph() switches at run time (A/B benchmarks) */
 int g_nt8 = [] { const char *e = getenv("HPNN_NT_8PH"); return !(e && e[0] == '0'); }();
+/* large weight gradients on the 8-phase TN kernel (HPNN_TN_8PH=0 keeps the 4-stage kernel) */
+int g_tn8 = [] { const char *e = getenv("HPNN_TN_8PH"); return !(e && e[0] == '0'); }();
 
 template <int EPI, bool CF32>
 int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
@@ -457,8 +463,13 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
     if (N % 32 || M % 32 || Bt % 64 || splits > Bt / 64) return -2;
     if (ldd % 8 || ldh % 8 || ldg % 4 || ldg < M) return -3;
     static const int big_off = [] { const char *e = getenv("HPNN_TN_BIG"); return e && e[0] == '0'; }();
-    if (!big_off && N % 256 == 0 && M % 256 == 0 && (long)(N / 256) * (M / 256) * splits >= 256)
+    if (!big_off && N % 256 == 0 && M % 256 == 0 && (long)(N / 256) * (M / 256) * splits >= 256) {
+        if (g_tn8) {
+            const int rc = hpnn_gemm_tn8_launch(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+            if (rc != -1) return rc;
+        }
         return launch_tn_big(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
+    }
     if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
@@ -469,6 +480,7 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
 }  // namespace
 
 extern "C" void hpnn_gemm_nt_set_8ph(int on) { g_nt8 = on ? 1 : 0; }
+extern "C" void hpnn_gemm_tn_set_8ph(int on) { g_tn8 = on ? 1 : 0; }
 
 extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {

@@ -63,6 +63,7 @@ PYBIND11_MODULE(_native, m) {
                   "output_delta");
         });
     m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
+    m.def("gemm_tn_set_8ph", [](int on) { hpnn_gemm_tn_set_8ph(on); });
     m.def(
         "gemm_nt8_bf16",
         [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M, int N, int K, int epi,

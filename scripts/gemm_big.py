@@ -50,7 +50,11 @@ def main():
     native().gemm_nt_set_8ph(1)
     S = 1
     slab = torch.empty(S, N, K, dtype=torch.float32, device=dev)
-    res["tn_grad"] = t(lambda: ops.gemm_tn(D, X, splits=S, out=slab))
+    for rnd in range(2):
+        for mode, tag in ((0, "4st"), (1, "8ph")):
+            native().gemm_tn_set_8ph(mode)
+            res[f"tn_grad_{tag}_r{rnd}"] = t(lambda: ops.gemm_tn(D, X, splits=S, out=slab))
+    native().gemm_tn_set_8ph(1)
     res["torch_mm_nt"] = t(lambda: torch.matmul(X, W.t()))
     res["torch_mm_tn"] = t(lambda: torch.matmul(D.t(), X))
     for k, v in res.items():

@@ -75,7 +75,7 @@ def test_gemm_nt_big_tile(gpu, M, N, K, epi):
                                    (2304, 256, 640)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
 def test_gemm_nt8(gpu, M, N, K, epi):
-    """the 8-phase 256x256 kernel (kernels_nt8.hip) called directly at small grids: one
+    """the 8-phase 256x256 kernel (kernels_8ph.hip) called directly at small grids: one
     iteration (K = 128, no restaging), odd iteration counts, a ragged XCD split (9 tiles),
     padded row strides on every operand"""
     from hpnn_amd._lib import native
@@ -139,9 +139,13 @@ def test_gemm_tn(gpu, Bt, N, M, S):
     assert (slab[0] - R0).abs().max().item() <= 1e-3 * R0.abs().max().item() + 1e-4
 
 
-@pytest.mark.parametrize("Bt,N,M,S", [(1024, 4096, 4096, 1), (2048, 2048, 4096, 2), (640, 4096, 2048, 3)])
+@pytest.mark.parametrize("Bt,N,M,S", [(1024, 4096, 4096, 1), (2048, 2048, 4096, 2), (640, 4096, 2048, 3),
+                                      (128, 4096, 4096, 1), (512, 2048, 2048, 4), (384, 4096, 4096, 1)])
 def test_gemm_tn_big_tile(gpu, Bt, N, M, S):
-    """>= 256 tiles of 256x256 take the 8-wave large-tile kernel; padded strides, uneven splits"""
+    """>= 256 tiles of 256x256 take the large-tile kernels: the 8-phase one (kernels_8ph.hip)
+    when every split holds an even number of 64-row units (one iteration: Bt = 128 and
+    the 4-split case; several: Bt = 1024, 2048), else the 4-stage 8-wave kernel (640 / 3,
+    384 = 6 units is even -> 8-phase with 3 iterations); padded strides, uneven splits"""
     torch.manual_seed(Bt + N + M)
     D = (_rand(Bt, N + 32) + torch.arange(N + 32, device="cuda")[None, :] * 0.001).bfloat16()[:, :N]
     H = _rand(Bt, M + 64).bfloat16()[:, :M]
