@@ -298,6 +298,14 @@ int pick_splits(int Np, int Kp, int Bp) {
         const int m = Bp / 64;
         return forced < m ? forced : (m > 0 ? m : 1);
     }
+    /* 256x256 tiles: enough splits for the 8-phase TN kernel (>= 256 workgroups, an even
+     * number of 64-row units per split), as MLP._splits_8ph */
+    static const int tn8 = [] { const char *e = getenv("HPNN_TN_8PH"); return !(e && e[0] == '0'); }();
+    if (tn8 && Np % 256 == 0 && Kp % 256 == 0 && Bp % 128 == 0) {
+        const int t8 = (Np / 256) * (Kp / 256), units = Bp / 64, s0 = (256 + t8 - 1) / t8;
+        for (int s8 = s0; s8 <= 2 * s0; s8++)
+            if (units % s8 == 0 && (units / s8) % 2 == 0) return s8;
+    }
     int s = (256 + tiles / 2) / (tiles > 0 ? tiles : 1);
     const int maxs = Bp / 512;
     if (s > maxs) s = maxs;

@@ -45,6 +45,10 @@ int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, i
 /* the same product on the 8-phase 256x256-tile kernel (kernels_8ph.hip): M % 256 == 0,
  * N % 256 == 0, K % 128 == 0, else -1.  hpnn_gemm_nt_bf16 routes large GEMMs here when
  * HPNN_NT_8PH is not 0. */
+/* split-K form of the same (S FP32 slabs in a library workspace, then one epilogue pass):
+ * M % 256 == 0, N % 256 == 0, K % (128 S) == 0; -1 when it does not apply */
+int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
+                              int ldaux, int M, int N, int K, int epi, int c_f32, int splits, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,

@@ -35,6 +35,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "kernels.h"
 #include "mfma_common.h"
 
@@ -59,20 +61,25 @@ template <int EPI, bool CF32>
 __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict__ A, int lda,
                                                        const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
                                                        int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
-                                                       int tiles_n, int ntiles) {
+                                                       int tiles_n, int ntiles, int splits, long cstride) {
     __shared__ __attribute__((aligned(16))) char lds[2 * KBUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3; /* wm = stagger group */
     /* XCD-aware, bijective: blocks b, b+8, b+16, ... (one XCD) take consecutive tiles */
-    const int bid = blockIdx.x, xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int total = ntiles * splits;
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
+    const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    /* split-K (splits > 1, EPI_NONE into FP32 slabs cstride floats apart): split s takes
+     * K-tiles [s KT, (s + 1) KT) */
+    const int tile = w % ntiles, split = w / ntiles;
     const int tm = tile / tiles_n, tn = tile % tiles_n;
     const int m0 = tm * 256, n0 = tn * 256;
-    const int KT = K / 64;
+    const int KT = K / 64 / splits;
     const size_t lda_b = (size_t)lda * 2, ldb_b = (size_t)ldb * 2;
-    const char *Ag = (const char *)(A + (size_t)m0 * lda);
-    const char *Bg = (const char *)(B + (size_t)n0 * ldb);
+    const char *Ag = (const char *)(A + (size_t)m0 * lda + (size_t)split * KT * 64);
+    const char *Bg = (const char *)(B + (size_t)n0 * ldb + (size_t)split * KT * 64);
+    if (splits > 1) C = (void *)((float *)C + (size_t)split * cstride);
 
     /* LDS-DMA of half-tile h (0,1: A rows 128h..; 2,3: B rows 128(h-2)..) of K-tile kt
      * into buffer kt & 1: 16 pieces of 8 rows, two per wave; wave-uniform base in SGPRs,
@@ -444,11 +451,77 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 
 template <int EPI, bool CF32>
 int launch8(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M, int N,
-            int K, hipStream_t s) {
+            int K, hipStream_t s, int splits = 1, long cstride = 0) {
     const int tiles_n = N / 256, ntiles = (M / 256) * tiles_n;
-    hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32>), dim3(ntiles), dim3(512), 0, s, (const __bf16 *)A, lda,
-                       (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n, ntiles);
+    hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32>), dim3(ntiles * splits), dim3(512), 0, s, (const __bf16 *)A, lda,
+                       (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n, ntiles, splits,
+                       cstride);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* C = epi(sum over S FP32 slabs [M][N] of the split-K GEMM), 4 consecutive columns per thread */
+template <int EPI, bool CF32>
+__global__ __launch_bounds__(256) void nt_splitk_epi_kernel(const float *__restrict__ P, int S, long cstride, int M,
+                                                            int N, const __bf16 *__restrict__ aux, int ldaux,
+                                                            void *__restrict__ C, int ldc) {
+    const long n4 = (long)M * N / 4;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
+        const int b = (int)(e * 4 / N), f = (int)(e * 4 % N);
+        f32x4 v = ((const f32x4 *)P)[e];
+        for (int s = 1; s < S; s++) v += ((const f32x4 *)(P + (size_t)s * cstride))[e];
+        if constexpr (EPI == HPNN_EPI_ACT) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = hpnn::bipolar(v[r]);
+        } else if constexpr (EPI == HPNN_EPI_DACT) {
+            const bf16x4 h = *(const bf16x4 *)(aux + (size_t)b * ldaux + f);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float y = (float)h[r];
+                v[r] *= -0.5f * (y * y - 1.0f);
+            }
+        }
+        if constexpr (CF32) {
+            *(f32x4 *)((float *)C + (size_t)b * ldc + f) = v;
+        } else {
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; r++) o[r] = (__bf16)v[r];
+            *(bf16x4 *)((__bf16 *)C + (size_t)b * ldc + f) = o;
+        }
+    }
+}
+
+template <int EPI, bool CF32>
+int splitk_epi(const float *P, int S, long cstride, int M, int N, const void *aux, int ldaux, void *C, int ldc,
+               hipStream_t s) {
+    const long n4 = (long)M * N / 4;
+    const int blocks = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
+    hipLaunchKernelGGL((nt_splitk_epi_kernel<EPI, CF32>), dim3(blocks), dim3(256), 0, s, P, S, cstride, M, N,
+                       (const __bf16 *)aux, ldaux, C, ldc);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* split-K workspace, one per device (train_nn -G drives several GPUs from one process, one
+ * host thread each): grown outside stream capture only -- a capture that would need a
+ * bigger one gets -1 and the caller takes another kernel */
+constexpr int WS_DEV = 64;
+float *g_ws[WS_DEV] = {};
+size_t g_ws_bytes[WS_DEV] = {};
+std::mutex g_ws_mu;
+float *splitk_ws(size_t bytes, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WS_DEV) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if (bytes <= g_ws_bytes[dev]) return g_ws[dev];
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr; /* the old buffer may be in use */
+    if (g_ws[dev]) hipFree(g_ws[dev]);
+    g_ws[dev] = nullptr;
+    g_ws_bytes[dev] = 0;
+    if (hipMalloc((void **)&g_ws[dev], bytes) != hipSuccess) return nullptr;
+    g_ws_bytes[dev] = bytes;
+    return g_ws[dev];
 }
 
 }  // namespace
@@ -480,4 +553,32 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     hipLaunchKernelGGL(gemm_tn8_kernel, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream, (const __bf16 *)D,
                        ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* split-K form for GEMMs with too few 256x256 tiles to fill the chip (the RRUFF-shaped
+ * first layer, 16384 x 256 x 4096: 64 tiles): S splits into FP32 slabs, then one
+ * elementwise pass sums them and applies the epilogue.  -1: shape / workspace not
+ * available (the caller keeps its other kernels). */
+extern "C" int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc,
+                                         const void *aux, int ldaux, int M, int N, int K, int epi, int c_f32,
+                                         int splits, hipStream_t stream) {
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || splits < 2 || K % (128 * splits)) return -1;
+    if (lda % 8 || ldb % 8 || ldc % 4 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return -1;
+    if ((size_t)lda * 2 * 256 >= (1u << 31) || (size_t)ldb * 2 * 256 >= (1u << 31)) return -1;
+    if (epi == HPNN_EPI_DACT && (!aux || ldaux % 4)) return -1;
+    const long cstride = (long)M * N;
+    float *P = splitk_ws((size_t)splits * cstride * 4, stream);
+    if (!P) return -1;
+    int rc = launch8<HPNN_EPI_NONE, true>(A, lda, B, ldb, P, N, nullptr, 0, M, N, K, stream, splits, cstride);
+    if (rc) return rc;
+#define HPNN_SKE(E_, F_) return splitk_epi<E_, F_>(P, splits, cstride, M, N, aux, ldaux, C, ldc, stream)
+    if (c_f32) {
+        if (epi == HPNN_EPI_NONE) HPNN_SKE(HPNN_EPI_NONE, true);
+        if (epi == HPNN_EPI_ACT) HPNN_SKE(HPNN_EPI_ACT, true);
+        HPNN_SKE(HPNN_EPI_DACT, true);
+    }
+    if (epi == HPNN_EPI_NONE) HPNN_SKE(HPNN_EPI_NONE, false);
+    if (epi == HPNN_EPI_ACT) HPNN_SKE(HPNN_EPI_ACT, false);
+    HPNN_SKE(HPNN_EPI_DACT, false);
+#undef HPNN_SKE
 }

@@ -374,6 +374,20 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
     if (!big_off && g_nt8 && K % 128 == 0 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 &&
         K >= 512)
         return hpnn_gemm_nt8_bf16(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, EPI, CF32 ? 1 : 0, s);
+    /* fewer 256x256 tiles than CUs but a long K: split-K on the 8-phase kernel.  Opt-in
+     * (HPNN_NT_SPLITK=1): measured slower on the RRUFF-shaped first layer (16384 x 256 x
+     * 4096, 4 splits: 168-169 vs 160 us per step with the 128x128 kernel,
+     * scripts/gpu_splitk.sh) -- the 67 MB of FP32 slabs cost more than the idle CUs */
+    static const int splitk = [] { const char *e = getenv("HPNN_NT_SPLITK"); return e && e[0] == '1'; }();
+    if (splitk && !big_off && g_nt8 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 32) {
+        const long t8 = (long)(M / 256) * (N / 256);
+        const int S = (int)((256 + t8 - 1) / t8);
+        if (S >= 2 && S <= 8 && K % (128 * S) == 0 && K / S >= 512) {
+            const int rc = hpnn_gemm_nt8_splitk_bf16(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, EPI, CF32 ? 1 : 0,
+                                                     S, s);
+            if (rc != -1) return rc;
+        }
+    }
     if (!big_off && k64 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 && K >= 512)
         return launch_nt_big<EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s);
 #define HPNN_NT(BN_)                                                                                  \

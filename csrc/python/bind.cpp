@@ -63,6 +63,12 @@ PYBIND11_MODULE(_native, m) {
                   "output_delta");
         });
     m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
+    m.def("gemm_nt8_splitk_bf16", [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M,
+                                     int N, int K, int epi, int c_f32, int splits, uptr stream) {
+        check(hpnn_gemm_nt8_splitk_bf16(P(A), lda, P(B), ldb, P(C), ldc, P(aux), ldaux, M, N, K, epi, c_f32, splits,
+                                        S(stream)),
+              "gemm_nt8_splitk_bf16");
+    });
     m.def("gemm_tn_set_8ph", [](int on) { hpnn_gemm_tn_set_8ph(on); });
     m.def(
         "gemm_nt8_bf16",

@@ -167,12 +167,29 @@ class MLP:
         forced = int(os.environ.get("HPNN_TN_SPLITS", "0"))
         if forced > 0:
             return max(1, min(forced, Bp // 64)) if Bp % 64 == 0 else 1
+        s8 = MLP._splits_8ph(N, K, Bp)
+        if s8:
+            return s8
         rows = int(os.environ.get("HPNN_TN_ROWS", "512"))
         s = (256 + tiles // 2) // max(tiles, 1)
         s = min(s, Bp // rows)
         if s >= 8:
             s -= s % 8
         return max(1, s)
+
+    @staticmethod
+    def _splits_8ph(N, K, Bp):
+        """split count that puts a weight gradient with 256x256 tiles on the 8-phase TN kernel
+        (kernels_8ph.hip: >= 256 workgroups, an even number of 64-row units per split), or 0.
+        RRUFF-shaped 4096 -> 256 first layer over 16384 rows: 16 splits, 162-164 us/step vs
+        171-173 with 4 splits on the 128x128 kernel (scripts/gpu_rruff_splits.sh)."""
+        if N % 256 or K % 256 or Bp % 128 or os.environ.get("HPNN_TN_8PH", "1") == "0":
+            return 0
+        t8, units = (N // 256) * (K // 256), Bp // 64
+        for s in range(max(1, -(-256 // t8)), 2 * max(1, -(-256 // t8)) + 1):
+            if units % s == 0 and (units // s) % 2 == 0:
+                return s
+        return 0
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:

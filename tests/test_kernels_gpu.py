@@ -52,10 +52,13 @@ def test_gemm_nt_weight_stationary(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 4096, 512), (8192, 2048, 640), (4352, 4096, 576)])
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 512), (8192, 2048, 640), (4352, 4096, 576), (16384, 256, 2048),
+                                   (4096, 1024, 4096)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
 def test_gemm_nt_big_tile(gpu, M, N, K, epi):
-    """shapes with >= 256 tiles of 256x256 take the 8-wave large-tile kernel (128 KiB ring);
+    """shapes with >= 256 tiles of 256x256 take the 8-phase kernel (K % 128 == 0) or the
+    1-phase large-tile kernel (K = 576); 64 tiles with a long K (16384 x 256 x 2048,
+    4096 x 1024 x 4096) take the 128x128 kernel (the split-K form with HPNN_NT_SPLITK=1);
     padded row strides on every operand"""
     torch.manual_seed(M + N + K + epi)
     A = _rand(M, K + 64).bfloat16()[:, :K]
@@ -88,6 +91,27 @@ def test_gemm_nt8(gpu, M, N, K, epi):
         native().gemm_nt8_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
                                aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                                M, N, K, epi, int(f32), torch.cuda.current_stream().cuda_stream)
+        R = ops.ref_gemm_nt(A, B, epi, aux)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (C.float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(512, 256, 1024, 2), (256, 512, 768, 3), (1024, 256, 4096, 8), (256, 256, 256, 2)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nt8_splitk(gpu, M, N, K, S, epi):
+    """split-K form (FP32 slabs in the library workspace + one epilogue pass)"""
+    from hpnn_amd._lib import native
+    torch.manual_seed(M + N + K + S + epi)
+    A = _rand(M, K + 64).bfloat16()[:, :K]
+    B = (_rand(N, K + 32) + torch.arange(N, device="cuda")[:, None] * 0.001).bfloat16()[:, :K]
+    aux = _rand(M, N + 32).bfloat16()[:, :N] if epi == ops.EPI_DACT else None
+    for f32 in (False, True):
+        C = torch.full((M, N + 64), float("nan"), dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")[:, :N]
+        native().gemm_nt8_splitk_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                                      aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+                                      M, N, K, epi, int(f32), S, torch.cuda.current_stream().cuda_stream)
         R = ops.ref_gemm_nt(A, B, epi, aux)
         tol = 2e-2 if not f32 else 2e-3
         err = (C.float() - R).abs().max().item()
