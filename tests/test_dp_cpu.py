@@ -73,3 +73,17 @@ def test_bucket_plan():
     for b in dp.buckets:
         v = dp._bucket_view(b)
         assert v.numel() == sum(m.G[l].numel() for l in b)
+
+
+def test_split_counts_for_8phase_tn():
+    """weight gradients with 256x256 tiles get a split count the 8-phase TN kernel accepts
+    (>= 256 workgroups, an even number of 64-row units per split); others keep the
+    one-workgroup-per-CU rule (MNIST's G0: 48)"""
+    from hpnn_amd.models.mlp import MLP
+    assert MLP._pick_splits(256, 4096, 16384) == 16       # RRUFF-shaped first layer
+    assert MLP._pick_splits(4096, 4096, 8192) == 1        # synthetic 8x4096 ANN
+    assert MLP._pick_splits(128, 800, 65536) == 48        # MNIST G0 (not 256-divisible)
+    for N, K, B in [(256, 4096, 16384), (512, 2048, 8192), (4096, 4096, 1024)]:
+        s = MLP._splits_8ph(N, K, B)
+        assert s and (N // 256) * (K // 256) * s >= 256 and (B // 64) % s == 0 and (B // 64 // s) % 2 == 0
+    assert MLP._splits_8ph(256, 256, 16384) == 0          # 256 splits would leave 1 unit each
