@@ -49,6 +49,11 @@ int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, i
  * M % 256 == 0, N % 256 == 0, K % (128 S) == 0; -1 when it does not apply */
 int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                               int ldaux, int M, int N, int K, int epi, int c_f32, int splits, hipStream_t stream);
+/* weight gradient of one layer over the whole batch with the optimizer step fused into the
+ * 8-phase TN kernel's epilogue (no gradient in memory): the step of hpnn_sgd_update with one
+ * slab.  N % 256 == 0, M % 256 == 0, Bt % 128 == 0, else -1. */
+int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
+                         void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,

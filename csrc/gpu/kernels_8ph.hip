@@ -259,10 +259,21 @@ __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict_
  * Split s covers the 64-row units [s U / S, (s + 1) U / S); every split must hold an even
  * number of units (two K-tiles per iteration).  Appended workgroups run the TnTail
  * reduction, as in gemm_tn_pipe_kernel. */
+/* optimizer step fused into the TN epilogue (one split: the product is the whole gradient
+ * G[n][m]), the math of sgd_tile (kernels_misc.hip) with one slab */
+struct Tn8Upd {
+    float *W32, *V32;
+    __bf16 *Wb, *Wt;
+    float lr, alpha, scale;
+    int momentum;
+};
+
+template <bool UPD>
 __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict__ D, int ldd,
                                                        const __bf16 *__restrict__ H, int ldh,
                                                        float *__restrict__ slab, int ldg, int N, int units,
-                                                       int splits, int tiles_n, int ntiles, hpnn::TnTail tail) {
+                                                       int splits, int tiles_n, int ntiles, hpnn::TnTail tail,
+                                                       Tn8Upd upd) {
     if ((int)blockIdx.x >= ntiles * splits) {
         if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - ntiles * splits);
         return;
@@ -435,18 +446,73 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 
     float *out = slab + (size_t)split * N * ldg;
     const int r16 = lane & 15, q = lane >> 4;
+    if constexpr (UPD) {
+        /* W [N][ldg]: W32 / V32 / Wb row-major, Wt [ldg][N].  Per quadrant: all loads
+         * first (8 fragments in flight), then the step, then the stores -- a load / use /
+         * store chain per fragment would leave the epilogue latency-bound */
+        float *__restrict__ W32 = upd.W32;
+        float *__restrict__ V32 = upd.V32;
+        __bf16 *__restrict__ Wb = upd.Wb;
+        __bf16 *__restrict__ Wt = upd.Wt;
 #pragma unroll
-    for (int mi = 0; mi < 2; mi++)
+        for (int mi = 0; mi < 2; mi++)
 #pragma unroll
-        for (int ni = 0; ni < 2; ni++)
+            for (int ni = 0; ni < 2; ni++) {
+                f32x4 w[4][2], v[4][2];
 #pragma unroll
-            for (int i = 0; i < 4; i++)
+                for (int i = 0; i < 4; i++)
 #pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
-                    const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
-                    *(f32x4 *)(out + (size_t)n * ldg + m) = acc[mi][ni][i][j];
-                }
+                    for (int j = 0; j < 2; j++) {
+                        const size_t idx = (size_t)(n0 + wn * 64 + ni * 32 + j * 16 + r16) * ldg +
+                                           (m0 + wm * 128 + mi * 64 + i * 16 + 4 * q);
+                        w[i][j] = *(const f32x4 *)(W32 + idx);
+                        if (upd.momentum) v[i][j] = *(const f32x4 *)(V32 + idx);
+                    }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
+                        const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                        const size_t idx = (size_t)n * ldg + m;
+                        const f32x4 g = acc[mi][ni][i][j];
+                        f32x4 ww = w[i][j];
+                        if (upd.momentum) {
+                            f32x4 vv = v[i][j];
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                vv[r] += upd.lr * (g[r] * upd.scale);
+                                ww[r] += vv[r];
+                                vv[r] *= upd.alpha;
+                            }
+                            *(f32x4 *)(V32 + idx) = vv;
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; r++) ww[r] += upd.lr * (g[r] * upd.scale);
+                        }
+                        *(f32x4 *)(W32 + idx) = ww;
+                        bf16x4 wb;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) wb[r] = (__bf16)ww[r];
+                        *(bf16x4 *)(Wb + idx) = wb;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) Wt[(size_t)(m + r) * N + n] = wb[r];
+                    }
+            }
+    } else {
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
+                        const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                        *(f32x4 *)(out + (size_t)n * ldg + m) = acc[mi][ni][i][j];
+                    }
+    }
 }
 
 template <int EPI, bool CF32>
@@ -550,8 +616,26 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     if (units % splits || (units / splits) % 2) return -1;
     if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    hipLaunchKernelGGL(gemm_tn8_kernel, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream, (const __bf16 *)D,
-                       ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles, tail);
+    hipLaunchKernelGGL(gemm_tn8_kernel<false>, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream,
+                       (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles,
+                       tail, Tn8Upd{});
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* G = D^T H over the whole batch (one split) with the optimizer step applied in the
+ * epilogue: the gradient never goes to memory (saves its write and the update kernel's
+ * read of it, and the update launch).  W [N][M] FP32 master (+ V32 momentum), Wbf [N][M],
+ * Wt [M][N] BF16 copies, exactly the step of hpnn_sgd_update with one slab.  -1: shape
+ * not supported (256x256 tiles, an even number of 64-row units). */
+extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32,
+                                    float *V32, void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum,
+                                    hipStream_t stream) {
+    if (N % 256 || M % 256 || Bt % 128 || ldd % 8 || ldh % 8 || !W32 || !Wbf || !Wt || (momentum && !V32)) return -1;
+    if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
+    const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
+    const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum};
+    hipLaunchKernelGGL(gemm_tn8_kernel<true>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
+                       (const __bf16 *)H, ldh, nullptr, M, N, Bt / 64, 1, tiles_n, ntiles, hpnn::TnTail{}, u);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -63,6 +63,13 @@ PYBIND11_MODULE(_native, m) {
                   "output_delta");
         });
     m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
+    m.def("gemm_tn8_update", [](uptr D, int ldd, uptr H, int ldh, int N, int M, int Bt, uptr W32, uptr V32, uptr Wbf,
+                                uptr Wt, float lr, float alpha, float scale, int momentum, uptr stream) {
+        const int rc = hpnn_gemm_tn8_update(P(D), ldd, P(H), ldh, N, M, Bt, (float *)P(W32), (float *)P(V32), P(Wbf),
+                                            P(Wt), lr, alpha, scale, momentum, S(stream));
+        if (rc != -1) check(rc, "gemm_tn8_update");
+        return rc == 0;
+    });
     m.def("gemm_nt8_splitk_bf16", [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M,
                                      int N, int K, int epi, int c_f32, int splits, uptr stream) {
         check(hpnn_gemm_nt8_splitk_bf16(P(A), lda, P(B), ldb, P(C), ldc, P(aux), ldaux, M, N, K, epi, c_f32, splits,

@@ -91,6 +91,7 @@ class MLP:
         self.batch = batch
         self.Bp = ops.pad_to(batch, 128)
         self.momentum = momentum
+        self.tn_update = os.environ.get("HPNN_TN_UPD", "1") != "0"
         self.Kp = [ops.pad_to(sizes[l], 32) for l in range(self.L)]
         self.Np = [ops.pad_to(sizes[l + 1], 32) for l in range(self.L)]
         self.n_out = sizes[-1]
@@ -387,9 +388,21 @@ class MLP:
         self.output(labels=labels, T=T, n_valid=n_valid)
         for l in range(self.L - 1, -1, -1):
             if l > 0:
-                self.backward_layer(l)
+                self.backward_layer(l)  # pre-update W_l^T, before layer l's step below
+            Hin = X if l == 0 else self.H[l - 1]
+            if self._tn_update_ok(l) and ops.gemm_tn_update(self.D[l], Hin, self.W32[l], self.V32[l], self.Wb[l],
+                                                             self.Wt[l], lr, alpha, scale, self.momentum):
+                continue  # gradient + step in one launch, no gradient in memory
             self.grad_layer(l, X)
             self.update_layer(l, lr, alpha, scale)
+
+    def _tn_update_ok(self, l):
+        """layer l's weight gradient and optimizer step can run as one 8-phase TN launch
+        (ops.gemm_tn_update): one split, 256x256 tiles, no fragment-major W0 copy to keep;
+        tn_update=False (or HPNN_TN_UPD=0) keeps the separate gradient + update kernels.
+        Synthetic 8x4096 ANN: see profiles/r2/s5_8ph_gemm.md."""
+        return (self.tn_update and self.device.type == "cuda" and self.S[l] == 1 and self.Np[l] % 256 == 0
+                and self.Kp[l] % 256 == 0 and self.Bp % 128 == 0 and not (l == 0 and self.W0f is not None))
 
     def predict(self, X, n_valid=None):
         """network outputs [n_valid, n_out] (fp32)."""

@@ -75,6 +75,22 @@ def gemm_tn(D, H, splits=1, out=None):
     return out
 
 
+def gemm_tn_update(D, H, W32, V32, Wbf, Wt, lr, alpha=0.0, scale=1.0, momentum=False):
+    """G = D^T H over the whole batch with the optimizer step of sgd_update (one slab) fused
+    into the 8-phase TN kernel's epilogue (csrc/gpu/kernels_8ph.hip): the gradient never
+    reaches memory.  Returns False (nothing launched) when the shape is not supported
+    (N, M % 256, batch % 128); the CPU emulation always applies."""
+    Bt, N = D.shape
+    M = H.shape[1]
+    if _cpu(D):
+        G = ref_gemm_tn(D, H)
+        sgd_update(W32, V32, G, Wbf, Wt, lr, alpha, scale, momentum)
+        return True
+    return bool(native().gemm_tn8_update(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), N, M, Bt,
+                                         W32.data_ptr(), _ptr(V32) if momentum else 0, Wbf.data_ptr(), Wt.data_ptr(),
+                                         float(lr), float(alpha), float(scale), int(bool(momentum)), _stream()))
+
+
 def gemm_tn_reduce(D, H, splits, out, rslab, groups, rout):
     """gemm_tn(D, H, splits, out) and reduce_groups(rslab, groups, rout) in ONE launch:
     the reduction runs on workgroups appended to the GEMM grid (csrc/gpu/kernels.h)."""

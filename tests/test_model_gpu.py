@@ -163,3 +163,34 @@ def test_update_multi_writes_fragment_major(gpu):
     assert torch.equal(Wb, W.bfloat16()) and torch.equal(Wt, W.bfloat16().t())
     assert torch.equal(Wf, ops.frag_major(Wb))
     assert torch.equal(W2t, W2.bfloat16().t())
+
+
+@pytest.mark.parametrize("momentum", [True, False])
+def test_tn_update_fused_matches_separate(gpu, momentum):
+    """the weight gradient with the optimizer step in the 8-phase TN epilogue
+    (ops.gemm_tn_update, one split, 256x256 tiles) against the separate gradient + update
+    kernels: same weights / momentum to GEMM summation order, and the BF16 copies W / W^T
+    written by the epilogue are the FP32 master rounded"""
+    torch.manual_seed(3)
+    sizes, B = [512, 512, 256], 2048
+    ms = []
+    for fused in (True, False):
+        m = MLP(sizes, "ANN", batch=B, momentum=momentum, seed=11, init="fast", splits=[1, 1])
+        m.tn_update = fused
+        ms.append(m)
+    assert all(ms[0]._tn_update_ok(l) for l in range(2)) and not ms[1]._tn_update_ok(0)
+    X = torch.rand(B, sizes[0])
+    T = torch.rand(B, sizes[-1], device="cuda") * 2 - 1
+    for m in ms:
+        Xd = m.prepare_input(X)
+        for _ in range(3):
+            m.train_step(Xd, T=T, lr=0.05, alpha=0.2)
+    torch.cuda.synchronize()
+    a, b = ms
+    for l in range(2):
+        W0 = b.W32[l]
+        assert (a.W32[l] - W0).abs().max().item() <= 1e-5 * max(1.0, W0.abs().max().item())
+        if momentum:
+            assert (a.V32[l] - b.V32[l]).abs().max().item() <= 1e-5 * max(1e-3, b.V32[l].abs().max().item())
+        assert torch.equal(a.Wb[l], a.W32[l].bfloat16())
+        assert torch.equal(a.Wt[l], a.W32[l].bfloat16().t().contiguous())
