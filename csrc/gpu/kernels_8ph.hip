@@ -1,5 +1,9 @@
 /*
- * 256x256-tile NT GEMM with an 8-phase software pipeline (gfx950, BF16 in, FP32 acc).
+ * 256x256-tile GEMMs with an 8-phase software pipeline (gfx950, BF16 in, FP32 acc):
+ *   gemm_nt8_kernel  NT (forward / delta GEMMs), also in a split-K form (opt-in);
+ *   gemm_tn8_kernel  TN (weight gradient), also with the optimizer step fused into the
+ *                    epilogue (hpnn_gemm_tn8_update).
+ * Measured on 8192x4096x4096: NT 1.32-1.42, TN 1.42 PFLOP/s (profiles/r2/s5_8ph_gemm.md).
  *
  *   C[M x N] = epi(A[M x K] . B[N x K]^T)   -- the forward (bipolar epilogue) and the
  *   delta (f'(h) epilogue) GEMMs of the large-layer path; same contract and epilogues
