@@ -55,6 +55,7 @@ int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, vo
 int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
                          void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
+void hpnn_gemm_nt8_set_m32(int on); /* 8-phase NT on v_mfma_f32_32x32x16_bf16 (A/B) */
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
                        int M, int N, int K, int epi, int c_f32, hipStream_t stream);

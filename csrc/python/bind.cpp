@@ -63,6 +63,7 @@ PYBIND11_MODULE(_native, m) {
                   "output_delta");
         });
     m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
+    m.def("gemm_nt8_set_m32", [](int on) { hpnn_gemm_nt8_set_m32(on); });
     m.def("gemm_tn8_update", [](uptr D, int ldd, uptr H, int ldh, int N, int M, int Bt, uptr W32, uptr V32, uptr Wbf,
                                 uptr Wt, float lr, float alpha, float scale, int momentum, uptr stream) {
         const int rc = hpnn_gemm_tn8_update(P(D), ldd, P(H), ldh, N, M, Bt, (float *)P(W32), (float *)P(V32), P(Wbf),

@@ -77,11 +77,20 @@ def test_gemm_nt_big_tile(gpu, M, N, K, epi):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 384), (256, 1024, 1152),
                                    (2304, 256, 640)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
-def test_gemm_nt8(gpu, M, N, K, epi):
+@pytest.mark.parametrize("m32", [0, 1])
+def test_gemm_nt8(gpu, M, N, K, epi, m32):
     """the 8-phase 256x256 kernel (kernels_8ph.hip) called directly at small grids: one
     iteration (K = 128, no restaging), odd iteration counts, a ragged XCD split (9 tiles),
-    padded row strides on every operand"""
+    padded row strides on every operand; both MFMA shapes (16x16x32, 32x32x16)"""
     from hpnn_amd._lib import native
+    native().gemm_nt8_set_m32(m32)
+    try:
+        _check_nt8(native, M, N, K, epi)
+    finally:
+        native().gemm_nt8_set_m32(0)
+
+
+def _check_nt8(native, M, N, K, epi):
     torch.manual_seed(M + 3 * N + K + epi)
     A = _rand(M, K + 64).bfloat16()[:, :K]
     B = (_rand(N, K + 32) + torch.arange(N, device="cuda")[:, None] * 0.001).bfloat16()[:, :K]
