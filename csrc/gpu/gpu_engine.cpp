@@ -516,23 +516,31 @@ struct Batched {
                 return FALSE;
             }
         }
-        /* every delta above used the pre-update weights: all gradients, then ONE update launch */
+        /* every delta above used the pre-update weights: all gradients, then ONE update launch
+         * for the layers whose step did not already run in the gradient GEMM's epilogue
+         * (one-split layers of 256x256 tiles: hpnn_gemm_tn8_update, as MLP._tn_update_ok) */
+        static const int tn_upd = [] { const char *e = getenv("HPNN_TN_UPD"); return !(e && e[0] == '0'); }();
         hpnn_upd_layer u[HPNN_UPD_MAX];
+        int nu = 0;
+        const float scale = 1.0f / (float)n_valid;
         for (int l = 0; l < L; l++) {
             const void *Hin = l ? H[l - 1] : X;
+            if (tn_upd && S[l] == 1 && Np[l] % 256 == 0 && Kp[l] % 256 == 0 && Bp % 128 == 0 &&
+                hpnn_gemm_tn8_update(D[l], Np[l], Hin, Kp[l], Np[l], Kp[l], Bp, W32[l], V32[l], Wb[l], Wt[l], lr,
+                                     alpha, scale, mom ? 1 : 0, s) == 0)
+                continue;
             int r = hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s);
             if (r) {
                 NN_ERROR(stderr, "gemm_tn (layer %d) failed: %d\n", l, r);
                 return FALSE;
             }
             if (L <= HPNN_UPD_MAX)
-                u[l] = {W32[l], V32[l], slab[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], nullptr, S[l], Np[l], Kp[l]};
+                u[nu++] = {W32[l], V32[l], slab[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], nullptr, S[l], Np[l], Kp[l]};
             else if (hpnn_sgd_update(W32[l], V32[l], slab[l], S[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], Np[l], Kp[l],
-                                     lr, alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s))
+                                     lr, alpha, scale, mom ? 1 : 0, s))
                 return FALSE;
         }
-        if (L <= HPNN_UPD_MAX && hpnn_sgd_update_multi(u, L, lr, alpha, 1.0f / (float)n_valid, mom ? 1 : 0, s))
-            return FALSE;
+        if (nu && hpnn_sgd_update_multi(u, nu, lr, alpha, scale, mom ? 1 : 0, s)) return FALSE;
         return TRUE;
     }
 

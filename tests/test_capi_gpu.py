@@ -135,3 +135,24 @@ def test_batched_gpu_exact_resume(tmp_path, dims):
     ep = [json.loads(x) for x in open(b / "m.jsonl")]
     assert [r["epoch"] for r in ep if r["event"] == "epoch"] == [1, 2]
     assert all(r["engine"] == "gpu" for r in ep if r["event"] == "epoch")
+
+
+def test_batched_gpu_tn_update_matches_separate(tmp_path):
+    """native batched engine: layers of 256x256 tiles with one gradient split take the
+    weight-gradient GEMM with the optimizer step in its epilogue (hpnn_gemm_tn8_update);
+    same training as the separate gradient + update kernels (HPNN_TN_UPD=0)"""
+    res = {}
+    for tag, env in (("fused", {}), ("separate", {"HPNN_TN_UPD": "0"})):
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 256, 256, 256, False, seed=4)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="w", type="ANN", seed=13, inputs=256, hiddens=[256],
+                           outputs=256, train="BPM", sample_dir="./samples", test_dir="./samples", mode="batched",
+                           batch=256, epochs=3, lr=0.05)
+        _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, extra_env=env)
+        res[tag] = (formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"],
+                    formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"])
+    for w0, wf, ws in zip(res["fused"][0], res["fused"][1], res["separate"][1]):
+        df, ds = wf - w0, ws - w0
+        assert np.linalg.norm(ds) > 0
+        rel = np.linalg.norm(df - ds) / np.linalg.norm(ds)
+        assert rel < 1e-3, rel
