@@ -7,7 +7,11 @@ bwd + update per sample), synthetic data, random-init weights (reference init ru
 Weak scaling: every GPU trains on its own `--batch` samples per step; gradients are
 all-reduced over RCCL (bucketed, overlapped with the backward).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+--model rruff / synth runs the other GPU configs of BASELINE.json through the same
+contract (RRUFF-shaped 4096-230-230 SNN, batch 16384 per GPU; synthetic 8 x 4096 ANN,
+global batch 8192 split over the GPUs = strong scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model mnist|rruff|synth]
   N>1 is launched by the driver as
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
 Prints ONE JSON line (rank 0).
@@ -29,13 +33,29 @@ from hpnn_amd.parallel import DataParallel, init_from_env  # noqa: E402
 
 METRIC = "training samples/sec (whole node), MNIST 784-128-64-10 SNN at 1/2/4/8 MI355X"
 
+# the other GPU configs of BASELINE.json (--model): sizes, type, batch, whether the batch is
+# per GPU (weak scaling) or for the whole node (strong scaling), metric name
+MODELS = {
+    "mnist": ([784, 128, 64, 10], "SNN", 65536, "weak", METRIC,
+              "mnist_snn 784-128-64-10 (SNN, BPM momentum 0.2, lr 0.01, batched mode)"),
+    "rruff": ([4096, 230, 230], "SNN", 16384, "weak",
+              "training samples/sec (whole node), RRUFF-XRD-shaped 4096-230-230 SNN",
+              "rruff_snn 4096-230-230 (SNN, BPM momentum 0.2, lr 0.01, batched mode)"),
+    "synth": ([4096] * 9, "ANN", 8192, "strong",
+              "training samples/sec (whole node), synthetic 8-layer x 4096-wide ANN, global batch 8192",
+              "synth_ann 4096^9 (ANN, BPM momentum 0.2, lr 0.01, batched mode)"),
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=65536, help="per-GPU minibatch (samples per step per GPU)")
+    ap.add_argument("--model", choices=sorted(MODELS), default="mnist",
+                    help="mnist: the headline config; rruff / synth: the other BASELINE.json GPU configs")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="per-GPU minibatch (default: the config's; synth splits its global 8192 over the GPUs)")
     ap.add_argument("--datasets", type=int, default=4, help="distinct synthetic minibatches cycled per GPU")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--alpha", type=float, default=0.2)
@@ -53,24 +73,34 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    sizes = [784, 128, 64, 10]
-    m = MLP(sizes, "SNN", batch=args.batch, device=dev, momentum=True, seed=10958)
+    sizes, net, batch, scaling, metric, model_name = MODELS[args.model]
+    if not args.batch:
+        args.batch = batch // world if scaling == "strong" else batch
+    m = MLP(sizes, net, batch=args.batch, device=dev, momentum=True, seed=10958,
+            init="reference" if args.model == "mnist" else "fast")
     dp = DataParallel(m)
     dp.broadcast_parameters()
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     Xs, Ls = [], []
     for _ in range(args.datasets):
-        if args.input == "u8":
+        if args.input == "u8" and args.model == "mnist":
             X = torch.randint(0, 256, (m.Bp, sizes[0]), device=dev, generator=g, dtype=torch.uint8)
         else:
             X = torch.rand(m.Bp, sizes[0], device=dev, generator=g)
         Xs.append(m.prepare_input(X))
-        Ls.append(torch.randint(0, sizes[-1], (m.Bp,), device=dev, generator=g, dtype=torch.int32))
+        if net == "SNN":
+            Ls.append(torch.randint(0, sizes[-1], (m.Bp,), device=dev, generator=g, dtype=torch.int32))
+        else:  # ANN: dense +-1 targets of a random class
+            T = torch.full((m.Bp, sizes[-1]), -1.0, device=dev)
+            T[torch.arange(m.Bp, device=dev), torch.randint(0, sizes[-1], (m.Bp,), device=dev, generator=g)] = 1.0
+            Ls.append(T)
     torch.cuda.synchronize()
 
     def step(i):
-        dp.train_step(Xs[i % args.datasets], labels=Ls[i % args.datasets], lr=args.lr, alpha=args.alpha)
+        tgt = Ls[i % args.datasets]
+        kw = dict(labels=tgt) if net == "SNN" else dict(T=tgt)
+        dp.train_step(Xs[i % args.datasets], lr=args.lr, alpha=args.alpha, **kw)
 
     # HIP graphs: single GPU always; data parallel when the gradient all-reduce goes through
     # libhpnn's native RCCL communicator (capturable: event fork/join of its side stream),
@@ -157,8 +187,9 @@ def main():
     samples = args.steps * m.Bp * world
     value = samples / elapsed
     if rank == 0:
+        u8 = args.input == "u8" and args.model == "mnist"
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": value,
             "unit": "samples/s",
             "n_gpus": world,
@@ -166,14 +197,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "bf16",
             "data": ("synthetic (uniform 8-bit pixels 0..255 -> pixel/255 in BF16 as MNIST images, uniform labels; "
-                     "random-init weights, reference init rule)" if args.input == "u8" else
-                     "synthetic (uniform [0,1) pixels, uniform labels; random-init weights, reference init rule)"),
+                     "random-init weights, reference init rule)" if u8 else
+                     ("synthetic (uniform [0,1) pixels, uniform labels; random-init weights, reference init rule)"
+                      if args.model == "mnist" else
+                      "synthetic (uniform [0,1) inputs, uniform labels (SNN) / +-1 one-hot targets (ANN); "
+                      "random-init weights)")),
             "config": {
-                "model": "mnist_snn 784-128-64-10 (SNN, BPM momentum 0.2, lr 0.01, batched mode)",
+                "model": model_name,
                 "global_batch": m.Bp * world,
                 "per_gpu_batch": m.Bp,
                 "seq_len": None,
