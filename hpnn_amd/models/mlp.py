@@ -266,6 +266,10 @@ class MLP:
         if Xg is not None:  # delta1 came fragment-major from the fused front
             ops.gemm_fm_direct(self.D[0], Xg, self.Np[0], self.Kp[0], splits=self.S[0], out=self.slab[0],
                                hscale=getattr(X, "hpnn_fm_scale", 1.0))
+        elif reduce and self.S[l] == 1:
+            # one split: the GEMM writes the all-reduce bucket itself (no slab copy)
+            ops.gemm_tn(self.D[l], Hin, splits=1, out=self.G[l].unsqueeze(0))
+            return
         else:
             ops.gemm_tn(self.D[l], Hin, splits=self.S[l], out=self.slab[l])
         if reduce:
