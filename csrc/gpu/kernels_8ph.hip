@@ -639,7 +639,9 @@ int splitk_epi(const float *P, int S, long cstride, int M, int N, const void *au
 
 /* split-K workspace, one per device (train_nn -G drives several GPUs from one process, one
  * host thread each): grown outside stream capture only -- a capture that would need a
- * bigger one gets -1 and the caller takes another kernel */
+ * bigger one gets -1 and the caller takes another kernel.  Split-K GEMMs of one device
+ * share it, so they must be stream-ordered (the engines issue GEMMs on one compute stream
+ * per device); it lives until the process exits. */
 constexpr int WS_DEV = 64;
 float *g_ws[WS_DEV] = {};
 size_t g_ws_bytes[WS_DEV] = {};
