@@ -640,6 +640,7 @@ struct UpdArgs {
     int n;
     float lr, alpha, scale;
     int momentum;
+    int prefetch; /* sub-tile kernel: W / V loads issued with the slab loads (HPNN_UPD_PREFETCH) */
 };
 
 __global__ __launch_bounds__(256) void sgd_update_multi_kernel(UpdArgs a) {
@@ -763,6 +764,13 @@ __global__ __launch_bounds__(512) void sgd_update_multi_sub_kernel(UpdArgs a) {
     const int ty = lane >> 3, tx = lane & 7;
     const int n = tn * 32 + sub * 8 + ty, k = tk * 32 + tx * 4;
     const size_t idx = (size_t)n * L.K + k;
+    /* the updating wave fetches its weights (and momentum) first, so those loads are in
+     * flight together with the slab loads instead of a round trip after the barrier */
+    f32x4 wv = {0.f, 0.f, 0.f, 0.f}, vv = wv;
+    if (w == 0 && a.prefetch) {
+        wv = *(const f32x4 *)(L.W32 + idx);
+        if (a.momentum) vv = *(const f32x4 *)(L.V32 + idx);
+    }
     /* up to 8 slab loads per lane in flight at once (the step is load-latency bound:
      * each wave owns only S/8 slabs), summed in a fixed order */
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -782,9 +790,12 @@ __global__ __launch_bounds__(512) void sgd_update_multi_sub_kernel(UpdArgs a) {
         f32x4 g = part[0][lane];
 #pragma unroll
         for (int ww = 1; ww < 8; ww++) g += part[ww][lane];
-        f32x4 wv = *(const f32x4 *)(L.W32 + idx);
+        if (!a.prefetch) {
+            wv = *(const f32x4 *)(L.W32 + idx);
+            if (a.momentum) vv = *(const f32x4 *)(L.V32 + idx);
+        }
         if (a.momentum) {
-            f32x4 v = *(const f32x4 *)(L.V32 + idx);
+            f32x4 v = vv;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 v[r] += a.lr * (g[r] * a.scale);
@@ -921,6 +932,8 @@ extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float 
     a.alpha = alpha;
     a.scale = scale;
     a.momentum = momentum;
+    static const int prefetch = [] { const char *e = getenv("HPNN_UPD_PREFETCH"); return !(e && e[0] == '0'); }();
+    a.prefetch = prefetch;
     int t = 0;
     for (int l = 0; l < n; l++) {
         const hpnn_upd_layer &L = layers[l];
