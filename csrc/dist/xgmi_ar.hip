@@ -114,18 +114,13 @@ __device__ __forceinline__ void add4(float4 &a, const float4 &b) {
     a.w += b.w;
 }
 
-/* local sum of element i of the input: slabs s = k (mod 8) accumulate in acc[k], eight
- * loads in flight per thread (the copy-in of a 48-slab weight gradient is latency-bound:
- * 2 loads in flight took 15.2 us per MNIST step), combined in a fixed tree */
-__device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
-    int j = 0;
-    while (j + 1 < in.nseg && i >= in.end4[j]) j++;
-    const long li = i - (j ? in.end4[j - 1] : 0);
-    const float4 *p = in.src[j] + li;
-    const long st = in.stride4[j];
-    const int S = in.S[j];
-    if (S == 1) return p[0];
-    constexpr int U = 8;
+/* local sum of element i of the input: slabs s = k (mod U) accumulate in acc[k], U = 8 loads
+ * in flight per thread, combined in a fixed tree (2 in flight took 15.2 us per MNIST step,
+ * 8 took 11.3).  More measured slower on the N > 1 step path timed on one GPU: 16 per batch
+ * +0.7-1.1 us, a software-pipelined 16 + 16 variant +8 us (scripts/gpu_xar_pipe.sh,
+ * profiles/r2/s5_xar_launch_shape.txt). */
+template <int U>
+__device__ __forceinline__ float4 xar_load_in_u(const float4 *p, long st, int S) {
     float4 acc[U];
     int s = 0;
     if (S >= U) {
@@ -150,6 +145,16 @@ __device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
 #pragma unroll
         for (int k = 0; k < U; k += 2 * w) add4(acc[k], acc[k + w]);
     return acc[0];
+}
+
+__device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
+    int j = 0;
+    while (j + 1 < in.nseg && i >= in.end4[j]) j++;
+    const long li = i - (j ? in.end4[j - 1] : 0);
+    const float4 *p = in.src[j] + li;
+    const int S = in.S[j];
+    if (S == 1) return p[0];
+    return xar_load_in_u<8>(p, in.stride4[j], S);
 }
 
 /* sum of element i over the first `world` data halves, rank order */
@@ -223,7 +228,7 @@ __device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g) {
  * TWO = true: shard s = [s * sh, min((s + 1) * sh, n4)), workgroup b owns
  * [s * sh + b * per, ...+ per) of every shard */
 template <bool TWO, bool UPD>
-__global__ __launch_bounds__(1024) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
+__global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
                                                   long n4, long half_stride4, unsigned long long timeout, int light,
                                                   XarUpd upd) {
     const int b = blockIdx.x;
@@ -315,7 +320,6 @@ struct hpnn_xar {
     int mode = 0;     /* HPNN_XAR_MODE: 0 auto, 1 one-shot, 2 two-shot */
     int light = 1;    /* HPNN_XAR_FENCE=1 -> 0: full system fences, see xbarrier */
     int blocks = 128; /* HPNN_XAR_BLOCKS (same on every rank), <= HPNN_XAR_MAX_BLOCKS */
-    int threads = 256; /* HPNN_XAR_THREADS: 64..1024, multiple of 64 */
 };
 
 extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
@@ -343,8 +347,6 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     c->light = !(fe && fe[0] == '1');
     const char *nb = getenv("HPNN_XAR_BLOCKS");
     if (nb && atoi(nb) > 0) c->blocks = atoi(nb) < HPNN_XAR_MAX_BLOCKS ? atoi(nb) : HPNN_XAR_MAX_BLOCKS;
-    const char *nt = getenv("HPNN_XAR_THREADS");
-    if (nt && atoi(nt) >= 64 && atoi(nt) <= 1024 && atoi(nt) % 64 == 0) c->threads = atoi(nt);
     c->peers.buf[rank] = (float4 *)c->buf;
     c->peers.sig[rank] = c->sig;
     return c;
@@ -407,7 +409,7 @@ static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipS
     XarUpd none = {};
     const XarUpd &u = upd ? *upd : none;
 #define HPNN_XARL(T_, U_)                                                                                          \
-    hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3((unsigned)c->threads), 0, stream, c->peers, c->rank,       \
+    hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,       \
                        c->world, in, (float4 *)out, n4, half4, c->timeout, c->light, u)
     if (two) {
         if (upd) HPNN_XARL(true, true);
