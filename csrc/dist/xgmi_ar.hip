@@ -23,7 +23,7 @@
  * barrier A of call e+1, which no peer signals before its call-e kernel (all its reads
  * of that half) has completed.
  * Epochs are per workgroup (every call runs the full fixed grid, so they stay equal),
- * kept in this rank's signal block and advanced by the kernel,
+ * kept in ordinary device memory of this rank and advanced by the kernel,
  * so launches captured in a HIP graph replay correctly; all ranks issue the same
  * sequence of all-reduces (same sizes, same mode), so the epochs and halves agree.  Every
  * wait is bounded by a wall-clock timeout: a missing peer sets the error word, never
@@ -44,7 +44,6 @@ namespace {
 
 struct Signal {
     unsigned int flag[2][HPNN_XAR_MAX_BLOCKS][HPNN_XAR_MAX_RANKS]; /* barriers A, B */
-    unsigned int epoch[HPNN_XAR_MAX_BLOCKS];
     unsigned int error;
 };
 
@@ -230,13 +229,16 @@ __device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g) {
 template <bool TWO, bool UPD>
 __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int world, XarIn in, float4 *__restrict__ out,
                                                   long n4, long half_stride4, unsigned long long timeout, int light,
-                                                  XarUpd upd) {
+                                                  XarUpd upd, unsigned int *__restrict__ ep) {
     const int b = blockIdx.x;
     Signal *me = P.sig[rank];
     __shared__ unsigned int s_ep;
     if (threadIdx.x == 0) {
-        const unsigned int e = me->epoch[b] + 1; /* only this workgroup writes epoch[b] */
-        me->epoch[b] = e;
+        /* the epochs live in ordinary device memory (only this workgroup of this rank ever
+         * touches ep[b], and kernel boundaries order launches): one uncached round trip
+         * less per call than keeping them in the signal block */
+        const unsigned int e = ep[b] + 1;
+        ep[b] = e;
         s_ep = e;
     }
     __syncthreads();
@@ -314,6 +316,7 @@ struct hpnn_xar {
     size_t max_bytes = 0;
     void *buf = nullptr;
     Signal *sig = nullptr;
+    unsigned int *ep = nullptr; /* per-workgroup barrier epochs (this rank only) */
     XarPeers peers = {};
     bool opened[HPNN_XAR_MAX_RANKS] = {};
     unsigned long long timeout = 0;
@@ -331,7 +334,10 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     if (hipGetDevice(&c->device) != hipSuccess ||
         hipExtMallocWithFlags(&c->buf, 2 * c->max_bytes, hipDeviceMallocUncached) != hipSuccess ||
         hipExtMallocWithFlags((void **)&c->sig, sizeof(Signal), hipDeviceMallocUncached) != hipSuccess ||
-        hipMemset(c->sig, 0, sizeof(Signal)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        hipMemset(c->sig, 0, sizeof(Signal)) != hipSuccess ||
+        hipMalloc((void **)&c->ep, HPNN_XAR_MAX_BLOCKS * sizeof(unsigned int)) != hipSuccess ||
+        hipMemset(c->ep, 0, HPNN_XAR_MAX_BLOCKS * sizeof(unsigned int)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
         NN_ERROR(stderr, "xgmi all-reduce: device allocation failed\n");
         hpnn_xar_destroy(c);
         return nullptr;
@@ -410,7 +416,7 @@ static int xar_launch(hpnn_xar *c, const XarIn &in, float *out, long count, hipS
     const XarUpd &u = upd ? *upd : none;
 #define HPNN_XARL(T_, U_)                                                                                          \
     hipLaunchKernelGGL((xar_kernel<T_, U_>), dim3((unsigned)blocks), dim3(256), 0, stream, c->peers, c->rank,       \
-                       c->world, in, (float4 *)out, n4, half4, c->timeout, c->light, u)
+                       c->world, in, (float4 *)out, n4, half4, c->timeout, c->light, u, c->ep)
     if (two) {
         if (upd) HPNN_XARL(true, true);
         else HPNN_XARL(true, false);
@@ -544,5 +550,6 @@ extern "C" void hpnn_xar_destroy(hpnn_xar *c) {
     }
     if (c->buf) hipFree(c->buf);
     if (c->sig) hipFree(c->sig);
+    if (c->ep) hipFree(c->ep);
     delete c;
 }
