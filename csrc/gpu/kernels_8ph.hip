@@ -516,6 +516,7 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
         float *__restrict__ V32 = upd.V32;
         __bf16 *__restrict__ Wb = upd.Wb;
         __bf16 *__restrict__ Wt = upd.Wt;
+        __bf16 *tw = (__bf16 *)(lds + wave * 16384);
 #pragma unroll
         for (int mi = 0; mi < 2; mi++)
 #pragma unroll
@@ -557,10 +558,20 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 #pragma unroll
                         for (int r = 0; r < 4; r++) wb[r] = (__bf16)ww[r];
                         *(bf16x4 *)(Wb + idx) = wb;
+                        /* W^T through this wave's 16 KiB of the (now idle) LDS: [m][n] image of
+                         * its 128 x 64 tile, written out below in 16-byte row pieces */
+                        const int ml = mi * 64 + i * 16 + 4 * q, nl = ni * 32 + j * 16 + r16;
 #pragma unroll
-                        for (int r = 0; r < 4; r++) Wt[(size_t)(m + r) * N + n] = wb[r];
+                        for (int r = 0; r < 4; r++) tw[(ml + r) * 64 + nl] = wb[r];
                     }
             }
+        /* every wave is past its last operand read of the main loop (the final barriers),
+         * and the region is this wave's own: LDS ops of one wave complete in order */
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int e = t * 64 + lane, ml = e >> 3, nc = (e & 7) * 8;
+            *(bf16x8 *)(Wt + (size_t)(m0 + wm * 128 + ml) * N + n0 + wn * 64 + nc) = *(const bf16x8 *)(tw + ml * 64 + nc);
+        }
     } else {
 #pragma unroll
         for (int mi = 0; mi < 2; mi++)
