@@ -345,8 +345,8 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     int khz = 100000;
     hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
     const char *e = getenv("HPNN_XAR_TIMEOUT_MS");
-    const long ms = e ? atol(e) : 5000;
-    c->timeout = (unsigned long long)(ms > 0 ? ms : 5000) * (unsigned long long)(khz > 0 ? khz : 100000);
+    const long ms = e ? atol(e) : 20000; /* generous: a late peer in the first step (lazy module loads) is not a failure */
+    c->timeout = (unsigned long long)(ms > 0 ? ms : 20000) * (unsigned long long)(khz > 0 ? khz : 100000);
     const char *m = getenv("HPNN_XAR_MODE");
     c->mode = m ? atoi(m) : 0;
     const char *fe = getenv("HPNN_XAR_FENCE");

@@ -17,7 +17,7 @@
  *
  * Graph capture: the barrier epochs live in device memory and are advanced by the
  * kernel itself, so a captured launch replays correctly any number of times.
- * Failure: every spin wait is bounded (HPNN_XAR_TIMEOUT_MS, default 5000); a peer that
+ * Failure: every spin wait is bounded (HPNN_XAR_TIMEOUT_MS, default 20000); a peer that
  * never arrives sets the error word instead of hanging the GPU, and
  * hpnn_xar_status reports it.
  *
