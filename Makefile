@@ -2,6 +2,8 @@
 #   make            -> hpnn_amd/lib/libhpnn.so, bin/train_nn, bin/run_nn,
 #                      bin/pmnist, bin/pdif, hpnn_amd/_native*.so
 #   make clean
+#   make install PREFIX=/usr/local  -> lib/libhpnn.so, include/libhpnn.h + include/libhpnn/*.h,
+#                                      lib/pkgconfig/libhpnn.pc, bin/{train_nn,run_nn,...}
 # Device code: hipcc --offload-arch=gfx950 only (no other targets).
 ROCM      ?= /opt/rocm
 ARCH      ?= gfx950
@@ -46,9 +48,9 @@ $(LIB): $(CORE_OBJ) $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ $(LDFLAGS) -Wl,-soname,libhpnn.so
 
-$(BINDIR)/%: tools/%.cpp $(LIB) tools/cli_common.h
+$(BINDIR)/%: tools/%.cpp $(LIB) tools/cli_common.h Makefile
 	@mkdir -p $(BINDIR)
-	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lhpnn $(LDFLAGS) -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lhpnn $(LDFLAGS) -Wl,-rpath,'$$ORIGIN/../$(LIBDIR):$$ORIGIN/../lib'
 
 $(PYMOD): csrc/python/bind.cpp $(LIB) $(HDRS)
 	$(CXX) $(CXXFLAGS) -shared $(PYINC) $< -o $@ -L$(LIBDIR) -lhpnn $(LDFLAGS) -Wl,-rpath,'$$ORIGIN/lib'
@@ -56,7 +58,26 @@ $(PYMOD): csrc/python/bind.cpp $(LIB) $(HDRS)
 clean:
 	rm -rf $(BUILD) $(LIB) $(BINS) $(PYMOD)
 
-.PHONY: all clean
+# Installation (the reference's src/Makefile.am:12-41 layout: libhpnn.h in include/, the
+# other headers in include/libhpnn/, pkg-config file in lib/pkgconfig/).  The CLIs find
+# the installed library through their $$ORIGIN/../lib rpath.
+PREFIX    ?= /usr/local
+VERSION   := 0.3.0
+install: $(LIB) $(BINS)
+	install -d $(DESTDIR)$(PREFIX)/lib/pkgconfig $(DESTDIR)$(PREFIX)/include/libhpnn $(DESTDIR)$(PREFIX)/bin
+	install -m 755 $(LIB) $(DESTDIR)$(PREFIX)/lib/libhpnn.so
+	install -m 644 include/libhpnn.h $(DESTDIR)$(PREFIX)/include/libhpnn.h
+	install -m 644 include/libhpnn/*.h $(DESTDIR)$(PREFIX)/include/libhpnn/
+	install -m 755 $(BINS) $(DESTDIR)$(PREFIX)/bin/
+	sed -e 's|@PREFIX@|$(PREFIX)|' -e 's|@ROCM@|$(ROCM)|' -e 's|@VERSION@|$(VERSION)|' libhpnn.pc.in \
+	    > $(DESTDIR)$(PREFIX)/lib/pkgconfig/libhpnn.pc
+
+uninstall:
+	rm -f $(DESTDIR)$(PREFIX)/lib/libhpnn.so $(DESTDIR)$(PREFIX)/include/libhpnn.h \
+	      $(DESTDIR)$(PREFIX)/lib/pkgconfig/libhpnn.pc $(addprefix $(DESTDIR)$(PREFIX)/bin/,$(notdir $(BINS)))
+	rm -rf $(DESTDIR)$(PREFIX)/include/libhpnn
+
+.PHONY: all clean install uninstall
 
 # Host-side sanitizer build (AddressSanitizer + UBSan) of the C API, CPU engine, runtime,
 # comm layer and CLIs; device code objects are the regular ones (GPU sanitizers are not

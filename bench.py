@@ -138,6 +138,10 @@ def main():
                 print("xGMI all-reduce barrier timed out on some rank; using RCCL", file=sys.stderr)
             dp.native.detach_xar()
             if not dp.native.h:  # xGMI-only (rehearsal): torch.distributed takes the gradients
+                # keep the detached communicator (and its IPC-mapped buffers) alive until
+                # every rank is past the final barrier: a peer may still be inside a
+                # timed-out all-reduce reading them
+                dp._detached_native = dp.native
                 dp.native = None
                 use_graph = bool(args.graph) and args.graph == 2
             dp.broadcast_parameters()
@@ -192,6 +196,25 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    # timed-region integrity: a barrier timeout inside a replayed xGMI all-reduce, or an
+    # asynchronous RCCL error, leaves wrong sums behind without stopping the ranks -- every
+    # rank re-checks its communicator and all must agree, else no number is reported
+    healthy = True
+    if dp.active:
+        try:
+            dp.check()
+        except RuntimeError as e:
+            print(f"rank {rank}: {e}", file=sys.stderr)
+            healthy = False
+        if dp.native is not None and not dp.native.xar_healthy():
+            healthy = False
+        healthy = dp.all_ok(healthy)
+    if not healthy:
+        if rank == 0:
+            print("communication failed during the timed steps; no result reported", file=sys.stderr)
+        if dp.active:
+            dist.barrier()
+        sys.exit(3)
     loss_sum, correct = m.read_stats()
     samples = args.steps * m.Bp * world
     value = samples / elapsed
@@ -234,6 +257,8 @@ def main():
         dist.barrier()
         if dp.native is not None:
             dp.native.close()
+        if getattr(dp, "_detached_native", None) is not None:
+            dp._detached_native.close()
         dist.destroy_process_group()
 
 

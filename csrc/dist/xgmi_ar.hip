@@ -480,6 +480,9 @@ extern "C" int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_
     for (int l = 0; l < nl; l++) {
         const hpnn_xar_upd_layer &L = layers[l];
         if (!L.W32 || !L.Wbf || !L.Wt || (momentum && !L.V32) || L.N <= 0 || L.K <= 0 || L.K % 4) return -1;
+        /* float4 / bf16x4 accesses: misaligned tensors take the caller's fallback path */
+        if (((uintptr_t)L.W32 | (uintptr_t)(momentum ? L.V32 : L.W32)) & 15 || ((uintptr_t)L.Wbf | (uintptr_t)L.Wt) & 7)
+            return -1;
         if (L.Wf && (L.N % 16 || L.K % 32)) return -1;
         u.W32[l] = L.W32;
         u.V32[l] = L.V32;

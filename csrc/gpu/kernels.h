@@ -179,6 +179,17 @@ int hpnn_mlp3_front_trace(unsigned long long *out);
 int hpnn_mlp3_fused_trace(unsigned long long *out);
 /* grid hpnn_mlp3_fused will use for Bp samples (slab rows to allocate) */
 int hpnn_mlp3_fused_grid(int Bp, int grid);
+/* the same step up to delta1 with 256-sample tiles (kernels_mlp3t.hip): X given
+ * FRAGMENT-MAJOR ([Bp/32][K0/16][64][8], ops.to_fragment_major), 8-bit (xu8: used as
+ * bf16(byte * xscale)) or BF16; W0f fragment-major BF16 W0, W1 [64][128], W2 [32][64] and
+ * W2t [64][32] BF16; delta1 written fragment-major ([Bp/32][8][64][8]); per-block
+ * [G1 | G2] slabs as hpnn_mlp3_mid.  Bp % 256 == 0, K0 in {256, 800}.  grid <= 0: one
+ * workgroup per CU (capped at Bp / 256).  Returns the grid used (> 0) or an error (< 0). */
+int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0f, const void *W1, const void *W2,
+                   const void *W2t, const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1,
+                   float *gslab, float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type,
+                   int grid, hipStream_t stream);
+int hpnn_mlp3_tile_grid(int Bp, int grid);
 /* floats per block slab written by hpnn_mlp3_mid */
 int hpnn_mlp3_slab_floats(void);
 /* deterministic 2-pass slab reduction: groups of slabs into tmp (>= 16*n floats,

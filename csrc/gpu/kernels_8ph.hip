@@ -566,7 +566,12 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
                     }
             }
         /* every wave is past its last operand read of the main loop (the final barriers),
-         * and the region is this wave's own: LDS ops of one wave complete in order */
+         * and the region is this wave's own: LDS ops of one wave complete in order; the
+         * fence + wave barrier order the cross-lane transpose (stores above by one lane,
+         * 16-byte reads below by others) for the compiler as well */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int t = 0; t < 16; t++) {
             const int e = t * 64 + lane, ml = e >> 3, nc = (e & 7) * 8;
@@ -714,6 +719,8 @@ extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int l
                                     float *V32, void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum,
                                     hipStream_t stream) {
     if (N % 256 || M % 256 || Bt % 128 || ldd % 8 || ldh % 8 || !W32 || !Wbf || !Wt || (momentum && !V32)) return -1;
+    /* the epilogue moves W32 / V32 as float4 and W / W^T as 8- and 16-byte pieces */
+    if (((uintptr_t)W32 | (uintptr_t)(momentum ? V32 : W32) | (uintptr_t)Wbf | (uintptr_t)Wt) & 15) return -1;
     if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
     const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum};

@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void output_delta_v4_kernel(const float *__res
                 e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
                 if (!labels && valid) {
                     const float *tr = T + (size_t)row * ldt + c;
-                    if ((ldt & 3) == 0) {
+                    if ((ldt & 3) == 0 && ((uintptr_t)T & 15) == 0) {
                         const float4 w = *(const float4 *)tr;
                         tv[0] = w.x; tv[1] = w.y; tv[2] = w.z; tv[3] = w.w;
                     } else { /* unaligned target rows: scalar loads, same values */
@@ -889,7 +889,8 @@ extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ld
         else if (n_out <= 192) HPNN_OD(3);
         else HPNN_OD(4);
 #undef HPNN_OD
-    } else if (ldz % 4 == 0 && ldd % 4 == 0 && !od_wave_mode()) {
+    } else if (ldz % 4 == 0 && ldd % 4 == 0 && ((uintptr_t)Z & 15) == 0 && ((uintptr_t)D & 7) == 0 &&
+               !od_wave_mode()) {
         const int grid = (B + 3) / 4 < 4096 ? (B + 3) / 4 : 4096;
         hipLaunchKernelGGL(output_delta_v4_kernel, dim3(grid), dim3(256), 0, stream, Z, ldz, T, ldt, labels, t_hi,
                            t_lo, (__bf16 *)D, ldd, O, ldo, loss_acc, correct, B, n_valid, n_out, type);

@@ -1,0 +1,440 @@
+/*
+ * mlp3_tile: the n_in -> 128 -> 64 -> n_out(<=32) training step up to delta1, one
+ * 256-sample tile per workgroup iteration (gfx950).
+ *
+ * Reference: the per-sample GEMV chain of ann_kernel_train / snn_kernel_train
+ * (ann.c:883-888, 1279-1592; snn.c:280-335, 481-794; cuda_ann.cu:426-2093,
+ * cuda_snn.cu:156-976 softmax, 2726-3717 train_momentum), batched.
+ *
+ * Input: the minibatch in FRAGMENT-MAJOR order ([Bp/32][K0/16][64 lanes][8], lane
+ * l = 16 g + r of chunk (t, cb) holding X[32 t + 8 g + j][16 cb + r], j < 8; see
+ * ops.to_fragment_major), either 8-bit pixels (used as bf16(byte * xscale)) or BF16.
+ * It is the SAME buffer the first-layer gradient kernel (kernels_g0.hip,
+ * gemm_fm_direct) streams right after this one, so a step reads the batch from HBM
+ * once; the second read is served by the 256 MB Infinity Cache.
+ *
+ * One 512-thread workgroup (8 waves) per CU; per 256-sample tile:
+ *
+ *  A  H1 = f(X W0^T)  [256 x 128]: K0/32 k-steps.  Wave (ng = w&3, sh = w>>2) owns 32
+ *     neurons x 128 samples (16 MFMA 16x16x32 per k-step, 64 accumulator registers).
+ *     Its two W0 fragments per k-step come straight from the L2-resident fragment-major
+ *     copy into registers (1 KiB per wave load); the X slice (256 samples x 32 features,
+ *     8 KiB of pixels) is loaded once per workgroup, one 16-byte load per lane,
+ *     converted in registers and written as the transposed image X^T [32 feat][256
+ *     samples] into one of two LDS stages; MFMA B operands are read from it with
+ *     ds_read_b64_tr_b16.  Loads run D k-steps ahead (register ring), one barrier per
+ *     k-step.  The K loop is fully unrolled (K0 is a template parameter) so every ring
+ *     index is static and the compiler's counted vmcnt waits stay exact.
+ *  B  back chain, per wave on ITS OWN 32 samples (no workgroup barrier inside):
+ *     H2 = f(H1 W1^T), logits, softmax / sigmoid + loss + delta3 + argmax,
+ *     delta2 = (delta3 W2) f'(H2), delta1 = (delta2 W1) f'(H1) -> HBM (fragment-major,
+ *     the operand layout of the G0 kernel).
+ *  C  one barrier, then G1 += H1^T delta2 and G2 += H2^T delta3 over all 256 samples,
+ *     each wave owning output tiles (accumulated in registers over the block's tiles,
+ *     written once as the block's [G1 | G2] FP32 slab, the layout of mlp3_mid).
+ *
+ * Versus mlp3_fused (kernels_mlp3x.hip, 32-sample tiles with a software-pipelined
+ * front/back interleave and W0 resident in VGPRs): the tile is 8x larger, so the
+ * latency-bound back chain runs once per 256 samples with 8x the independent MFMA work
+ * per phase, and needs 2 barriers per tile instead of 4 per 32 samples.
+ *
+ * LDS (160 KiB, exactly): H1 [256][128] 64 KiB | X^T stages 2 x 16 KiB, aliased by
+ * H2 [256][64] in the chain | delta2 [256][64] 32 KiB | delta3 [256][32] 16 KiB |
+ * W1 [64][128] 16 KiB.  All images use the T32 layout of mfma_common.h.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "kernels.h"
+#include "mfma_common.h"
+#include "mlp3_common.h"
+
+using namespace hpnn;
+using namespace hpnn::mlp3;
+
+namespace {
+
+constexpr int TS = 256;              /* samples per tile */
+constexpr int XR = 32;               /* features per k-step (rows of the X^T stage) */
+constexpr int IMG_XT = XR * TS * 2;  /* 16 KiB */
+constexpr int OFF_H1 = 0;
+constexpr int OFF_XT = OFF_H1 + TS * H1 * 2;
+constexpr int OFF_H2 = OFF_XT; /* chain only: the X^T stages are dead then */
+constexpr int OFF_D2 = OFF_XT + 2 * IMG_XT;
+constexpr int OFF_D3 = OFF_D2 + TS * H2 * 2;
+constexpr int OFF_W1 = OFF_D3 + TS * NO * 2;
+constexpr int LDS_TOTAL = OFF_W1 + IMG_W1;
+static_assert(TS * H2 * 2 <= 2 * IMG_XT, "H2 aliases the X^T stages");
+static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
+
+/* 8 unsigned bytes -> bf16x8 of (byte * scale); the same rounding as gemm_fm_direct */
+__device__ __forceinline__ bf16x8 u8x8_to_bf16(unsigned int lo, unsigned int hi, float scale) {
+    bf16x8 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        r[e] = (__bf16)((float)((lo >> (8 * e)) & 0xffu) * scale);
+        r[4 + e] = (__bf16)((float)((hi >> (8 * e)) & 0xffu) * scale);
+    }
+    return r;
+}
+
+/* within-wave ordering of LDS writes before other lanes' reads (one wave's LDS
+ * instructions execute in order; this keeps the compiler from moving them) */
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int TYPE, bool LABELS, int KS, bool XU8, int D>
+__global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
+                                                         const __bf16 *__restrict__ W0f,
+                                                         const __bf16 *__restrict__ W1,
+                                                         const __bf16 *__restrict__ W2,
+                                                         const __bf16 *__restrict__ W2t,
+                                                         const int *__restrict__ labels,
+                                                         const float *__restrict__ T, int ldt, float t_hi,
+                                                         float t_lo, __bf16 *__restrict__ D1,
+                                                         float *__restrict__ gslab, float *__restrict__ loss_acc,
+                                                         unsigned int *__restrict__ correct, int n_tiles,
+                                                         int n_valid, int n_out) {
+    constexpr int XN = XU8 ? 1 : 2;       /* 16-byte loads per lane per k-step */
+    constexpr int CHUNK = XU8 ? 512 : 1024; /* bytes of one 32 x 16 input chunk */
+    constexpr int NCB = 2 * KS;           /* 16-feature blocks per 32-sample row of chunks */
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ng = wave & 3, sh = wave >> 2; /* phase A: neurons 32 ng.., samples 128 sh.. */
+    const int r16 = lane & 15, q = lane >> 4;
+    const LaneOff lo = lane_offsets(lane);
+    char *imgH1 = lds + OFF_H1, *imgH2 = lds + OFF_H2, *imgD2 = lds + OFF_D2, *imgD3 = lds + OFF_D3;
+    char *imgW1 = lds + OFF_W1;
+
+    /* ---- once per launch: W1 -> LDS image, W2 / W2^T operand fragments -> registers ---- */
+    {
+        constexpr int PIECES = (H1 / 32) * (H2 / 16);
+        for (int p = wave; p < PIECES; p += 8) glds_t32_piece<H2>((const char *)W1, (size_t)H1 * 2, imgW1, p, lane);
+    }
+    bf16x8 w2f[2][2], w2tf[4]; /* P2: A = W2[o][h2] rows; P3: A = W2^T[h2][o] rows */
+#pragma unroll
+    for (int ot = 0; ot < 2; ot++)
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+            w2f[ot][kk] = *(const bf16x8 *)(W2 + (size_t)(16 * ot + r16) * H2 + 32 * kk + 8 * q);
+#pragma unroll
+    for (int ht = 0; ht < 4; ht++) w2tf[ht] = *(const bf16x8 *)(W2t + (size_t)(16 * ht + r16) * NO + 8 * q);
+    __builtin_amdgcn_s_waitcnt(0xF70); /* vmcnt(0): W1 pieces landed (their DMA is inline asm) */
+
+    f32x4 g1acc[4], g2acc; /* G1: h1 tile = wave, h2 tiles 0..3; G2: h2 tile w&3, o tile w>>2 */
+#pragma unroll
+    for (int i = 0; i < 4; i++) g1acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    g2acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    const int n_ot = n_out > 16 ? 2 : 1;
+    const float inv_nout = 1.0f / (float)n_out;
+
+    /* X^T stage image: row = feature within the k-step, column = sample of the tile.
+     * This lane converts slots 2i, 2i+1 (i = lane & 31) of chunk (t = wave, cb = 2s + lane/32). */
+    const int xi = lane & 31, xcbh = lane >> 5;
+    const int xg = xi >> 3;
+    int xoff[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 16 * xcbh + 2 * (xi & 7) + e;
+        xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
+    }
+
+    for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
+        const char *xbase = (const char *)Xg + ((size_t)(T0 + wave) * NCB + xcbh) * CHUNK + (size_t)xi * (16 * XN);
+        const __bf16 *wbase = W0f + ((size_t)(2 * ng) * KS * 64 + lane) * 8;
+
+        uint4 xr[KS][XN];
+        bf16x8 wr[KS][2];
+        auto issue = [&](int s) {
+            /* an opaque zero pins the loads to this point of the k-loop: the operands are
+             * read-only, so the compiler would otherwise hoist every W0 load out of the
+             * tile loop (50 live fragments: spills) */
+            unsigned int z = 0;
+            asm volatile("" : "+s"(z));
+#pragma unroll
+            for (int n = 0; n < XN; n++) xr[s][n] = *(const uint4 *)(xbase + z + (size_t)(2 * s) * CHUNK + 16 * n);
+#pragma unroll
+            for (int i = 0; i < 2; i++) wr[s][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + s) * 512);
+        };
+        auto convert = [&](int s) {
+            char *img = lds + OFF_XT + (s & 1) * IMG_XT;
+            bf16x8 v[2];
+            if constexpr (XU8) {
+                v[0] = u8x8_to_bf16(xr[s][0].x, xr[s][0].y, xscale);
+                v[1] = u8x8_to_bf16(xr[s][0].z, xr[s][0].w, xscale);
+            } else {
+                v[0] = __builtin_bit_cast(bf16x8, xr[s][0]);
+                v[1] = __builtin_bit_cast(bf16x8, xr[s][1]);
+            }
+            *(bf16x8 *)(img + xoff[0]) = v[0];
+            *(bf16x8 *)(img + xoff[1]) = v[1];
+        };
+
+        f32x4 acc[2][8];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int st = 0; st < 8; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        /* the previous tile's chain read H2 (= the X^T stages) and H1 */
+        lds_barrier();
+#pragma unroll
+        for (int s = 0; s <= D && s < KS; s++) issue(s);
+        convert(0);
+        lds_barrier();
+        /* ================= phase A: H1 = f(X W0^T) ================= */
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            if (s + D + 1 < KS) issue(s + D + 1);
+            const char *img = lds + OFF_XT + (s & 1) * IMG_XT;
+#pragma unroll
+            for (int st = 0; st < 8; st++) {
+                const bf16x8 b = rd_tr<XR>(img, lo, 0, 128 * sh + 16 * st);
+                acc[0][st] = mfma(wr[s][0], b, acc[0][st]);
+                acc[1][st] = mfma(wr[s][1], b, acc[1][st]);
+            }
+            if (s + 1 < KS) convert(s + 1);
+            lds_barrier();
+        }
+        /* H1 tile -> LDS image [sample][neuron] */
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int st = 0; st < 8; st++) {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r]);
+                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, 128 * sh + 16 * st, 32 * ng + 16 * i) = o;
+            }
+        lds_barrier();
+
+        /* ================= phase B: back chain on this wave's 32 samples ================= */
+        const int sw = 32 * wave;
+        int lab[2] = {-1, -1};
+        if constexpr (LABELS) {
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                int s = tile * TS + sw + 16 * st + r16;
+                s = s < n_valid ? s : (n_valid > 0 ? n_valid - 1 : 0);
+                lab[st] = labels[s];
+            }
+        }
+        /* P1: H2^T [h2][sample] = f(W1 H1^T) */
+#pragma unroll
+        for (int st = 0; st < 2; st++) {
+            const int r0 = sw + 16 * st;
+            f32x4 a[4];
+#pragma unroll
+            for (int ht = 0; ht < 4; ht++) a[ht] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < H1; k += 32) {
+                const bf16x8 b = rd_row<TS>(imgH1, lo, r0, k);
+#pragma unroll
+                for (int ht = 0; ht < 4; ht++) a[ht] = mfma(rd_row<H2>(imgW1, lo, 16 * ht, k), b, a[ht]);
+            }
+#pragma unroll
+            for (int ht = 0; ht < 4; ht++) {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[ht][r]);
+                *(bf16x4 *)wr_ptr<TS>(imgH2, lo, r0, 16 * ht) = o;
+            }
+        }
+        wave_lds_fence();
+        /* P2: logits, output activation, loss, delta3 -> D3 image */
+#pragma unroll
+        for (int st = 0; st < 2; st++) {
+            const int r0 = sw + 16 * st;
+            const int s = tile * TS + r0 + r16;
+            f32x4 z[2];
+            z[0] = z[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const bf16x8 b0 = rd_row<TS>(imgH2, lo, r0, 0), b1 = rd_row<TS>(imgH2, lo, r0, 32);
+            z[0] = mfma(w2f[0][0], b0, z[0]);
+            z[0] = mfma(w2f[0][1], b1, z[0]);
+            if (n_ot > 1) {
+                z[1] = mfma(w2f[1][0], b0, z[1]);
+                z[1] = mfma(w2f[1][1], b1, z[1]);
+                output_layer<TYPE, LABELS, TS, 2>(z, lab[st], T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
+                                                  r0, lane, inv_nout, my_loss, my_hit);
+            } else {
+                output_layer<TYPE, LABELS, TS, 1>(z, lab[st], T, ldt, t_hi, t_lo, s, s < n_valid, n_out, imgD3, lo,
+                                                  r0, lane, inv_nout, my_loss, my_hit);
+            }
+        }
+        wave_lds_fence();
+        /* P3: delta2^T [h2][sample] = (W2^T delta3^T) * f'(H2) */
+#pragma unroll
+        for (int st = 0; st < 2; st++) {
+            const int r0 = sw + 16 * st;
+            const bf16x8 b = rd_row<TS>(imgD3, lo, r0, 0);
+#pragma unroll
+            for (int ht = 0; ht < 4; ht++) {
+                const f32x4 a = mfma(w2tf[ht], b, f32x4{0.f, 0.f, 0.f, 0.f});
+                const bf16x4 h = *(const bf16x4 *)wr_ptr<TS>(imgH2, lo, r0, 16 * ht);
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)h[r]));
+                *(bf16x4 *)wr_ptr<TS>(imgD2, lo, r0, 16 * ht) = o;
+            }
+        }
+        wave_lds_fence();
+        /* P4: delta1 [sample][h1] = (delta2 W1) * f'(H1) -> HBM, fragment-major:
+         * chunk (32-sample row, h1 block) = [g][r][j] = delta1[32 t + 8 g + j][16 hb + r] */
+        {
+            __bf16 *chunk0 = D1 + (size_t)(T0 + wave) * (H1 / 16) * 512;
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                const int r0 = sw + 16 * st;
+                const bf16x8 d0 = rd_row<TS>(imgD2, lo, r0, 0), d1 = rd_row<TS>(imgD2, lo, r0, 32);
+#pragma unroll
+                for (int ht = 0; ht < 8; ht++) {
+                    f32x4 a = mfma(d0, rd_tr<H2>(imgW1, lo, 0, 16 * ht), f32x4{0.f, 0.f, 0.f, 0.f});
+                    a = mfma(d1, rd_tr<H2>(imgW1, lo, 32, 16 * ht), a);
+                    /* D[row = sample r0 + 4q + r][col = h1 16 ht + r16]; f'(H1) of those 4 samples */
+                    const s16x4 hr = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4 *)(imgH1 + t32<TS>(r0 + 4 * q + (r16 >> 2), 16 * ht + 4 * (r16 & 3))));
+                    const bf16x4 hv = __builtin_bit_cast(bf16x4, hr);
+                    bf16x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)hv[r]));
+                    const int g = 2 * st + (q >> 1);
+                    *(bf16x4 *)(chunk0 + (size_t)ht * 512 + (g * 16 + r16) * 8 + 4 * (q & 1)) = o;
+                }
+            }
+        }
+        lds_barrier();
+
+        /* ================= phase C: G1, G2 over the tile's 256 samples ================= */
+#pragma unroll
+        for (int k = 0; k < TS; k += 32) {
+            const bf16x8 a = rd_tr<TS>(imgH1, lo, k, 16 * wave); /* A[h1][sample] */
+#pragma unroll
+            for (int t2 = 0; t2 < 4; t2++) g1acc[t2] = mfma(a, rd_tr<TS>(imgD2, lo, k, 16 * t2), g1acc[t2]);
+        }
+        if ((wave >> 2) < n_ot) {
+#pragma unroll
+            for (int k = 0; k < TS; k += 32)
+                g2acc = mfma(rd_tr<TS>(imgH2, lo, k, 16 * (wave & 3)), rd_tr<TS>(imgD3, lo, k, 16 * (wave >> 2)), g2acc);
+        }
+    }
+
+    /* ---- the block's [G1 (H2 x H1) | G2 (NO x H2)] slab ---- */
+    float *slab = gslab + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+    for (int t2 = 0; t2 < 4; t2++) /* D[h1 = 16w + 4q + r][h2 = 16 t2 + r16] */
+        *(f32x4 *)(slab + (size_t)(t2 * 16 + r16) * H1 + wave * 16 + 4 * q) = g1acc[t2];
+    /* D[h2 = 16 (w&3) + 4q + r][o = 16 (w>>2) + r16] */
+    *(f32x4 *)(slab + H2 * H1 + (size_t)((wave >> 2) * 16 + r16) * H2 + (wave & 3) * 16 + 4 * q) = g2acc;
+    lds_barrier();
+    float *sl = (float *)(lds + OFF_D3);
+    unsigned int *shh = (unsigned int *)(lds + OFF_D3 + 64);
+    my_loss = wave_sum(my_loss);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) my_hit += __shfl_xor(my_hit, o, 64);
+    if (lane == 0) {
+        sl[wave] = my_loss;
+        shh[wave] = my_hit;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float a = 0.f;
+        unsigned int h = 0;
+        for (int w = 0; w < 8; w++) {
+            a += sl[w];
+            h += shh[w];
+        }
+        if (loss_acc) atomicAdd(loss_acc + HPNN_STAT_SLOT(blockIdx.x), a);
+        if (correct) atomicAdd(correct + HPNN_STAT_SLOT(blockIdx.x), h);
+    }
+}
+
+int g_tile_cus = 0;
+
+template <int TYPE, bool LABELS, int KS, bool XU8>
+int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, const void *W2, const void *W2t,
+                const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
+                float *loss_acc, unsigned int *correct, int n_tiles, int n_valid, int n_out, int grid,
+                hipStream_t stream) {
+    constexpr int D = 3;
+    auto kern = mlp3_tile_kernel<TYPE, LABELS, KS, XU8, D>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), LDS_TOTAL, stream, Xg, xscale, (const __bf16 *)W0f,
+                       (const __bf16 *)W1, (const __bf16 *)W2, (const __bf16 *)W2t, labels, T, ldt, t_hi, t_lo,
+                       (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
+    return hipGetLastError() == hipSuccess ? grid : -5;
+}
+
+template <int KS>
+int launch_tile_k(const void *Xg, int xu8, float xscale, const void *W0f, const void *W1, const void *W2,
+                  const void *W2t, const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1,
+                  float *gslab, float *loss_acc, unsigned int *correct, int n_tiles, int n_valid, int n_out, int type,
+                  int grid, hipStream_t stream) {
+#define HPNN_TL(TY, LB, U8)                                                                                     \
+    return launch_tile<TY, LB, KS, U8>(Xg, xscale, W0f, W1, W2, W2t, labels, T, ldt, t_hi, t_lo, D1, gslab,     \
+                                       loss_acc, correct, n_tiles, n_valid, n_out, grid, stream)
+#define HPNN_TL2(TY, LB)       \
+    if (xu8) HPNN_TL(TY, LB, true); \
+    HPNN_TL(TY, LB, false)
+    if (labels) {
+        if (type == 2) { HPNN_TL2(2, true); }
+        if (type == 0) { HPNN_TL2(0, true); }
+        HPNN_TL2(1, true);
+    }
+    if (type == 2) { HPNN_TL2(2, false); }
+    if (type == 0) { HPNN_TL2(0, false); }
+    HPNN_TL2(1, false);
+#undef HPNN_TL2
+#undef HPNN_TL
+}
+
+}  // namespace
+
+extern "C" int hpnn_mlp3_tile_grid(int Bp, int grid) {
+    if (Bp <= 0 || Bp % TS) return -2;
+    if (g_tile_cus <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&g_tile_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            g_tile_cus = 256;
+    }
+    const int n_tiles = Bp / TS;
+    if (grid <= 0) grid = g_tile_cus;
+    return grid < n_tiles ? grid : n_tiles;
+}
+
+extern "C" int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0f, const void *W1,
+                              const void *W2, const void *W2t, const int *labels, const float *T, int ldt,
+                              float t_hi, float t_lo, void *D1, float *gslab, float *loss_acc,
+                              unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
+                              hipStream_t stream) {
+    if (Bp <= 0 || Bp % TS || n_out > NO || n_out < 1) return -2;
+    if (!labels && !T) return -1;
+    if (((uintptr_t)Xg | (uintptr_t)W0f | (uintptr_t)W1 | (uintptr_t)W2 | (uintptr_t)W2t | (uintptr_t)D1 |
+         (uintptr_t)gslab) & 15)
+        return -4;
+    grid = hpnn_mlp3_tile_grid(Bp, grid);
+    if (grid <= 0) return -2;
+    const int n_tiles = Bp / TS;
+#define HPNN_TK(K_)                                                                                              \
+    if (K0 == K_)                                                                                                \
+    return launch_tile_k<K_ / 32>(Xg, xu8, xscale, W0f, W1, W2, W2t, labels, T, ldt, t_hi, t_lo, D1, gslab,     \
+                                  loss_acc, correct, n_tiles, n_valid, n_out, type, grid, stream)
+    HPNN_TK(800);
+    HPNN_TK(256);
+#undef HPNN_TK
+    return -3;
+}

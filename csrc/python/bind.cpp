@@ -132,6 +132,16 @@ PYBIND11_MODULE(_native, m) {
         check(hpnn_mlp3_fused_trace(v.data()), "mlp3_fused_trace");
         return v;
     });
+    m.def("mlp3_tile", [](uptr Xg, int xu8, float xscale, int K0, uptr W0f, uptr W1, uptr W2, uptr W2t, uptr labels,
+                          uptr T, int ldt, float t_hi, float t_lo, uptr D1, uptr gslab, uptr loss, uptr correct, int Bp,
+                          int n_valid, int n_out, int type, int grid, uptr stream) {
+        const int rc = hpnn_mlp3_tile(P(Xg), xu8, xscale, K0, P(W0f), P(W1), P(W2), P(W2t), (const int *)P(labels),
+                                      (const float *)P(T), ldt, t_hi, t_lo, P(D1), (float *)P(gslab), (float *)P(loss),
+                                      (unsigned int *)P(correct), Bp, n_valid, n_out, type, grid, S(stream));
+        if (rc <= 0) check(rc ? rc : -1, "mlp3_tile");
+        return rc;
+    });
+    m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
     m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, int h_u8, float hscale, uptr slab, int ldg, int N, int M,
                            int Bt, int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,

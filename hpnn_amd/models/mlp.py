@@ -40,6 +40,9 @@ _G0_FM_U8 = os.environ.get("HPNN_G0_FM_U8", "1") == "1"
 # the value a uint8 input means (1/255: MNIST pixels normalised to [0, 1])
 PIXEL_SCALE = float(torch.tensor(float(os.environ.get("HPNN_PIXEL_SCALE", str(1.0 / 255.0))),
                                  dtype=torch.float32).item())
+# HPNN_TILE=0: the 32-sample pipelined front (mlp3_fused, "x") instead of the 256-sample
+# tile kernel (mlp3_tile, "t") on eligible MNIST-shaped nets
+_TILE = os.environ.get("HPNN_TILE", "0") != "0"
 # HPNN_G0_RS=1: first-layer gradient with the register-staged TN kernel (kernels_g0.hip):
 # 75.46-76.57 us/step vs 75.73-77.32 with the LDS-DMA TN kernel (scripts/gpu_ab_g0.sh),
 # within noise of each other
@@ -128,12 +131,13 @@ class MLP:
         #   "mid" : gemm_nt layer 0 + mlp3_mid (H1 -> delta1)
         eligible = self.L == 3 and tuple(self.Np) == ops.MLP3_DIMS
         x_ok = eligible and self.Kp[0] in ops.MLP3F_K0
+        t_ok = eligible and self.Kp[0] in ops.MLP3T_K0 and self.Bp % ops.MLP3T_TILE == 0
         if fused is None or fused is True:
-            mode = "x" if x_ok else ("mid" if eligible else None)
+            mode = "t" if (t_ok and _TILE) else ("x" if x_ok else ("mid" if eligible else None))
             if fused is True and mode is None:
                 raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
-        elif fused in ("x", "mid"):
-            if not (x_ok if fused == "x" else eligible):
+        elif fused in ("x", "mid", "t"):
+            if not {"x": x_ok, "mid": eligible, "t": t_ok}[fused]:
                 raise ValueError(f"fused={fused!r} not available for dims {self.Kp[0]}-{self.Np}")
             mode = fused
         else:
@@ -145,8 +149,8 @@ class MLP:
             grid = max(1, min(mid_grid, self.Bp // 64))
             self.midslab = torch.empty(grid, ops.MLP3_SLAB, dtype=torch.float32, device=dev)
             self.midtmp = torch.empty(16 * self.midslab.shape[1], dtype=torch.float32, device=dev)
-        elif mode == "x":
-            grid = ops.mlp3_fused_grid(self.Bp, dev)
+        elif mode in ("x", "t"):
+            grid = ops.mlp3_fused_grid(self.Bp, dev) if mode == "x" else ops.mlp3_tile_grid(self.Bp, dev)
             self.midslab = torch.empty(grid, ops.MLP3_SLAB, dtype=torch.float32, device=dev)
             self.mid_groups = min(16, grid)
             self.midtmp = torch.empty(16 * ops.MLP3_SLAB, dtype=torch.float32, device=dev)
@@ -218,6 +222,8 @@ class MLP:
         LDS transposes -- and converts it exactly as above.  HPNN_G0_FM=1 attaches a
         fragment-major BF16 copy for float input too (off by default, see _G0_FM)."""
         Xd = X.to(self.device)
+        if self.fused_mode == "t":
+            return self._prepare_fm(Xd)
         rows = ops.pad_to(X.shape[0], 128)
         out = torch.empty(rows, self.Kp[0], dtype=torch.bfloat16, device=self.device)
         if Xd.dtype == torch.uint8:
@@ -234,8 +240,44 @@ class MLP:
             out.hpnn_fm_scale = 1.0
         return out
 
+    def _prepare_fm(self, Xd):
+        """tile path ("t"): the batch itself fragment-major ([rows/32, Kp0/16, 64, 8],
+        ops.to_fragment_major), 8-bit pixels kept as bytes (the kernels use bf16(x *
+        PIXEL_SCALE)), anything else as BF16.  Both the front kernel and the first-layer
+        gradient kernel stream this one buffer."""
+        rows = ops.pad_to(Xd.shape[0], ops.MLP3T_TILE)
+        if Xd.dtype == torch.uint8:
+            u8 = torch.zeros(rows, self.Kp[0], dtype=torch.uint8, device=self.device)
+            u8[:Xd.shape[0], :Xd.shape[1]] = Xd
+            out = ops.to_fragment_major(u8).view(rows // 32, self.Kp[0] // 16, 64, 8)
+            out.hpnn_fm_scale = PIXEL_SCALE
+        else:
+            b = torch.empty(rows, self.Kp[0], dtype=torch.bfloat16, device=self.device)
+            ops.pack_bf16(Xd.contiguous(), b)
+            out = ops.to_fragment_major(b).view(rows // 32, self.Kp[0] // 16, 64, 8)
+            out.hpnn_fm_scale = 1.0
+        out.hpnn_fm_rows = rows
+        return out
+
+    @staticmethod
+    def _is_fm(X):
+        return X.dim() >= 4
+
+    def _rowmajor(self, X):
+        """row-major BF16 [rows, Kp0] view of a prepared batch (fragment-major input of the
+        tile path is converted; the per-layer kernels need rows)"""
+        if not self._is_fm(X):
+            return X
+        rows = X.shape[0] * 32
+        R = ops.from_fragment_major(X, rows, X.shape[1] * 16)
+        if X.dtype == torch.uint8:
+            return (R.float() * getattr(X, "hpnn_fm_scale", PIXEL_SCALE)).bfloat16()
+        return R.contiguous()
+
     def _fm_input(self, X):
         """the fragment-major copy of a prepared batch X (prepare_input), or None"""
+        if self._is_fm(X):
+            return X if X.shape[0] * 32 == self.Bp else None
         Xg = getattr(X, "hpnn_fm", None)
         if Xg is None or X.shape[0] != self.Bp or Xg.numel() != X.shape[0] * self.Kp[0]:
             return None
@@ -243,6 +285,7 @@ class MLP:
 
     # ------------------------------------------------------------------ phases
     def forward(self, X):
+        X = self._rowmajor(X)
         for l in range(self.L):
             A = X if l == 0 else self.H[l - 1]
             if l == self.L - 1:
@@ -262,7 +305,7 @@ class MLP:
 
     def grad_layer(self, l, X, reduce=False):
         Hin = X if l == 0 else self.H[l - 1]
-        Xg = self._fm_input(X) if l == 0 and self.fused_mode == "x" else None
+        Xg = self._fm_input(X) if l == 0 and self.fused_mode in ("x", "t") else None
         if Xg is not None:  # delta1 came fragment-major from the fused front
             ops.gemm_fm_direct(self.D[0], Xg, self.Np[0], self.Kp[0], splits=self.S[0], out=self.slab[0],
                                hscale=getattr(X, "hpnn_fm_scale", 1.0))
@@ -331,7 +374,10 @@ class MLP:
         t_hi, t_lo = self._t_hilo()
         kw = dict(labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid, loss_acc=self.stats[0, 0:1],
                   correct=self.stats[0, 1:2])
-        if self.fused_mode == "x":
+        if self.fused_mode == "t":
+            ops.mlp3_tile(X, self.Kp[0], self.Wb[0], self.W0f, self.Wb[1], self.Wb[2], self.Wt[2], self.D[0],
+                          self.midslab, self.n_out, self.type, xscale=getattr(X, "hpnn_fm_scale", 1.0), **kw)
+        elif self.fused_mode == "x":
             ops.mlp3_fused(X, self.Wb[0], self.W0f, self.Wb[1], self.Wb[2], self.D[0], self.midslab, self.n_out,
                            self.type, d1_fm=self._fm_input(X) is not None, **kw)
         else:
@@ -356,7 +402,7 @@ class MLP:
         """One minibatch fwd + bwd + update on the current stream (no host sync)."""
         n_valid = self.Bp if n_valid is None else n_valid
         scale = 1.0 / n_valid
-        if self.fused_mode == "x":
+        if self.fused_mode in ("x", "t"):
             # 4 launches: fused front, then the G0 GEMM and the first [G1|G2] reduction pass
             # side by side (the reduction forks onto a second stream: it only needs the
             # fused front's block slabs and fills CUs the memory-bound GEMM leaves idle),
@@ -410,7 +456,7 @@ class MLP:
 
     def predict(self, X, n_valid=None):
         """network outputs [n_valid, n_out] (fp32)."""
-        n_valid = X.shape[0] if n_valid is None else n_valid
+        n_valid = (X.shape[0] * 32 if self._is_fm(X) else X.shape[0]) if n_valid is None else n_valid
         self.forward(X)
         O = torch.empty(self.Bp, self.Np[-1], dtype=torch.float32, device=self.device)
         Tz = torch.zeros(self.Bp, self.n_out, dtype=torch.float32, device=self.device)

@@ -264,6 +264,47 @@ def mlp3_fused(X, W0, W0f, W1, W2, D1, gslab, n_out, net_type, labels=None, T=No
     return D1
 
 
+MLP3T_K0 = (256, 800)  # first-layer input widths of hpnn_mlp3_tile
+MLP3T_TILE = 256  # samples per tile (the batch must be a multiple)
+
+
+def mlp3_tile_grid(Bp, device=None):
+    """workgroups (= gradient slab rows) hpnn_mlp3_tile uses for Bp samples."""
+    if device is not None and torch.device(device).type == "cpu":
+        return 1
+    g = native().mlp3_tile_grid(int(Bp), 0)
+    if g <= 0:
+        raise ValueError(f"mlp3_tile: batch {Bp} not a multiple of {MLP3T_TILE}")
+    return g
+
+
+def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=None, T=None, t_hi=1.0, t_lo=0.0,
+              n_valid=None, loss_acc=None, correct=None, xscale=1.0):
+    """The n_in-128-64-(<=32) step up to delta1 with 256-sample tiles
+    (csrc/gpu/kernels_mlp3t.hip): Xg fragment-major [Bp/32, K0/16, 64, 8] (to_fragment_major)
+    uint8 (used as bf16(x * xscale)) or bf16 -> delta1 fragment-major into D1g
+    [Bp/32, 8, 64, 8] bf16, per-block [G1 | G2] slabs into gslab [grid, MLP3_SLAB],
+    loss / hits.  W0f: fragment-major BF16 W0 (frag_major); W0 (row-major) is used by the
+    CPU emulation only; W2t: W2^T [64, 32] BF16."""
+    Bp = Xg.shape[0] * 32
+    n_valid = Bp if n_valid is None else int(n_valid)
+    u8 = Xg.dtype == torch.uint8
+    if _cpu(Xg):
+        X = from_fragment_major(Xg, Bp, K0)
+        Xb = (X.float() * xscale).bfloat16() if u8 else X
+        H1 = bipolar(Xb.float() @ W0.float().t()).bfloat16()
+        D1 = torch.empty(Bp, 128, dtype=torch.bfloat16)
+        _cpu_mlp3_mid(H1, W1, None, W2, None, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid, loss_acc,
+                      correct)
+        D1g.view(-1).copy_(to_fragment_major(D1).view(-1))
+        return D1g
+    native().mlp3_tile(Xg.data_ptr(), int(u8), float(xscale), K0, W0f.data_ptr(), W1.data_ptr(), W2.data_ptr(),
+                       W2t.data_ptr(), _ptr(labels), _ptr(T), T.stride(0) if T is not None else 0, float(t_hi),
+                       float(t_lo), D1g.data_ptr(), gslab.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid,
+                       n_out, net_type, gslab.shape[0], _stream())
+    return D1g
+
+
 def frag_major(W):
     """[N, K] -> flat MFMA-fragment-major copy (layout of hpnn_sgd_update_multi's Wf):
     element (n, k) at (((n//16)*(K//32) + k//32)*64 + n%16 + 16*((k//8)%4))*8 + k%8."""

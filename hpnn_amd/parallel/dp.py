@@ -128,7 +128,7 @@ class DataParallel:
         n_valid = m.Bp if n_valid is None else n_valid
         if not self.active:
             return m.train_step(X, labels=labels, T=T, n_valid=n_valid, lr=lr, alpha=alpha)
-        if (self.native is not None and self.native.xar and getattr(m, "fused_mode", None) == "x"
+        if (self.native is not None and self.native.xar and getattr(m, "fused_mode", None) in ("x", "t")
                 and m.grad_flat.numel() * 4 <= self.native.xar_max
                 and m.grad_flat.numel() - m.G[0].numel() == ops.MLP3_SLAB):
             return self._fused_xgmi_step(X, labels, T, n_valid, lr, alpha)

@@ -24,9 +24,11 @@ def _data(rank, step, u8=False):
     return x, torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
 
 
-def _worker(rank, world, port, graph, q, u8=False):
+def _worker(rank, world, port, graph, q, u8=False, xar_mode=None):
     try:
         os.environ["LOCAL_WORLD_SIZE"] = str(world)
+        if xar_mode is not None:  # 1 one-shot, 2 two-shot (the default from 4 ranks), unset: auto
+            os.environ["HPNN_XAR_MODE"] = str(xar_mode)
         os.environ["HPNN_XAR_TIMEOUT_MS"] = "2000"
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -35,7 +37,7 @@ def _worker(rank, world, port, graph, q, u8=False):
         dev = torch.device("cuda", 0)
         m = MLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=3)
         dp = DataParallel(m, comm="xar")
-        assert dp.native is not None and dp.native.xar and m.fused_mode == "x"
+        assert dp.native is not None and dp.native.xar and m.fused_mode in ("x", "t")
         dp.broadcast_parameters()
         batches = []
         for step in range(3):
@@ -70,27 +72,25 @@ def _worker(rank, world, port, graph, q, u8=False):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def _reference(u8=False):
+def _reference(u8=False, world=2):
     from hpnn_amd.models import MLP
     dev = torch.device("cuda", 0)
-    m = MLP(SIZES, "SNN", batch=2 * B, device=dev, momentum=True, seed=3)
+    m = MLP(SIZES, "SNN", batch=world * B, device=dev, momentum=True, seed=3)
     for step in (0, 1, 1):
-        xs, ls = zip(*[_data(r, step, u8) for r in range(2)])
+        xs, ls = zip(*[_data(r, step, u8) for r in range(world)])
         X = m.prepare_input(torch.cat(xs).to(dev))
         m.train_step(X, labels=torch.cat(ls).to(dev), lr=0.05, alpha=0.2)
     torch.cuda.synchronize()
     return torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("graph,u8", [(False, False), (True, False), (True, True)])
-def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph, u8):
+def _run(world, graph, u8, xar_mode=None):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, graph, q, u8)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=110) for _ in ps)
@@ -98,9 +98,25 @@ def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph, u8):
         p.join(timeout=30)
         if p.is_alive():
             p.kill()
-    for r in (0, 1):
+    for r in range(world):
         assert isinstance(res[r], torch.Tensor), res[r]
-    assert torch.equal(res[0], res[1])  # deterministic, identical on every rank
-    ref = _reference(u8)
+    for r in range(1, world):
+        assert torch.equal(res[0], res[r])  # deterministic, identical on every rank
+    ref = _reference(u8, world)
     err = (res[0] - ref).abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph,u8", [(False, False), (True, False), (True, True)])
+def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph, u8):
+    _run(2, graph, u8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,xar_mode", [(2, 2), (3, 2), (4, None)])
+def test_dp_step_two_shot_with_fused_update(gpu, world, xar_mode):
+    """the two-shot all-reduce with the optimizer step fused in (each rank updates its own
+    shard in the reduce phase and the peers' shards after the gather): forced at 2 and 3
+    ranks, and the auto choice at 4 ranks (two-shot from 4 ranks and 64 KiB)"""
+    _run(world, True, True, xar_mode)
