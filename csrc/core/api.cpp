@@ -608,18 +608,52 @@ extern "C" void _NN(run, kernel)(nn_def *conf) {
     if (conf->seed == 0) conf->seed = (UINT)time(NULL);
     const bool gpu = use_gpu(conf);
     std::vector<UINT> order = seeded_order((UINT)src.size(), conf->seed);
-    for (UINT idx : order) {
+    /* GPU: the whole test set goes through the batched engine of the model's precision
+     * ([dtype], default f64 = the reference's) in one call -- one launch sequence and one
+     * device-to-host copy per block of samples instead of one kernel launch, copy and host
+     * sync per file; the per-file lines below are then produced from the outputs.
+     * HPNN_RUN_ONLINE=1 keeps the reference's one-forward-per-file loop. */
+    const char *ro = getenv("HPNN_RUN_ONLINE");
+    const bool batched = gpu && !(ro && ro[0] == '1');
+    std::vector<DOUBLE> Xall, Tall, Yall;
+    std::vector<long> row_of(order.size(), -1);
+    if (batched) {
+        long rows = 0;
+        for (size_t p = 0; p < order.size(); p++) {
+            DOUBLE *in = NULL, *out = NULL;
+            if (!src.get(order[p], &in, &out)) continue;
+            Xall.insert(Xall.end(), in, in + k->n_inputs);
+            Tall.insert(Tall.end(), out, out + k->n_outputs);
+            row_of[p] = rows++;
+            free(in);
+            free(out);
+        }
+        Yall.assign((size_t)rows * k->n_outputs, 0.0);
+        if (rows > 0 && !hpnn_gpu_infer_batched(k, conf->type, conf->dtype, Xall.data(), (UINT)rows, Yall.data())) {
+            NN_ERROR(stderr, "batched GPU evaluation failed\n");
+            return;
+        }
+    }
+    for (size_t p = 0; p < order.size(); p++) {
+        const UINT idx = order[p];
         const std::string &f = src.names[idx];
         NN_OUT(stdout, "TESTING FILE: %16.16s\t", f.c_str());
         DOUBLE *in = NULL, *out = NULL;
-        if (!src.get(idx, &in, &out)) continue;
-        if (gpu) {
-            hpnn_gpu_forward(k, conf->type, in);
+        const DOUBLE *o;
+        if (batched) {
+            if (row_of[p] < 0) continue;
+            o = Yall.data() + (size_t)row_of[p] * k->n_outputs;
+            out = Tall.data() + (size_t)row_of[p] * k->n_outputs;
         } else {
-            memcpy(k->in, in, sizeof(DOUBLE) * k->n_inputs);
-            hpnn_cpu_forward(k, conf->type);
+            if (!src.get(idx, &in, &out)) continue;
+            if (gpu) {
+                hpnn_gpu_forward(k, conf->type, in);
+            } else {
+                memcpy(k->in, in, sizeof(DOUBLE) * k->n_inputs);
+                hpnn_cpu_forward(k, conf->type);
+            }
+            o = k->output.vec;
         }
-        const DOUBLE *o = k->output.vec;
         UINT guess, truth = 0;
         DOUBLE res;
         if (conf->type == NN_TYPE_ANN) {
@@ -657,8 +691,10 @@ extern "C" void _NN(run, kernel)(nn_def *conf) {
             NN_COUT(stdout, " [FAIL idx=%u]\n", truth + 1);
         }
         fflush(stdout);
-        free(in);
-        free(out);
+        if (!batched) {
+            free(in);
+            free(out);
+        }
     }
     if (hpnn_metrics_active()) {
         char buf[128];

@@ -313,7 +313,21 @@ int pick_splits(int Np, int Kp, int Bp) {
     return s < 1 ? 1 : s;
 }
 
+BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t s);
+
 struct Batched {
+    /* what the precision-generic drivers (train_batched, train_dp, train_dp_mp) need */
+    typedef float target_t; /* dense targets, uploaded once */
+    typedef float grad_t;   /* flat gradient buffer (the all-reduce payload) */
+    static constexpr size_t xelem = 2;
+    static constexpr hpnn_comm_dtype comm_dt = HPNN_DT_F32;
+    static const char *name() { return "bf16"; }
+    static BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t st) {
+        return upload_bf16(src, rows, cols, rows_p, cols_p, dst, st);
+    }
+    static int reduce_sum(grad_t *buf, int G, size_t count, hipStream_t st) {
+        return hpnn_reduce_slabs(buf, G, (long)count, (long)count, buf, st);
+    }
     int L = 0, Bp = 0, n_out = 0, type = 2;
     int M[16], N[16], Kp[16], Np[16], S[16];
     float *W32[16] = {0}, *V32[16] = {0}, *slab[16] = {0};
@@ -666,6 +680,222 @@ BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, 
     return TRUE;
 }
 
+/* FP64 / FP32 batched engine ([dtype] f64 | f32): the reference's precision (the
+ * reference computes in double throughout, cuda_ann.cu:41-148, 546-548, 2139-2142) on the
+ * FP64 / FP32 MFMA kernels of kernels_fp.hip.  Same minibatch semantics as the FP64 CPU
+ * oracle (cpu_batched.cpp) and as Batched: forward, output delta, deltas with the
+ * pre-update weights, G = sum over the batch, W updated with scale = 1 / n_valid.  No
+ * padding: the kernels take any shape; the backward delta reads W itself (transposed
+ * operand), so no W^T copy is kept. */
+template <typename T>
+struct BatchedFP {
+    typedef T target_t;
+    typedef T grad_t;
+    static constexpr int F64 = sizeof(T) == 8 ? 1 : 0;
+    static constexpr size_t xelem = sizeof(T);
+    static constexpr hpnn_comm_dtype comm_dt = sizeof(T) == 8 ? HPNN_DT_F64 : HPNN_DT_F32;
+    static const char *name() { return sizeof(T) == 8 ? "f64" : "f32"; }
+    static constexpr size_t ACC_BYTES = Batched::ACC_BYTES;
+    int L = 0, Bp = 0, n_out = 0, type = 2;
+    int M[16], N[16], S[16];
+    int Kp[16]; /* Kp[0] = n_in: the row pitch of the uploaded input (drivers index rows by it) */
+    T *W[16] = {0}, *V[16] = {0}, *slab[16] = {0}, *H[16] = {0}, *D[16] = {0};
+    T *Z = nullptr, *gflat = nullptr;
+    float *acc = nullptr;
+    bool own_flat = false;
+    size_t goff[17] = {0};
+    hipStream_t s = nullptr;
+
+    static BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t st) {
+        std::vector<T> h((size_t)rows_p * cols_p, (T)0);
+        for (int r = 0; r < rows; r++)
+            for (int c = 0; c < cols; c++) h[(size_t)r * cols_p + c] = (T)src[(size_t)r * cols + c];
+        HIPCHK(hpnn_dev_malloc(dst, h.size() * sizeof(T)));
+        HIPCHK(hipMemcpyAsync(*dst, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return TRUE;
+    }
+    static int reduce_sum(grad_t *buf, int G, size_t count, hipStream_t st) {
+        return hpnn_reduce_fp(F64, buf, buf, G, (long)count, (long)count, st);
+    }
+
+    ~BatchedFP() {
+        if (s) hipStreamSynchronize(s);
+        for (int l = 0; l < 16; l++) {
+            hpnn_dev_free(W[l]);
+            hpnn_dev_free(V[l]);
+            hpnn_dev_free(slab[l]);
+            hpnn_dev_free(H[l]);
+            hpnn_dev_free(D[l]);
+        }
+        hpnn_dev_free(Z);
+        hpnn_dev_free(acc);
+        if (own_flat) hpnn_dev_free(gflat);
+    }
+
+    BOOL read_stats(double *loss, unsigned int *hits) {
+        std::vector<float> h(HPNN_STAT_SLOTS * HPNN_STAT_STRIDE);
+        HIPCHK(hipMemcpyAsync(h.data(), acc, ACC_BYTES, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double l = 0.0;
+        unsigned int c = 0;
+        for (int i = 0; i < HPNN_STAT_SLOTS; i++) {
+            l += h[(size_t)i * HPNN_STAT_STRIDE];
+            unsigned int u;
+            memcpy(&u, &h[(size_t)i * HPNN_STAT_STRIDE + 1], 4);
+            c += u;
+        }
+        *loss = l;
+        *hits = c;
+        return TRUE;
+    }
+
+    /* split-K factor of a weight gradient over the batch: ~256 workgroups, >= 256 rows each */
+    static int pick(int Nn, int Mm, int B) {
+        const int tiles = ((Nn + 63) / 64) * ((Mm + 63) / 64);
+        int sp = (256 + tiles - 1) / tiles;
+        const int maxs = B / 256 > 0 ? B / 256 : 1;
+        sp = sp < maxs ? sp : maxs;
+        return hpnn_gemm_fp_splits(B, sp < 1 ? 1 : sp);
+    }
+
+    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st) {
+        s = st;
+        L = (int)k->n_hiddens + 1;
+        Bp = B;
+        n_out = (int)k->n_outputs;
+        type = t == NN_TYPE_ANN ? 0 : (t == NN_TYPE_LNN ? 1 : 2);
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            M[l] = (int)ly->n_inputs;
+            N[l] = (int)ly->n_neurons;
+            Kp[l] = M[l];
+            S[l] = pick(N[l], M[l], Bp);
+            const size_t nw = (size_t)N[l] * M[l];
+            HIPCHK(hpnn_dev_malloc(&W[l], nw * sizeof(T)));
+            HIPCHK(hpnn_dev_malloc(&slab[l], nw * sizeof(T) * S[l]));
+            if (momentum) {
+                HIPCHK(hpnn_dev_malloc(&V[l], nw * sizeof(T)));
+                HIPCHK(hipMemsetAsync(V[l], 0, nw * sizeof(T), s));
+            }
+            HIPCHK(hpnn_dev_malloc(&D[l], (size_t)Bp * N[l] * sizeof(T)));
+            if (l < L - 1) HIPCHK(hpnn_dev_malloc(&H[l], (size_t)Bp * N[l] * sizeof(T)));
+            std::vector<T> tmp(nw);
+            for (size_t i = 0; i < nw; i++) tmp[i] = (T)ly->weights[i];
+            HIPCHK(hipMemcpyAsync(W[l], tmp.data(), nw * sizeof(T), hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        HIPCHK(hpnn_dev_malloc(&Z, (size_t)Bp * N[L - 1] * sizeof(T)));
+        HIPCHK(hpnn_dev_malloc(&acc, ACC_BYTES));
+        HIPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
+        return TRUE;
+    }
+
+    BOOL forward(const void *X, int rows) {
+        for (int l = 0; l < L; l++) {
+            const T *A = l ? H[l - 1] : (const T *)X;
+            const bool last = l == L - 1;
+            int r = hpnn_gemm_fp(F64, A, M[l], 0, W[l], M[l], 0, last ? (void *)Z : H[l], N[l], nullptr, 0, rows, N[l],
+                                 M[l], last ? HPNN_EPI_NONE : HPNN_EPI_ACT, 1, 0, s);
+            if (r) {
+                NN_ERROR(stderr, "gemm_fp (fwd layer %d) failed: %d\n", l, r);
+                return FALSE;
+            }
+        }
+        return TRUE;
+    }
+
+    /* forward + output delta + hidden deltas + weight gradients (slab[l], S[l] slabs) */
+    BOOL backprop(const void *X, const T *Tt, int ldt, int n_valid) {
+        if (!forward(X, Bp)) return FALSE;
+        if (hpnn_output_fp(F64, Z, N[L - 1], Tt, ldt, D[L - 1], N[L - 1], nullptr, 0, nullptr, acc,
+                           (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
+            return FALSE;
+        for (int l = L - 1; l >= 1; l--) {
+            /* D[l-1] = (D[l] W_l) * f'(H[l-1]): B(n = input m, k = neuron j) = W_l[j][m] */
+            if (hpnn_gemm_fp(F64, D[l], N[l], 0, W[l], M[l], 1, D[l - 1], N[l - 1], H[l - 1], N[l - 1], Bp, M[l], N[l],
+                             HPNN_EPI_DACT, 1, 0, s))
+                return FALSE;
+        }
+        for (int l = 0; l < L; l++) {
+            /* G[n][m] = sum_b D[b][n] H[b][m]: both operands transposed (k = the batch row) */
+            const T *Hin = l ? H[l - 1] : (const T *)X;
+            if (hpnn_gemm_fp(F64, D[l], N[l], 1, Hin, M[l], 1, slab[l], M[l], nullptr, 0, N[l], M[l], Bp,
+                             HPNN_EPI_NONE, S[l], (long)N[l] * M[l], s))
+                return FALSE;
+        }
+        return TRUE;
+    }
+
+    BOOL step(const void *X, const T *Tt, int ldt, int n_valid, double lr, double alpha, bool mom) {
+        if (!backprop(X, Tt, ldt, n_valid)) return FALSE;
+        const double scale = 1.0 / (double)n_valid;
+        for (int l = 0; l < L; l++)
+            if (hpnn_update_fp(F64, W[l], V[l], slab[l], S[l], (long)N[l] * M[l], (long)N[l] * M[l], lr, alpha, scale,
+                               mom ? 1 : 0, s))
+                return FALSE;
+        return hpnn_debug_check("batched training step (fp)") == 0;
+    }
+
+    BOOL alloc_flat(T *external = nullptr) {
+        goff[0] = 0;
+        for (int l = 0; l < L; l++) goff[l + 1] = goff[l] + (size_t)N[l] * M[l];
+        if (external) {
+            gflat = external;
+            own_flat = false;
+            return TRUE;
+        }
+        HIPCHK(hpnn_dev_malloc(&gflat, goff[L] * sizeof(T)));
+        own_flat = true;
+        return TRUE;
+    }
+    size_t flat_count() const { return goff[L]; }
+
+    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid) {
+        if (!backprop(X, Tt, ldt, n_valid)) return FALSE;
+        for (int l = 0; l < L; l++)
+            if (hpnn_reduce_fp(F64, gflat + goff[l], slab[l], S[l], (long)N[l] * M[l], (long)N[l] * M[l], s))
+                return FALSE;
+        return TRUE;
+    }
+
+    BOOL update_flat(const T *G, double lr, double alpha, double scale, bool mom) {
+        for (int l = 0; l < L; l++)
+            if (hpnn_update_fp(F64, W[l], V[l], G + goff[l], 1, 0, (long)N[l] * M[l], lr, alpha, scale, mom ? 1 : 0, s))
+                return FALSE;
+        return TRUE;
+    }
+
+    BOOL download(kernel_ann *k) {
+        HIPCHK(hipStreamSynchronize(s));
+        if (V[0]) ann_momentum_init(k);
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            const size_t nw = (size_t)N[l] * M[l];
+            std::vector<T> tmp(nw);
+            HIPCHK(hipMemcpy(tmp.data(), W[l], nw * sizeof(T), hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < nw; i++) ly->weights[i] = (DOUBLE)tmp[i];
+            if (!V[l]) continue;
+            HIPCHK(hipMemcpy(tmp.data(), V[l], nw * sizeof(T), hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < nw; i++) k->dw[l][i] = (DOUBLE)tmp[i];
+        }
+        return TRUE;
+    }
+
+    BOOL upload_momentum(const kernel_ann *k) {
+        if (!k->dw) return TRUE;
+        for (int l = 0; l < L; l++) {
+            if (!V[l]) continue;
+            const size_t nw = (size_t)N[l] * M[l];
+            std::vector<T> tmp(nw);
+            for (size_t i = 0; i < nw; i++) tmp[i] = (T)k->dw[l][i];
+            HIPCHK(hipMemcpyAsync(V[l], tmp.data(), nw * sizeof(T), hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        return TRUE;
+    }
+};
+
 }  // namespace
 
 namespace {
@@ -679,58 +909,88 @@ namespace {
  * equals the single-GPU step up to summation order.
  * loopback: G virtual replicas on ONE device (CI without a multi-GPU node): the buffers
  * live in one allocation and the all-reduce is a deterministic slab sum. */
+template <class Net>
 BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
               hpnn_batched_stats *st, int G, bool loopback);
+template <class Net>
 BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
                  hpnn_batched_stats *st);
+template <class Net>
+BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                  hpnn_batched_stats *st);
 
 }  // namespace
 
 extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
                                        const hpnn_batched_opts *o, hpnn_batched_stats *st) {
-    {
-        const char *lb = getenv("HPNN_LOOPBACK_RANKS");
-        const int lbr = lb ? atoi(lb) : 0;
-        const char *fr = getenv("HPNN_FORCE_RCCL");
-        if (lbr >= 2) return train_dp(k, X, T, n, o, st, lbr, true);
-        /* one process per GPU under a launcher (torchrun --no-python bin/train_nn ...) */
-        const char *nd = getenv("HPNN_NATIVE_DP");
-        if (hpnn_boot_world() > 1 && !(nd && nd[0] == '0')) return train_dp_mp(k, X, T, n, o, st);
-        if (o->n_gpu > 1 || (fr && fr[0] == '1')) return train_dp(k, X, T, n, o, st, (int)(o->n_gpu ? o->n_gpu : 1), false);
+    if (o->dtype != NN_DTYPE_BF16 && o->dtype != NN_DTYPE_F32 && o->dtype != NN_DTYPE_F64) {
+        NN_ERROR(stderr, "GPU batched engine: unsupported dtype %d\n", (int)o->dtype);
+        return FALSE;
     }
-    if (o->dtype != NN_DTYPE_BF16) {
-        NN_WARN(stderr, "GPU batched engine runs BF16 MFMA; requested dtype promoted to bf16\n");
+    const char *lb = getenv("HPNN_LOOPBACK_RANKS");
+    const int lbr = lb ? atoi(lb) : 0;
+    const char *fr = getenv("HPNN_FORCE_RCCL");
+    const char *nd = getenv("HPNN_NATIVE_DP");
+    const nn_dtype dt = o->dtype;
+    if (lbr >= 2) {
+        if (dt == NN_DTYPE_BF16) return train_dp<Batched>(k, X, T, n, o, st, lbr, true);
+        if (dt == NN_DTYPE_F32) return train_dp<BatchedFP<float>>(k, X, T, n, o, st, lbr, true);
+        return train_dp<BatchedFP<double>>(k, X, T, n, o, st, lbr, true);
     }
+    /* one process per GPU under a launcher (torchrun --no-python bin/train_nn ...) */
+    if (hpnn_boot_world() > 1 && !(nd && nd[0] == '0')) {
+        if (dt == NN_DTYPE_BF16) return train_dp_mp<Batched>(k, X, T, n, o, st);
+        if (dt == NN_DTYPE_F32) return train_dp_mp<BatchedFP<float>>(k, X, T, n, o, st);
+        return train_dp_mp<BatchedFP<double>>(k, X, T, n, o, st);
+    }
+    if (o->n_gpu > 1 || (fr && fr[0] == '1')) {
+        const int G = (int)(o->n_gpu ? o->n_gpu : 1);
+        if (dt == NN_DTYPE_BF16) return train_dp<Batched>(k, X, T, n, o, st, G, false);
+        if (dt == NN_DTYPE_F32) return train_dp<BatchedFP<float>>(k, X, T, n, o, st, G, false);
+        return train_dp<BatchedFP<double>>(k, X, T, n, o, st, G, false);
+    }
+    if (dt == NN_DTYPE_BF16) return train_single<Batched>(k, X, T, n, o, st);
+    if (dt == NN_DTYPE_F32) return train_single<BatchedFP<float>>(k, X, T, n, o, st);
+    return train_single<BatchedFP<double>>(k, X, T, n, o, st);
+}
+
+namespace {
+
+template <class Net>
+BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                  hpnn_batched_stats *st) {
+    typedef typename Net::target_t TT;
     if (k->n_hiddens + 1 > 16) return FALSE;
     hpnn_gpu_sync_host(k);
     HIPCHK(hipSetDevice(hpnn_rt_device(0)));
     hipStream_t s = hpnn_rt_stream(0, 0);
     const int B = (int)(o->batch ? o->batch : 256);
     const bool mom = o->train == NN_TRAIN_BPM;
-    Batched net;
+    Net net;
     if (!net.init(k, B, o->type, mom, s)) return FALSE;
+    NN_OUT(stdout, "batched GPU training: %s, %d samples per step\n", Net::name(), B);
     if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = (n_batches - 1) * B + net.Bp; /* last batch reads Bp rows */
     void *Xd = nullptr;
-    float *Td = nullptr;
-    if (!upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
+    TT *Td = nullptr;
+    if (!Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
     {
-        std::vector<float> tf((size_t)rows_p * k->n_outputs, 0.f);
-        for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (float)T[i];
-        HIPCHK(hpnn_dev_malloc(&Td, tf.size() * 4));
-        HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice));
+        std::vector<TT> tf((size_t)rows_p * k->n_outputs, (TT)0);
+        for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (TT)T[i];
+        HIPCHK(hpnn_dev_malloc(&Td, tf.size() * sizeof(TT)));
+        HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * sizeof(TT), hipMemcpyHostToDevice));
     }
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
     for (UINT e = 0; e < o->epochs; e++) {
-        HIPCHK(hipMemsetAsync(net.acc, 0, Batched::ACC_BYTES, s));
+        HIPCHK(hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s));
         for (int b = 0; b < n_batches; b++) {
             const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-            const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * 2;
-            const float *tb = Td + (size_t)b * B * k->n_outputs;
-            if (!net.step(xb, tb, (int)k->n_outputs, nv, (float)o->lr, (float)o->alpha, mom)) {
+            const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * Net::xelem;
+            const TT *tb = Td + (size_t)b * B * k->n_outputs;
+            if (!net.step(xb, tb, (int)k->n_outputs, nv, o->lr, o->alpha, mom)) {
                 hpnn_dev_free(Xd);
                 hpnn_dev_free(Td);
                 return FALSE;
@@ -758,10 +1018,15 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     return TRUE;
 }
 
+}  // namespace
+
 namespace {
 
+template <class Net>
 BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
               hpnn_batched_stats *st, int G, bool loopback) {
+    typedef typename Net::target_t TT;
+    typedef typename Net::grad_t GT;
     if (k->n_hiddens + 1 > 16 || G < 1) return FALSE;
     if (!loopback && !hpnn_comm_available()) return FALSE;
     hpnn_gpu_sync_host(k);
@@ -771,10 +1036,10 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     const int n_out = (int)k->n_outputs;
     std::vector<int> dev(G);
     std::vector<hipStream_t> str(G);
-    std::vector<std::unique_ptr<Batched>> nets(G);
-    float *lb_flat = nullptr; /* loopback: [G][count] in one allocation */
+    std::vector<std::unique_ptr<Net>> nets(G);
+    GT *lb_flat = nullptr; /* loopback: [G][count] in one allocation */
     std::vector<void *> Xd(G, nullptr);
-    std::vector<float *> Td(G, nullptr);
+    std::vector<TT *> Td(G, nullptr);
     std::vector<hpnn_comm *> comms(G, nullptr);
     BOOL ok = TRUE;
     const int n_batches = (int)((n + B - 1) / B);
@@ -800,19 +1065,23 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     const int rows_p = n_batches * B + Bg + 128;
     for (int g = 0; g < G && ok; g++) {
         if (hipSetDevice(dev[g]) != hipSuccess) return FALSE;
-        nets[g].reset(new Batched());
+        nets[g].reset(new Net());
         ok = nets[g]->init(k, Bg, o->type, mom, str[g]);
         if (ok && mom && o->resume) ok = nets[g]->upload_momentum(k);
         if (!ok) break;
         if (loopback) {
             if (g == 0) {
                 size_t tot = 0;
-                for (int l = 0; l < nets[0]->L; l++) tot += (size_t)nets[0]->Np[l] * nets[0]->Kp[l];
-                if (hpnn_dev_malloc(&lb_flat, tot * 4 * G) != hipSuccess) ok = FALSE;
+                if (!nets[0]->alloc_flat(nullptr)) ok = FALSE; /* sizes only; re-pointed below */
+                if (ok) tot = nets[0]->flat_count();
+                if (ok && hpnn_dev_malloc(&lb_flat, tot * sizeof(GT) * G) != hipSuccess) ok = FALSE;
             }
             if (ok) {
-                size_t tot = 0;
-                for (int l = 0; l < nets[g]->L; l++) tot += (size_t)nets[g]->Np[l] * nets[g]->Kp[l];
+                const size_t tot = nets[0]->flat_count();
+                if (g == 0 && nets[0]->own_flat) {
+                    hpnn_dev_free(nets[0]->gflat);
+                    nets[0]->own_flat = false;
+                }
                 ok = nets[g]->alloc_flat(lb_flat + tot * g);
             }
         } else {
@@ -820,12 +1089,12 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         }
         if (!ok) break;
         if (!loopback || g == 0) {
-            ok = upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, nets[g]->Kp[0], &Xd[g], str[g]);
+            ok = Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, nets[g]->Kp[0], &Xd[g], str[g]);
             if (ok) {
-                std::vector<float> tf((size_t)rows_p * n_out, 0.f);
-                for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (float)T[i];
-                ok = hpnn_dev_malloc(&Td[g], tf.size() * 4) == hipSuccess &&
-                     hipMemcpy(Td[g], tf.data(), tf.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+                std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
+                for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];
+                ok = hpnn_dev_malloc(&Td[g], tf.size() * sizeof(TT)) == hipSuccess &&
+                     hipMemcpy(Td[g], tf.data(), tf.size() * sizeof(TT), hipMemcpyHostToDevice) == hipSuccess;
             }
         } else {
             Xd[g] = Xd[0];
@@ -840,15 +1109,15 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         return FALSE;
     }
     const size_t count = nets[0]->flat_count();
-    NN_OUT(stdout, "data-parallel batched training: %d replicas (%s), %d samples per replica per step\n", G,
-           loopback ? "loopback on one GPU" : "RCCL all-reduce", Bg);
+    NN_OUT(stdout, "data-parallel batched training: %d replicas (%s, %s), %d samples per replica per step\n", G,
+           loopback ? "loopback on one GPU" : "RCCL all-reduce", Net::name(), Bg);
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
     for (UINT e = 0; e < o->epochs && ok; e++) {
         for (int g = 0; g < G; g++) {
             hipSetDevice(dev[g]);
-            hipMemsetAsync(nets[g]->acc, 0, Batched::ACC_BYTES, str[g]);
+            hipMemsetAsync(nets[g]->acc, 0, Net::ACC_BYTES, str[g]);
         }
         for (int b = 0; b < n_batches && ok; b++) {
             const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
@@ -859,20 +1128,20 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                 nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
                 total += nv;
                 hipSetDevice(dev[g]);
-                const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * 2;
-                const float *tb = Td[g] + (size_t)start * n_out;
+                const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * Net::xelem;
+                const TT *tb = Td[g] + (size_t)start * n_out;
                 ok = nets[g]->grads(xb, tb, n_out, nv);
             }
             if (!ok) break;
             if (loopback) {
                 /* virtual replicas share one stream: sum the G buffers into replica 0's */
-                ok = hpnn_reduce_slabs(lb_flat, G, (long)count, (long)count, lb_flat, str[0]) == 0;
+                ok = Net::reduce_sum(lb_flat, G, count, str[0]) == 0;
             } else {
                 /* one grouped launch: the per-device calls of a single-process communicator
                  * clique must not block each other */
                 int r = hpnn_comm_group_start();
                 for (int g = 0; g < G && r == 0; g++)
-                    r = hpnn_comm_all_reduce(comms[g], nets[g]->gflat, nets[g]->gflat, (long)count, HPNN_DT_F32,
+                    r = hpnn_comm_all_reduce(comms[g], nets[g]->gflat, nets[g]->gflat, (long)count, Net::comm_dt,
                                              HPNN_OP_SUM, str[g]);
                 const int r2 = hpnn_comm_group_end();
                 if (r || r2) {
@@ -880,10 +1149,10 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                     ok = FALSE;
                 }
             }
-            const float scale = 1.0f / (float)(total > 0 ? total : 1);
+            const double scale = 1.0 / (double)(total > 0 ? total : 1);
             for (int g = 0; g < G && ok; g++) {
                 hipSetDevice(dev[g]);
-                ok = nets[g]->update_flat(loopback ? lb_flat : nets[g]->gflat, (float)o->lr, (float)o->alpha, scale,
+                ok = nets[g]->update_flat(loopback ? lb_flat : nets[g]->gflat, o->lr, o->alpha, scale,
                                           mom);
             }
         }
@@ -932,8 +1201,10 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
  * ranks on one node, gradients <= 4 MiB) or RCCL, the bootstrap exchange (IPC handles /
  * unique id / epoch statistics) goes through include/libhpnn/bootstrap.h; every rank
  * applies the same update, so the weights stay identical (rank 0 writes the files). */
+template <class Net>
 BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
                  hpnn_batched_stats *st) {
+    typedef typename Net::target_t TT;
     const int W = hpnn_boot_world(), R = hpnn_boot_rank();
     if (k->n_hiddens + 1 > 16 || W < 2 || W > 64) return FALSE;
     hpnn_gpu_sync_host(k);
@@ -944,7 +1215,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const int Bg = (B + W - 1) / W;
     const bool mom = o->train == NN_TRAIN_BPM;
     const int n_out = (int)k->n_outputs;
-    Batched net;
+    Net net;
     if (!net.init(k, Bg, o->type, mom, s) || !net.alloc_flat()) return FALSE;
     if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const size_t count = net.flat_count();
@@ -954,8 +1225,9 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     hpnn_comm *comm = nullptr;
     const char *xe = getenv("HPNN_XAR");
     const char *lws = getenv("LOCAL_WORLD_SIZE");
-    bool use_xar = !(xe && xe[0] == '0') && lws && atoi(lws) == W && W <= HPNN_XAR_MAX_RANKS &&
-                   count * 4 <= ((size_t)4 << 20);
+    /* the xGMI all-reduce sums FP32; FP64 gradients go through RCCL */
+    bool use_xar = Net::comm_dt == HPNN_DT_F32 && !(xe && xe[0] == '0') && lws && atoi(lws) == W &&
+                   W <= HPNN_XAR_MAX_RANKS && count * 4 <= ((size_t)4 << 20);
     if (use_xar) {
         xar = hpnn_xar_create(R, W, count * 4);
         std::vector<char> h(HPNN_XAR_HANDLE_BYTES, 0), all((size_t)W * HPNN_XAR_HANDLE_BYTES);
@@ -985,38 +1257,38 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         comm = hpnn_comm_init_rank(all.data(), W, R, dev); /* rank 0's id */
         if (!comm) return FALSE;
     }
-    NN_OUT(stdout, "data-parallel batched training: %d processes (%s), %d samples per rank per step\n", W,
-           use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Bg);
+    NN_OUT(stdout, "data-parallel batched training: %d processes (%s, %s), %d samples per rank per step\n", W,
+           use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Net::name(), Bg);
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = n_batches * B + Bg + 128;
     void *Xd = nullptr;
-    float *Td = nullptr;
-    BOOL ok = upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s);
+    TT *Td = nullptr;
+    BOOL ok = Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s);
     if (ok) {
-        std::vector<float> tf((size_t)rows_p * n_out, 0.f);
-        for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (float)T[i];
-        ok = hpnn_dev_malloc(&Td, tf.size() * 4) == hipSuccess &&
-             hipMemcpy(Td, tf.data(), tf.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+        std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
+        for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];
+        ok = hpnn_dev_malloc(&Td, tf.size() * sizeof(TT)) == hipSuccess &&
+             hipMemcpy(Td, tf.data(), tf.size() * sizeof(TT), hipMemcpyHostToDevice) == hipSuccess;
     }
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
     for (UINT e = 0; e < o->epochs && ok; e++) {
-        ok = hipMemsetAsync(net.acc, 0, Batched::ACC_BYTES, s) == hipSuccess;
+        ok = hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) == hipSuccess;
         for (int b = 0; b < n_batches && ok; b++) {
             const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
             const int start = b * B + R * Bg;
             int nv = end - start;
             nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
-            const char *xb = (const char *)Xd + (size_t)start * net.Kp[0] * 2;
-            const float *tb = Td + (size_t)start * n_out;
+            const char *xb = (const char *)Xd + (size_t)start * net.Kp[0] * Net::xelem;
+            const TT *tb = Td + (size_t)start * n_out;
             ok = net.grads(xb, tb, n_out, nv);
             if (!ok) break;
-            ok = (use_xar ? hpnn_xar_all_reduce_f32(xar, net.gflat, net.gflat, (long)count, s)
-                          : hpnn_comm_all_reduce(comm, net.gflat, net.gflat, (long)count, HPNN_DT_F32, HPNN_OP_SUM,
+            ok = (use_xar ? hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s)
+                          : hpnn_comm_all_reduce(comm, net.gflat, net.gflat, (long)count, Net::comm_dt, HPNN_OP_SUM,
                                                  s)) == 0;
             const int total = end - b * B;
-            if (ok) ok = net.update_flat(net.gflat, (float)o->lr, (float)o->alpha, 1.0f / (float)(total > 0 ? total : 1),
+            if (ok) ok = net.update_flat(net.gflat, o->lr, o->alpha, 1.0 / (double)(total > 0 ? total : 1),
                                          mom);
         }
         if (!ok) break;
@@ -1063,12 +1335,9 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
 
 }  // namespace
 
-extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
-                                       DOUBLE *Y) {
-    (void)dtype;
-    hpnn_gpu_sync_host(k);
-    HIPCHK(hipSetDevice(hpnn_rt_device(0)));
-    hipStream_t s = hpnn_rt_stream(0, 0);
+namespace {
+
+BOOL infer_bf16(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, hipStream_t s) {
     const int B = 4096;
     Batched net;
     if (!net.init(k, B, type, false, s)) return FALSE;
@@ -1081,19 +1350,73 @@ extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dty
     HIPCHK(hpnn_dev_malloc(&Tz, (size_t)net.Bp * k->n_outputs * 4));
     HIPCHK(hipMemset(Tz, 0, (size_t)net.Bp * k->n_outputs * 4));
     std::vector<float> h((size_t)net.Bp * net.Np[net.L - 1]);
-    for (int b = 0; b < n_batches; b++) {
+    BOOL ok = TRUE;
+    for (int b = 0; b < n_batches && ok; b++) {
         const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-        if (!net.forward((const char *)Xd + (size_t)b * B * net.Kp[0] * 2)) return FALSE;
-        hpnn_output_delta(net.Z, net.Np[net.L - 1], Tz, (int)k->n_outputs, nullptr, 0.f, 0.f, net.D[net.L - 1],
-                          net.Np[net.L - 1], O, net.Np[net.L - 1], nullptr, nullptr, net.Bp, nv, net.n_out, net.type, s);
-        HIPCHK(hipMemcpyAsync(h.data(), O, h.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        for (int r = 0; r < nv; r++)
+        ok = net.forward((const char *)Xd + (size_t)b * B * net.Kp[0] * 2);
+        if (ok)
+            ok = hpnn_output_delta(net.Z, net.Np[net.L - 1], Tz, (int)k->n_outputs, nullptr, 0.f, 0.f,
+                                   net.D[net.L - 1], net.Np[net.L - 1], O, net.Np[net.L - 1], nullptr, nullptr, net.Bp,
+                                   nv, net.n_out, net.type, s) == 0;
+        ok = ok && hipMemcpyAsync(h.data(), O, h.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+        for (int r = 0; ok && r < nv; r++)
             for (UINT c = 0; c < k->n_outputs; c++)
                 Y[((size_t)b * B + r) * k->n_outputs + c] = h[(size_t)r * net.Np[net.L - 1] + c];
     }
     hpnn_dev_free(Xd);
     hpnn_dev_free(O);
     hpnn_dev_free(Tz);
-    return TRUE;
+    return ok;
+}
+
+/* FP64 / FP32 inference: the forward GEMMs and the output activation in the model's
+ * precision, one device-to-host copy of the outputs per block of samples */
+template <typename T>
+BOOL infer_fp(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, hipStream_t s) {
+    const int B = (int)(n < 16384 ? n : 16384);
+    BatchedFP<T> net;
+    if (!net.init(k, B, type, false, s)) return FALSE;
+    const int n_batches = (int)((n + B - 1) / B);
+    const int rows_p = n_batches * B;
+    const int no = (int)k->n_outputs;
+    void *Xd = nullptr;
+    T *O = nullptr;
+    if (!BatchedFP<T>::upload_x(X, (int)n, (int)k->n_inputs, rows_p, (int)k->n_inputs, &Xd, s)) return FALSE;
+    HIPCHK(hpnn_dev_malloc(&O, (size_t)B * no * sizeof(T)));
+    std::vector<T> h((size_t)B * no);
+    BOOL ok = TRUE;
+    for (int b = 0; b < n_batches && ok; b++) {
+        const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
+        ok = net.forward((const char *)Xd + (size_t)b * B * k->n_inputs * sizeof(T), B);
+        if (ok)
+            ok = hpnn_output_fp(BatchedFP<T>::F64, net.Z, no, nullptr, 0, nullptr, 0, O, no, nullptr, nullptr, nullptr,
+                                B, 0, no, net.type, s) == 0;
+        ok = ok && hipMemcpyAsync(h.data(), O, (size_t)nv * no * sizeof(T), hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+        for (size_t i = 0; ok && i < (size_t)nv * no; i++) Y[(size_t)b * B * no + i] = (DOUBLE)h[i];
+    }
+    hpnn_dev_free(Xd);
+    hpnn_dev_free(O);
+    return ok;
+}
+
+}  // namespace
+
+/* batched evaluation (run_nn on the GPU): the whole test set through the batched engine
+ * of the requested precision instead of one online forward per file */
+extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
+                                       DOUBLE *Y) {
+    if (!k || n == 0) return FALSE;
+    hpnn_gpu_sync_host(k);
+    HIPCHK(hipSetDevice(hpnn_rt_device(0)));
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    switch (dtype) {
+    case NN_DTYPE_BF16: return infer_bf16(k, type, X, n, Y, s);
+    case NN_DTYPE_F32: return infer_fp<float>(k, type, X, n, Y, s);
+    case NN_DTYPE_F64: return infer_fp<double>(k, type, X, n, Y, s);
+    default:
+        NN_ERROR(stderr, "GPU inference: unsupported dtype %d\n", (int)dtype);
+        return FALSE;
+    }
 }

@@ -190,6 +190,27 @@ int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0
                    float *gslab, float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type,
                    int grid, hipStream_t stream);
 int hpnn_mlp3_tile_grid(int Bp, int grid);
+/* ---- FP64 / FP32 batched engine (kernels_fp.hip): f64 selects double, else float ----
+ * gemm_fp: C[M x N] (ldc) = sum_k A(m, k) B(n, k) with A(m, k) = A[m*lda + k] (ta = 0) or
+ * A[k*lda + m] (ta = 1), B(n, k) = B[n*ldb + k] (tb = 0) or B[k*ldb + n] (tb = 1), on the FP64 /
+ * FP32 MFMA; epi as hpnn_gemm_nt_bf16 (aux [M x N], ldaux); splits > 1: split-K into
+ * hpnn_gemm_fp_splits(K, splits) slabs slab_stride elements apart.  Any sizes. */
+int hpnn_gemm_fp(int f64, const void *A, int lda, int ta, const void *B, int ldb, int tb, void *C, int ldc,
+                 const void *aux, int ldaux, int M, int N, int K, int epi, int splits, long slab_stride,
+                 hipStream_t stream);
+int hpnn_gemm_fp_splits(int K, int splits);
+/* output layer in FP64 / FP32: O (optional) = output, D (optional) = delta, guess (optional)
+ * = argmax per row (first maximum), loss / hits into the stat slots for rows < n_valid
+ * (T required for D, loss, hits) */
+int hpnn_output_fp(int f64, const void *Z, int ldz, const void *T, int ldt, void *D, int ldd, void *O, int ldo,
+                   int *guess, float *loss_acc, unsigned int *correct, int B, int n_valid, int n_out, int type,
+                   hipStream_t stream);
+/* W += step(scale * sum_s G[s]) (BP / BPM), n elements */
+int hpnn_update_fp(int f64, void *W, void *V, const void *G, int S, long gstride, long n, double lr, double alpha,
+                   double scale, int momentum, hipStream_t stream);
+/* out = sum_s G[s] */
+int hpnn_reduce_fp(int f64, void *out, const void *G, int S, long gstride, long n, hipStream_t stream);
+
 /* floats per block slab written by hpnn_mlp3_mid */
 int hpnn_mlp3_slab_floats(void);
 /* deterministic 2-pass slab reduction: groups of slabs into tmp (>= 16*n floats,

@@ -141,6 +141,24 @@ PYBIND11_MODULE(_native, m) {
         if (rc <= 0) check(rc ? rc : -1, "mlp3_tile");
         return rc;
     });
+    m.def("gemm_fp", [](int f64, uptr A, int lda, int ta, uptr B, int ldb, int tb, uptr C, int ldc, uptr aux, int ldaux,
+                        int M, int N, int K, int epi, int splits, long slab_stride, uptr stream) {
+        check(hpnn_gemm_fp(f64, P(A), lda, ta, P(B), ldb, tb, P(C), ldc, P(aux), ldaux, M, N, K, epi, splits,
+                           slab_stride, S(stream)),
+              "gemm_fp");
+        return hpnn_gemm_fp_splits(K, splits);
+    });
+    m.def("output_fp", [](int f64, uptr Z, int ldz, uptr T, int ldt, uptr D, int ldd, uptr O, int ldo, uptr guess,
+                          uptr loss, uptr correct, int B, int n_valid, int n_out, int type, uptr stream) {
+        check(hpnn_output_fp(f64, P(Z), ldz, P(T), ldt, P(D), ldd, P(O), ldo, (int *)P(guess), (float *)P(loss),
+                             (unsigned int *)P(correct), B, n_valid, n_out, type, S(stream)),
+              "output_fp");
+    });
+    m.def("update_fp", [](int f64, uptr W, uptr V, uptr G, int Sn, long gstride, long n, double lr, double alpha,
+                          double scale, int momentum, uptr stream) {
+        check(hpnn_update_fp(f64, P(W), P(V), P(G), Sn, gstride, n, lr, alpha, scale, momentum, S(stream)),
+              "update_fp");
+    });
     m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
     m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, int h_u8, float hscale, uptr slab, int ldg, int N, int M,

@@ -42,7 +42,7 @@ PIXEL_SCALE = float(torch.tensor(float(os.environ.get("HPNN_PIXEL_SCALE", str(1.
                                  dtype=torch.float32).item())
 # HPNN_TILE=0: the 32-sample pipelined front (mlp3_fused, "x") instead of the 256-sample
 # tile kernel (mlp3_tile, "t") on eligible MNIST-shaped nets
-_TILE = os.environ.get("HPNN_TILE", "0") != "0"
+_TILE = os.environ.get("HPNN_TILE", "1") != "0"
 # HPNN_G0_RS=1: first-layer gradient with the register-staged TN kernel (kernels_g0.hip):
 # 75.46-76.57 us/step vs 75.73-77.32 with the LDS-DMA TN kernel (scripts/gpu_ab_g0.sh),
 # within noise of each other

@@ -36,14 +36,15 @@ def _env(**kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dims", [(784, [128, 64], 10), (100, [48], 7)])
-def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims):
+@pytest.mark.parametrize("dims,dtype", [((784, [128, 64], 10), "bf16"), ((100, [48], 7), "bf16"),
+                                        ((100, [48], 7), "f32")])
+def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims, dtype):
     n_in, hid, n_out = dims
     for sub in ("one", "two"):
         d = tmp_path / sub
         _data(str(d / "s"), 700, n_in, n_out)
         formats.write_conf(str(d / "nn.conf"), name="mp", type="SNN", seed=4, inputs=n_in, hiddens=hid, outputs=n_out,
-                           train="BPM", sample_dir="./s", test_dir="./s")
+                           train="BPM", sample_dir="./s", test_dir="./s", dtype=dtype)
     flags = ["-vv", "-b", "256", "-e", "2", "nn.conf"]
     r = subprocess.run([TN] + flags, cwd=tmp_path / "one", env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
@@ -67,7 +68,7 @@ def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims):
         outs.append((p.returncode, o, e))
     for rc, o, e in outs:
         assert rc == 0, o[-2000:] + e[-2000:]
-    assert "2 processes (xGMI all-reduce)" in outs[0][1]
+    assert f"2 processes (xGMI all-reduce, {dtype})" in outs[0][1]
     assert outs[1][1].strip() == ""  # rank 1 prints nothing
     w1 = formats.read_kernel(str(tmp_path / "one" / "kernel.opt"))["weights"]
     w2 = formats.read_kernel(str(tmp_path / "two" / "kernel.opt"))["weights"]

@@ -23,6 +23,51 @@ def _data(rank, n, it):
     return torch.randn(n, generator=g)
 
 
+def _check_slabs_update(n, x, rank, world, s):
+    """the all-reduce with every layer's optimizer step fused in (the DP MNIST step's
+    exchange): MNIST-shaped layers (G0 128 x 800 from 3 split-K slabs, [G1 | G2] from 2
+    group slabs, 450 KB: two-shot from 4 ranks in auto mode), BPM; every rank must end with
+    the same W32 / V32 / BF16 copies as a host update on the summed gradient"""
+    shapes = [(128, 800), (64, 128), (32, 64)]
+    lr, alpha, scale = 0.05, 0.2, 1.0 / 777
+    g = torch.Generator().manual_seed(5)  # same initial weights on every rank
+    Ws = [torch.randn(N, K, generator=g) * 0.1 for N, K in shapes]
+    Vs = [torch.randn(N, K, generator=g) * 0.01 for N, K in shapes]
+    W32 = [w.clone().cuda() for w in Ws]
+    V32 = [v.clone().cuda() for v in Vs]
+    Wb = [torch.empty(N, K, dtype=torch.bfloat16, device="cuda") for N, K in shapes]
+    Wt = [torch.empty(K, N, dtype=torch.bfloat16, device="cuda") for N, K in shapes]
+    n0 = 128 * 800
+    n12 = 64 * 128 + 32 * 64
+    sl0 = torch.stack([_data(rank, n0, 200 + k) for k in range(3)]).cuda()
+    sl1 = torch.stack([_data(rank, n12, 300 + k) for k in range(2)]).cuda()
+    out = torch.empty(n0 + n12, device="cuda")
+    layers = [(W32[i].data_ptr(), V32[i].data_ptr(), Wb[i].data_ptr(), Wt[i].data_ptr(), 0, N, K)
+              for i, (N, K) in enumerate(shapes)]
+    n.xar_all_reduce_slabs_update_f32(x, [(sl0.data_ptr(), sl0.stride(0), 3, n0), (sl1.data_ptr(), sl1.stride(0), 2,
+                                                                                    n12)],
+                                      out.data_ptr(), layers, lr, alpha, scale, 1, s)
+    torch.cuda.synchronize()
+    G = torch.cat([sum(_data(r, n0, 200 + k) for r in range(world) for k in range(3)),
+                   sum(_data(r, n12, 300 + k) for r in range(world) for k in range(2))])
+    errs = []
+    if (out.cpu() - G).abs().max().item() > 1e-4:
+        errs.append("slabs-update: reduced gradient mismatch")
+    off = 0
+    for i, (N, K) in enumerate(shapes):
+        gi = G[off:off + N * K].view(N, K) * scale
+        off += N * K
+        v = Vs[i] + lr * gi
+        w = Ws[i] + v
+        v = v * alpha
+        if (W32[i].cpu() - w).abs().max().item() > 1e-5 or (V32[i].cpu() - v).abs().max().item() > 1e-6:
+            errs.append(f"slabs-update: layer {i} W32/V32 mismatch")
+        if not torch.equal(Wb[i].cpu(), W32[i].cpu().bfloat16()) or not torch.equal(Wt[i].cpu(),
+                                                                                     W32[i].cpu().bfloat16().t()):
+            errs.append(f"slabs-update: layer {i} bf16 copies mismatch")
+    return errs
+
+
 def _worker(rank, world, port, q, mode):
     try:
         os.environ["HPNN_XAR_TIMEOUT_MS"] = "400"
@@ -68,6 +113,7 @@ def _worker(rank, world, port, q, mode):
                          sum(_data(r, 1000, 60) for r in range(world))])
         if (out.cpu() - ref).abs().max().item() > 1e-4:
             errs.append("slab-sum all-reduce mismatch")
+        errs += _check_slabs_update(n, x, rank, world, s)
         # graph capture: the kernel advances its own barrier epochs on every replay
         buf = _data(rank, 9280, 99).cuda()
         base = buf.clone()
@@ -104,7 +150,7 @@ def _worker(rank, world, port, q, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,mode", [(2, "1"), (2, "2"), (3, "2"), (4, "0")])
+@pytest.mark.parametrize("world,mode", [(2, "1"), (2, "2"), (3, "2"), (4, "0"), (8, "0"), (8, "1")])
 def test_xgmi_allreduce_processes(gpu, world, mode):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -114,7 +160,7 @@ def test_xgmi_allreduce_processes(gpu, world, mode):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=100) for _ in ps)
+    res = dict(q.get(timeout=110) for _ in ps)
     for p in ps:
         p.join(timeout=30)
         if p.is_alive():

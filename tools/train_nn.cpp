@@ -74,12 +74,20 @@ int main(int argc, char *argv[]) {
     UINT task = 0;
     _NN(get, curr_mpi_task)(&task);
     const bool writer = !_NN(return, dry)() && task == 0;
+    /* HPNN_KERNEL_EXACT=1: kernel files with %.17g (bit-exact FP64 round trip) instead of
+     * the reference's %17.15f -- parity tests compare weights below the text rounding */
+    const char *ex = getenv("HPNN_KERNEL_EXACT");
+    const bool exact = ex && ex[0] == '1';
+    auto dump = [&](FILE *f) {
+        if (exact) _NN(dump, kernel_exact)(neural, f);
+        else _NN(dump, kernel)(neural, f);
+    };
     if (writer) {
         FILE *f = fopen("./kernel.tmp", "w");
         if (!f) {
             _OUT(stderr, "FAILED to open kernel.tmp for writing!\n");
         } else {
-            _NN(dump, kernel)(neural, f);
+            dump(f);
             fclose(f);
         }
     }
@@ -90,7 +98,7 @@ int main(int argc, char *argv[]) {
         if (!f) {
             _OUT(stderr, "FAILED to open kernel.opt for writing!\n");
         } else {
-            _NN(dump, kernel)(neural, f);
+            dump(f);
             fclose(f);
         }
         if (o.state && ok && !_NN(dump, state)(neural, o.state)) ok = FALSE;
