@@ -89,7 +89,12 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int TYPE, bool LABELS, int KS, bool XU8, int D>
+/* HPNN_TILE_TRACE=1 (profiling only): s_memtime stamps of every workgroup's wave 0 at the
+ * phase boundaries, [block][mark]; read back with hpnn_mlp3_tile_trace */
+constexpr int TR_BLOCKS = 1024, TR_MARKS = 8;
+__device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
+
+template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                          const __bf16 *__restrict__ W0f,
                                                          const __bf16 *__restrict__ W1,
@@ -112,21 +117,21 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     const LaneOff lo = lane_offsets(lane);
     char *imgH1 = lds + OFF_H1, *imgH2 = lds + OFF_H2, *imgD2 = lds + OFF_D2, *imgD3 = lds + OFF_D3;
     char *imgW1 = lds + OFF_W1;
+    auto mark = [&](int i) {
+        if constexpr (TRACE) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (tid == 0 && blockIdx.x < TR_BLOCKS) g_tile_trace[blockIdx.x][i] = t;
+        }
+    };
+    mark(0);
 
     /* ---- once per launch: W1 -> LDS image, W2 / W2^T operand fragments -> registers ---- */
     {
         constexpr int PIECES = (H1 / 32) * (H2 / 16);
         for (int p = wave; p < PIECES; p += 8) glds_t32_piece<H2>((const char *)W1, (size_t)H1 * 2, imgW1, p, lane);
     }
-    bf16x8 w2f[2][2], w2tf[4]; /* P2: A = W2[o][h2] rows; P3: A = W2^T[h2][o] rows */
-#pragma unroll
-    for (int ot = 0; ot < 2; ot++)
-#pragma unroll
-        for (int kk = 0; kk < 2; kk++)
-            w2f[ot][kk] = *(const bf16x8 *)(W2 + (size_t)(16 * ot + r16) * H2 + 32 * kk + 8 * q);
-#pragma unroll
-    for (int ht = 0; ht < 4; ht++) w2tf[ht] = *(const bf16x8 *)(W2t + (size_t)(16 * ht + r16) * NO + 8 * q);
     __builtin_amdgcn_s_waitcnt(0xF70); /* vmcnt(0): W1 pieces landed (their DMA is inline asm) */
+    mark(1);
 
     f32x4 g1acc[4], g2acc; /* G1: h1 tile = wave, h2 tiles 0..3; G2: h2 tile w&3, o tile w>>2 */
 #pragma unroll
@@ -147,6 +152,12 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         const int row = 16 * xcbh + 2 * (xi & 7) + e;
         xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
     }
+
+    /* transposed-read addresses of this wave's 8 sample tiles in an X^T stage: sample tile st
+     * sits in 32-column sub-tile 4 sh + st/2, with the T32 chunk swap (lo.tr ^ 32) on odd st;
+     * two bases + immediate offsets (st/2 * 2 KiB, + 256 for rows 4..7, + 16 KiB per stage) */
+    const char *xt_e = lds + OFF_XT + (4 * sh) * (XR * 64) + lo.tr;
+    const char *xt_o = lds + OFF_XT + (4 * sh) * (XR * 64) + (lo.tr ^ 32);
 
     for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
@@ -192,20 +203,30 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         for (int s = 0; s <= D && s < KS; s++) issue(s);
         convert(0);
         lds_barrier();
+        mark(2);
         /* ================= phase A: H1 = f(X W0^T) ================= */
 #pragma unroll
         for (int s = 0; s < KS; s++) {
             if (s + D + 1 < KS) issue(s + D + 1);
-            const char *img = lds + OFF_XT + (s & 1) * IMG_XT;
+            /* all 8 B fragments first (16 transposed reads in flight), then the 16 MFMAs */
+            bf16x8 b[8];
 #pragma unroll
             for (int st = 0; st < 8; st++) {
-                const bf16x8 b = rd_tr<XR>(img, lo, 0, 128 * sh + 16 * st);
-                acc[0][st] = mfma(wr[s][0], b, acc[0][st]);
-                acc[1][st] = mfma(wr[s][1], b, acc[1][st]);
+                const char *pb = ((st & 1) ? xt_o : xt_e) + (s & 1) * IMG_XT + (st >> 1) * (XR * 64);
+                const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)pb);
+                const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(pb + 256));
+                const s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+                b[st] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int st = 0; st < 8; st++) {
+                acc[0][st] = mfma(wr[s][0], b[st], acc[0][st]);
+                acc[1][st] = mfma(wr[s][1], b[st], acc[1][st]);
             }
             if (s + 1 < KS) convert(s + 1);
             lds_barrier();
         }
+        mark(3);
         /* H1 tile -> LDS image [sample][neuron] */
 #pragma unroll
         for (int i = 0; i < 2; i++)
@@ -218,8 +239,18 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             }
         lds_barrier();
 
+        mark(4);
         /* ================= phase B: back chain on this wave's 32 samples ================= */
         const int sw = 32 * wave;
+        /* W2 / W2^T operand fragments (L2-resident), not held through phase A */
+        bf16x8 w2f[2][2], w2tf[4]; /* P2: A = W2[o][h2] rows; P3: A = W2^T[h2][o] rows */
+#pragma unroll
+        for (int ot = 0; ot < 2; ot++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++)
+                w2f[ot][kk] = *(const bf16x8 *)(W2 + (size_t)(16 * ot + r16) * H2 + 32 * kk + 8 * q);
+#pragma unroll
+        for (int ht = 0; ht < 4; ht++) w2tf[ht] = *(const bf16x8 *)(W2t + (size_t)(16 * ht + r16) * NO + 8 * q);
         int lab[2] = {-1, -1};
         if constexpr (LABELS) {
 #pragma unroll
@@ -312,6 +343,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 }
             }
         }
+        mark(5);
         lds_barrier();
 
         /* ================= phase C: G1, G2 over the tile's 256 samples ================= */
@@ -328,6 +360,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         }
     }
 
+    mark(6);
     /* ---- the block's [G1 (H2 x H1) | G2 (NO x H2)] slab ---- */
     float *slab = gslab + (size_t)blockIdx.x * SLAB;
 #pragma unroll
@@ -356,6 +389,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         if (loss_acc) atomicAdd(loss_acc + HPNN_STAT_SLOT(blockIdx.x), a);
         if (correct) atomicAdd(correct + HPNN_STAT_SLOT(blockIdx.x), h);
     }
+    mark(7);
 }
 
 int g_tile_cus = 0;
@@ -365,17 +399,26 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
                 const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                 float *loss_acc, unsigned int *correct, int n_tiles, int n_valid, int n_out, int grid,
                 hipStream_t stream) {
-    constexpr int D = 3;
-    auto kern = mlp3_tile_kernel<TYPE, LABELS, KS, XU8, D>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
-        attr = true;
+    /* k-steps of loads in flight (HPNN_TILE_D tunes the MNIST-shaped instance) */
+    static const int dsel = [] { const char *e = getenv("HPNN_TILE_D"); return e ? atoi(e) : 0; }();
+    static const bool trace = [] { const char *e = getenv("HPNN_TILE_TRACE"); return e && e[0] == '1'; }();
+    auto go = [&](auto kern) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
+            attr = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), LDS_TOTAL, stream, Xg, xscale, (const __bf16 *)W0f,
+                           (const __bf16 *)W1, (const __bf16 *)W2, (const __bf16 *)W2t, labels, T, ldt, t_hi, t_lo,
+                           (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
+        return hipGetLastError() == hipSuccess ? grid : -5;
+    };
+    if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
+        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5, true>);
+        if (dsel == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>);
+        if (dsel == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 7>);
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), LDS_TOTAL, stream, Xg, xscale, (const __bf16 *)W0f,
-                       (const __bf16 *)W1, (const __bf16 *)W2, (const __bf16 *)W2t, labels, T, ldt, t_hi, t_lo,
-                       (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
-    return hipGetLastError() == hipSuccess ? grid : -5;
+    return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5>);
 }
 
 template <int KS>
@@ -437,4 +480,9 @@ extern "C" int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, con
     HPNN_TK(256);
 #undef HPNN_TK
     return -3;
+}
+
+/* HPNN_TILE_TRACE=1 stamps: out[TR_BLOCKS][TR_MARKS] shader-clock ticks */
+extern "C" int hpnn_mlp3_tile_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_trace), sizeof(g_tile_trace)) == hipSuccess ? 0 : -5;
 }

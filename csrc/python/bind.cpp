@@ -160,6 +160,11 @@ PYBIND11_MODULE(_native, m) {
               "update_fp");
     });
     m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
+    m.def("mlp3_tile_trace", []() {
+        std::vector<unsigned long long> v(1024 * 8);
+        check(hpnn_mlp3_tile_trace(v.data()), "mlp3_tile_trace");
+        return v;
+    });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
     m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, int h_u8, float hscale, uptr slab, int ldg, int N, int M,
                            int Bt, int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,
