@@ -343,15 +343,9 @@ struct Batched {
     float *midslab = nullptr, *midtmp = nullptr, *G12 = nullptr;
     void *W0f = nullptr; /* fragment-major BF16 W0 (fused_x) */
     hipStream_t s = nullptr;
-    /* fused_x: the [G1|G2] reduction pass forks onto `side` next to the G0 GEMM */
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
     ~Batched() {
         if (s) hipStreamSynchronize(s);
-        if (side) hipStreamDestroy(side);
-        if (ev_fork) hipEventDestroy(ev_fork);
-        if (ev_join) hipEventDestroy(ev_join);
         for (int l = 0; l < 16; l++) {
             hpnn_dev_free(W32[l]);
             hpnn_dev_free(V32[l]);
@@ -433,15 +427,6 @@ struct Batched {
             HIPCHK(hpnn_dev_malloc(&midslab, (size_t)mid_grid * slab_f * 4));
             HIPCHK(hpnn_dev_malloc(&midtmp, (size_t)16 * slab_f * 4));
             HIPCHK(hpnn_dev_malloc(&G12, (size_t)slab_f * 4));
-            static const bool side_reduce = [] {
-                const char *e = getenv("HPNN_SIDE_REDUCE");
-                return e && e[0] == '1';
-            }();
-            if (fused_x && side_reduce) { /* measured slower than the GEMM-tail reduction */
-                HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-                HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-                HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-            }
             if (fused_x) {
                 HIPCHK(hpnn_dev_malloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
                 hpnn_upd_layer c0 = {W32[0], nullptr, W32[0], 0, Wb[0], Wt[0], W0f, 1, Np[0], Kp[0]};
@@ -482,22 +467,11 @@ struct Batched {
                                   (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid,
                                   s);
         }
-        /* first reduction pass of the [G1 | G2] block slabs (the optimizer sums the groups):
-         * tail workgroups of the G0 GEMM launch, or (HPNN_SIDE_REDUCE=1) a separate launch on
-         * the side stream, concurrently with the G0 GEMM */
-        hipStream_t rs = s;
-        if (!r && side && hipEventRecord(ev_fork, s) == hipSuccess && hipStreamWaitEvent(side, ev_fork, 0) == hipSuccess)
-            rs = side;
-        if (rs != s) {
-            if (!r) r = hpnn_reduce_groups(midslab, mid_grid, slab_f, slab_f, mid_groups, midtmp, rs);
-            if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
-        } else if (!r) {
-            /* one launch: the reduction rides on workgroups appended to the G0 GEMM grid */
+        /* first reduction pass of the [G1 | G2] block slabs (the optimizer sums the groups) on
+         * tail workgroups appended to the G0 GEMM grid: one launch */
+        if (!r)
             r = hpnn_gemm_tn_bf16_reduce(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], midslab,
                                          mid_grid, slab_f, slab_f, mid_groups, midtmp, s);
-        }
-        if (rs != s && (hipEventRecord(ev_join, rs) != hipSuccess || hipStreamWaitEvent(s, ev_join, 0) != hipSuccess))
-            r = r ? r : -9;
         if (!r) {
             const long n1 = (long)Np[1] * Kp[1];
             hpnn_upd_layer u[3] = {

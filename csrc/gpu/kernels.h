@@ -55,7 +55,6 @@ int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, vo
 int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
                          void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
-void hpnn_gemm_nt8_set_m32(int on); /* 8-phase NT on v_mfma_f32_32x32x16_bf16 (A/B) */
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
                        int M, int N, int K, int epi, int c_f32, hipStream_t stream);
@@ -75,13 +74,6 @@ int hpnn_gemm_tn_bf16_reduce(const void *D, int ldd, const void *H, int ldh, flo
                              int Bt, int splits, const float *rslab, int rS, long rstride, long rn, int rgroups,
                              float *rout, hipStream_t stream);
 
-/* hpnn_gemm_tn_bf16(_reduce) with register-staged operands (kernels_g0.hip): coalesced
- * vector loads P steps ahead -> T32 LDS image -> transposed MFMA reads.  M % 160 or 128,
- * N % 128, Bt % 64.  h_u8: H is uint8 [Bt x ldh] (ldh % 16 == 0) used as bf16(h * hscale)
- * (exact for pixel values 0..255 with hscale 1).  rslab == NULL: no tail reduction. */
-int hpnn_gemm_tn_rs(const void *D, int ldd, const void *H, int ldh, int h_u8, float hscale, float *slab, int ldg,
-                    int N, int M, int Bt, int splits, const float *rslab, int rS, long rstride, long rn, int rgroups,
-                    float *rout, hipStream_t stream);
 /* weight gradient of hpnn_gemm_tn_bf16 over FRAGMENT-MAJOR operands (kernels_g0.hip):
  * Dg [Bt/32][N/16][64][8], Hg [Bt/32][M/16][64][8], lane l = 16 g + r of fragment (t, cb)
  * holding A[32 t + 8 g + j][16 cb + r] (j < 8); slab[s][n][m] as hpnn_gemm_tn_bf16.
@@ -168,15 +160,6 @@ int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, const void 
                     const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                     float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
                     int d1fm, hipStream_t stream);
-/* role-split variant of hpnn_mlp3_fused (kernels_mlp3f.hip, selected by HPNN_FRONT=f for
- * K0 >= 800): same arguments, outputs and slab layout; grid > 0 required */
-int hpnn_mlp3_front(const void *X, int ldx, int K0, const void *W0f, const void *W1, const void *W2,
-                    const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
-                    float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type, int grid,
-                    hipStream_t stream);
-int hpnn_mlp3_front_trace(unsigned long long *out);
-/* profiling: s_memtime timeline of block 0 (HPNN_FZ_MODE=9), [8 waves][8 stages][8 marks] */
-int hpnn_mlp3_fused_trace(unsigned long long *out);
 /* grid hpnn_mlp3_fused will use for Bp samples (slab rows to allocate) */
 int hpnn_mlp3_fused_grid(int Bp, int grid);
 /* the same step up to delta1 with 256-sample tiles (kernels_mlp3t.hip): X given

@@ -61,11 +61,8 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-/* M32: v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (same wave tile, LDS traffic and
- * schedule; a quadrant is 2 x 1 fragments of 32 x 32 over 4 k16-substeps = 8 MFMAs) */
-template <int EPI, bool CF32, bool M32 = false>
+template <int EPI, bool CF32>
 __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict__ A, int lda,
                                                        const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
                                                        int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
@@ -107,86 +104,52 @@ __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict_
         for (int i = 0; i < 2; i++) hpnn::glds16_sv(g, h < 2 ? voa[i] : vob[i], dst + (wave * 2 + i) * 1024);
     };
 
-    /* accumulators: 16x16 -> [mi][ni][j: 16-row frag][i: 16-col frag];
-     * 32x32 -> [mi][ni][j: 32-row frag] (one 32-col fragment per quadrant) */
+    /* accumulators: [mi][ni][j: 16-row frag][i: 16-col frag] */
     f32x4 acc[2][2][4][2];
-    f32x16 acc32[2][2][2];
-    if constexpr (M32) {
 #pragma unroll
-        for (int a = 0; a < 2; a++)
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int j = 0; j < 2; j++)
-#pragma unroll
-                    for (int e = 0; e < 16; e++) acc32[a][b][j][e] = 0.f;
-    } else {
-#pragma unroll
-        for (int a = 0; a < 2; a++)
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-#pragma unroll
-                    for (int i = 0; i < 2; i++) acc[a][b][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    const int r16 = lane & 15, q = lane >> 4, r32 = lane & 31, h32 = lane >> 5;
-    /* operand registers, flattened: 16x16 ra[j * 2 + kk] (4 frags x 2 k32), rb[i * 2 + kk];
-     * 32x32 ra[j * 4 + kk] (2 frags x 4 k16), rb[kk] */
-    bf16x8 ra[8], rb0[4], rb1[4];
-    auto read_a = [&](const char *buf, int mi) __attribute__((always_inline)) {
-        const char *img = buf + wm * HALF;
-        if constexpr (M32) {
-#pragma unroll
-            for (int j = 0; j < 2; j++)
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++)
-                    ra[j * 4 + kk] = *(const bf16x8 *)(img + off8(mi * 64 + j * 32 + r32, kk * 2 + h32));
-        } else {
+        for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
-                for (int kk = 0; kk < 2; kk++)
-                    ra[j * 2 + kk] = *(const bf16x8 *)(img + off8(mi * 64 + j * 16 + r16, kk * 4 + q));
-        }
+                for (int i = 0; i < 2; i++) acc[a][b][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int r16 = lane & 15, q = lane >> 4;
+    /* operand registers, flattened: ra[j * 2 + kk] (4 frags x 2 k32), rb[i * 2 + kk] */
+    bf16x8 ra[8], rb0[4], rb1[4];
+    auto read_a = [&](const char *buf, int mi) __attribute__((always_inline)) {
+        const char *img = buf + wm * HALF;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++)
+                ra[j * 2 + kk] = *(const bf16x8 *)(img + off8(mi * 64 + j * 16 + r16, kk * 4 + q));
+    
     };
     auto read_b = [&](const char *buf, int ni, bf16x8 (&rb)[4]) __attribute__((always_inline)) {
         const char *img = buf + (2 + (wn >> 1)) * HALF;
-        if constexpr (M32) {
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++)
-                rb[kk] = *(const bf16x8 *)(img + off8((wn & 1) * 64 + ni * 32 + r32, kk * 2 + h32));
-        } else {
+        for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-#pragma unroll
-                for (int kk = 0; kk < 2; kk++)
-                    rb[i * 2 + kk] = *(const bf16x8 *)(img + off8((wn & 1) * 64 + ni * 32 + i * 16 + r16, kk * 4 + q));
-        }
+            for (int kk = 0; kk < 2; kk++)
+                rb[i * 2 + kk] = *(const bf16x8 *)(img + off8((wn & 1) * 64 + ni * 32 + i * 16 + r16, kk * 4 + q));
+    
     };
     auto mma = [&](int mi, int ni, const bf16x8 (&rb)[4]) __attribute__((always_inline)) {
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
-        if constexpr (M32) {
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++)
+        for (int kk = 0; kk < 2; kk++)
 #pragma unroll
-                for (int j = 0; j < 2; j++)
-                    acc32[mi][ni][j] =
-                        __builtin_amdgcn_mfma_f32_32x32x16_bf16(rb[kk], ra[j * 4 + kk], acc32[mi][ni][j], 0, 0, 0);
-        } else {
+            for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int kk = 0; kk < 2; kk++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-#pragma unroll
-                    for (int i = 0; i < 2; i++)
-                        acc[mi][ni][j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[i * 2 + kk], ra[j * 2 + kk],
-                                                                                    acc[mi][ni][j][i], 0, 0, 0);
-        }
+                for (int i = 0; i < 2; i++)
+                    acc[mi][ni][j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[i * 2 + kk], ra[j * 2 + kk],
+                                                                                acc[mi][ni][j][i], 0, 0, 0);
+    
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -288,24 +251,13 @@ __global__ __launch_bounds__(512) void gemm_nt8_kernel(const __bf16 *__restrict_
     for (int mi = 0; mi < 2; mi++)
 #pragma unroll
         for (int ni = 0; ni < 2; ni++) {
-            if constexpr (M32) {
-                /* 32x32 D: column (sample) = lane & 31, rows (features) 8 g + 4 (lane >> 5) + 0..3 */
 #pragma unroll
-                for (int j = 0; j < 2; j++)
+            for (int j = 0; j < 4; j++)
 #pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        const f32x16 &a = acc32[mi][ni][j];
-                        emit(m0 + wm * 128 + mi * 64 + j * 32 + r32, n0 + wn * 64 + ni * 32 + 8 * g + 4 * h32,
-                             f32x4{a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]});
-                    }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-#pragma unroll
-                    for (int i = 0; i < 2; i++)
-                        emit(m0 + wm * 128 + mi * 64 + j * 16 + r16, n0 + wn * 64 + ni * 32 + i * 16 + 4 * q,
-                             acc[mi][ni][j][i]);
-            }
+                for (int i = 0; i < 2; i++)
+                    emit(m0 + wm * 128 + mi * 64 + j * 16 + r16, n0 + wn * 64 + ni * 32 + i * 16 + 4 * q,
+                         acc[mi][ni][j][i]);
+        
         }
 }
 
@@ -593,21 +545,13 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
     }
 }
 
-/* MFMA shape of the NT kernel: 0 = 16x16x32, 1 = 32x32x16 (HPNN_NT8_M32, A/B switch) */
-int g_nt8_m32 = [] { const char *e = getenv("HPNN_NT8_M32"); return e && e[0] == '1' ? 1 : 0; }();
 
 template <int EPI, bool CF32>
 int launch8(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M, int N,
             int K, hipStream_t s, int splits = 1, long cstride = 0) {
     const int tiles_n = N / 256, ntiles = (M / 256) * tiles_n;
-    if (g_nt8_m32)
-        hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32, true>), dim3(ntiles * splits), dim3(512), 0, s,
-                           (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K,
-                           tiles_n, ntiles, splits, cstride);
-    else
-        hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32, false>), dim3(ntiles * splits), dim3(512), 0, s,
-                           (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K,
-                           tiles_n, ntiles, splits, cstride);
+    hipLaunchKernelGGL((gemm_nt8_kernel<EPI, CF32>), dim3(ntiles * splits), dim3(512), 0, s, (const __bf16 *)A, lda,
+                       (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n, ntiles, splits, cstride);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -757,4 +701,4 @@ extern "C" int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, 
 #undef HPNN_SKE
 }
 
-extern "C" void hpnn_gemm_nt8_set_m32(int on) { g_nt8_m32 = on ? 1 : 0; }
+

@@ -374,20 +374,9 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
     if (!big_off && g_nt8 && K % 128 == 0 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 &&
         K >= 512)
         return hpnn_gemm_nt8_bf16(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, EPI, CF32 ? 1 : 0, s);
-    /* fewer 256x256 tiles than CUs but a long K: split-K on the 8-phase kernel.  Opt-in
-     * (HPNN_NT_SPLITK=1): measured slower on the RRUFF-shaped first layer (16384 x 256 x
-     * 4096, 4 splits: 168-169 vs 160 us per step with the 128x128 kernel,
-     * scripts/gpu_splitk.sh) -- the 67 MB of FP32 slabs cost more than the idle CUs */
-    static const int splitk = [] { const char *e = getenv("HPNN_NT_SPLITK"); return e && e[0] == '1'; }();
-    if (splitk && !big_off && g_nt8 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 32) {
-        const long t8 = (long)(M / 256) * (N / 256);
-        const int S = (int)((256 + t8 - 1) / t8);
-        if (S >= 2 && S <= 8 && K % (128 * S) == 0 && K / S >= 512) {
-            const int rc = hpnn_gemm_nt8_splitk_bf16(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, EPI, CF32 ? 1 : 0,
-                                                     S, s);
-            if (rc != -1) return rc;
-        }
-    }
+    /* (a split-K form of the 8-phase kernel for grids of fewer 256x256 tiles than CUs,
+     * hpnn_gemm_nt8_splitk_bf16, measured slower on the RRUFF-shaped first layer: 168 vs
+     * 160 us per step -- the FP32 slabs cost more than the idle CUs; not dispatched here) */
     if (!big_off && k64 && M % 256 == 0 && N % 256 == 0 && (long)(M / 256) * (N / 256) >= 256 && K >= 512)
         return launch_nt_big<EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s);
 #define HPNN_NT(BN_)                                                                                  \
@@ -417,42 +406,13 @@ int launch_tn_t(const void *D, int ldd, const void *H, int ldh, float *slab, int
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-/* HPNN_TN_DEEP: 1 forces the deep ring, 0 disables it; unset = deep ring when the GEMM
- * grid has at most HPNN_TN_DEEP_MAX_WG workgroups (default 0: off).  Measured and rejected
- * for MNIST's G0 (800x128 over 65536 rows, 48 splits): 74.3-74.6 us/step with the deep
- * ring vs 73.4-73.5 us with the 72 KiB ring (the tail reduction workgroups lose their
- * co-residence with the GEMM workgroups); fewer / more splits with the deep ring were
- * slower still (32: 80.3, 40: 76.2, 64: 88.3, 96: 84.1 us) -- scripts/gpu_ab_tn.sh */
-int tn_deep_mode() {
-    static const int v = [] { const char *e = getenv("HPNN_TN_DEEP"); return e ? atoi(e) : -1; }();
-    return v;
-}
-
-#ifndef HPNN_TN_DEEP_MAX_WG
-#define HPNN_TN_DEEP_MAX_WG 0
-#endif
-
+/* (Measured and rejected for MNIST's G0, 800 x 128 over 65536 rows, 48 splits: a deep
+ * ~144 KiB ring, one workgroup per CU, 74.3-74.6 vs 73.4-73.5 us per step -- the tail
+ * reduction workgroups lose their co-residence; 8-wave / 64-row-stage variants 28.6-33.6
+ * vs 29.6-29.8 us for the GEMM alone, none a clear win) */
 template <int TM>
 int launch_tn_m(const void *D, int ldd, const void *H, int ldh, float *slab, int ldg, int N, int M, int Bt, int splits,
                 hipStream_t s, const TnTail &t) {
-    const int dm = tn_deep_mode();
-    const long wgs = (long)(N / 128) * (M / TM) * splits;
-    /* HPNN_TN_VAR (experiments, TM = 160 / N % 128 == 0): 1 = 8 waves, 32-row stages, 72 KiB
-     * ring; 2 = 8 waves, 64-row stages, 144 KiB; 3 = 4 waves, 64-row stages, 144 KiB;
-     * 4 = 8 waves, 32-row stages, 144 KiB; 5 = 8 waves, 64-row stages, 72 KiB.  MNIST G0
-     * (800 x 128 over 65536 rows, 48 splits), scripts/g0_sweep.py: default 29.6-29.8 us,
-     * 1: 31.8, 2: 30.4, 3: 28.6-29.0, 4: 33.6, 5: 28.9; D stored pre-tiled for linear
-     * 1 KiB LDS-DMA pieces (a DT template flag, timing probe): 27.9-30.1 -- none a clear win */
-    static const int var = [] { const char *e = getenv("HPNN_TN_VAR"); return e ? atoi(e) : 0; }();
-    if constexpr (TM == 160) {
-        if (N % 128 == 0 && var == 1) return launch_tn_t<TM, 128, 73728, 6, 32, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
-        if (N % 128 == 0 && var == 2) return launch_tn_t<TM, 128, 147456, 6, 64, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
-        if (N % 128 == 0 && var == 3) return launch_tn_t<TM, 128, 147456, 6, 64, 2, 2>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
-        if (N % 128 == 0 && var == 4) return launch_tn_t<TM, 128, 147456, 8, 32, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
-        if (N % 128 == 0 && var == 5) return launch_tn_t<TM, 128, 73728, 6, 64, 2, 4>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
-    }
-    if (N % 128 == 0 && (dm == 1 || (dm < 0 && wgs <= HPNN_TN_DEEP_MAX_WG)))
-        return launch_tn_t<TM, 128, 147456, 8>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     if (N % 128 == 0) return launch_tn_t<TM, 128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     if (N % 64 == 0) return launch_tn_t<TM, 64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);
     return launch_tn_t<TM, 32>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, s, t);

@@ -652,95 +652,6 @@ __global__ __launch_bounds__(256) void sgd_update_multi_kernel(UpdArgs a) {
              blockIdx.x - a.tile0[l], a.lr, a.alpha, a.scale, a.momentum, tile);
 }
 
-/* Optimizer step for layers with many gradient slabs: 1024 threads (16 waves) per 32x32
- * tile.  Wave w sums the slabs w, w+16, ... of the tile (lane l holds tile elements
- * e = l + 64 i, i < 4, of the tile seen as 256 f32x4: row e/8, columns 4(e%8)..+3), two
- * slabs per iteration (8 loads in flight per lane); the 16 partials meet in LDS in wave
- * order (deterministic), then threads 0..255 apply the step exactly as sgd_tile.  The
- * narrow kernel above had each thread walk all S slabs of its element alone, which left
- * the step latency-bound at ~110 workgroups for MNIST's 96-slab first layer. */
-__global__ __launch_bounds__(1024) void sgd_update_multi_wide_kernel(UpdArgs a) {
-    __shared__ f32x4 part[16][256];
-    __shared__ float tilebuf[32][33];
-    int l = 0;
-    while (l + 1 < a.n && (int)blockIdx.x >= a.tile0[l + 1]) l++;
-    const hpnn_upd_layer &L = a.L[l];
-    const int tile = blockIdx.x - a.tile0[l];
-    const int tiles_k = L.K / 32;
-    const int tn = tile / tiles_k, tk = tile % tiles_k;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    size_t off[4];
-    f32x4 acc[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int e = lane + 64 * i;
-        off[i] = (size_t)(tn * 32 + (e >> 3)) * L.K + tk * 32 + (e & 7) * 4;
-        acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    int s = w;
-    for (; s + 16 < L.S; s += 32) {
-        const float *g0 = L.G + (long)s * L.gstride, *g1 = g0 + 16 * L.gstride;
-        f32x4 x[4], y[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) x[i] = *(const f32x4 *)(g0 + off[i]);
-#pragma unroll
-        for (int i = 0; i < 4; i++) y[i] = *(const f32x4 *)(g1 + off[i]);
-#pragma unroll
-        for (int i = 0; i < 4; i++) acc[i] += x[i] + y[i];
-    }
-    if (s < L.S) {
-        const float *g0 = L.G + (long)s * L.gstride;
-#pragma unroll
-        for (int i = 0; i < 4; i++) acc[i] += *(const f32x4 *)(g0 + off[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) part[w][lane + 64 * i] = acc[i];
-    __syncthreads();
-    const int t = threadIdx.x;
-    const bool act = t < 256;
-    const int tx = t & 7, ty = (t >> 3) & 31;
-    const int n = tn * 32 + ty, k = tk * 32 + tx * 4;
-    const size_t idx = (size_t)n * L.K + k;
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    if (act) {
-        f32x4 g = part[0][t];
-#pragma unroll
-        for (int ww = 1; ww < 16; ww++) g += part[ww][t];
-        f32x4 wv = *(const f32x4 *)(L.W32 + idx);
-        if (a.momentum) {
-            f32x4 v = *(const f32x4 *)(L.V32 + idx);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                v[r] += a.lr * (g[r] * a.scale);
-                wv[r] += v[r];
-                v[r] *= a.alpha;
-            }
-            *(f32x4 *)(L.V32 + idx) = v;
-        } else {
-#pragma unroll
-            for (int r = 0; r < 4; r++) wv[r] += a.lr * (g[r] * a.scale);
-        }
-        *(f32x4 *)(L.W32 + idx) = wv;
-        bf16x4 wb;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            wb[r] = (__bf16)wv[r];
-            tilebuf[ty][tx * 4 + r] = wv[r];
-        }
-        *(bf16x4 *)((__bf16 *)L.Wbf + idx) = wb;
-        if (L.Wf) {
-            const size_t fo = (((size_t)(n >> 4) * tiles_k + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
-            *(bf16x4 *)((__bf16 *)L.Wf + fo) = wb;
-        }
-    }
-    __syncthreads();
-    if (act) {
-        bf16x4 tb;
-#pragma unroll
-        for (int r = 0; r < 4; r++) tb[r] = (__bf16)tilebuf[tx * 4 + r][ty];
-        *(bf16x4 *)((__bf16 *)L.Wt + (size_t)(tk * 32 + ty) * L.N + tn * 32 + tx * 4) = tb;
-    }
-}
 
 /* Same step over 8-row sub-tiles (8 x 32 elements, one f32x4 per lane of a wave): four
  * workgroups per 32x32 tile, so MNIST's update (~110 tiles) fills the 256 CUs (~440
@@ -950,14 +861,10 @@ extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float 
     int max_s = 0;
     for (int l = 0; l < n; l++) max_s = layers[l].S > max_s ? layers[l].S : max_s;
     static const int wide_off = [] { const char *e = getenv("HPNN_UPD_NARROW"); return e && atoi(e) ? 1 : 0; }();
-    /* HPNN_UPD_MODE=1: one 16-wave workgroup per 32x32 tile (previous default) */
-    static const int tile_mode = [] { const char *e = getenv("HPNN_UPD_MODE"); return e ? atoi(e) : 0; }();
-    if (max_s >= 8 && !wide_off && tile_mode != 1) {
+    if (max_s >= 8 && !wide_off) {
         for (int l = 0; l <= n; l++) a.tile0[l] *= 4;
         hipLaunchKernelGGL(sgd_update_multi_sub_kernel, dim3(4 * t), dim3(512), 0, stream, a);
-    } else if (max_s >= 8 && !wide_off)
-        hipLaunchKernelGGL(sgd_update_multi_wide_kernel, dim3(t), dim3(1024), 0, stream, a);
-    else
+    } else
         hipLaunchKernelGGL(sgd_update_multi_kernel, dim3(t), dim3(256), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -41,8 +41,6 @@ using namespace hpnn::mlp3;
 namespace {
 
 constexpr int FR = 32;   /* samples per tile */
-/* MODE 9 timeline (profiling only): block 0, waves 0..7, stages 0..7, 8 marks per stage */
-__device__ unsigned long long g_fz_trace[8][8][8];
 constexpr int NCH = 4;   /* X chunks (intervals) per tile */
 
 template <int KS>
@@ -96,10 +94,7 @@ __device__ __forceinline__ void load_img8(const __bf16 *g, int ld, char *img, in
 
 __device__ __forceinline__ int clamp_sample(int s, int n_valid) { return s < n_valid ? s : (n_valid > 0 ? n_valid - 1 : 0); }
 
-/* MODE (profiling experiments only, HPNN_FZ_MODE): 0 normal, 1 no back phases, 2 no front MFMAs,
- * 3 no X DMA, 4 no W0 load, 5 no P2, 6 no P4, 7 no P5/P6, 8 no P1/P3, 9 normal + s_memtime
- * timeline of block 0 (hpnn_mlp3_fused_trace) */
-template <int TYPE, bool LABELS, int KS, int MODE = 0>
+template <int TYPE, bool LABELS, int KS>
 __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__restrict__ X, int ldx,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -139,7 +134,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
     auto issue_chunk = [&](int u, auto cc) {
         constexpr int c = decltype(cc)::value;
         constexpr int P = XP::pieces(c), p0 = XP::piece0(c), LC = XP::L(c);
-        if constexpr (MODE == 3 || MODE == 10 || LC == 0) return;
+        if constexpr (LC == 0) return;
         const char *g = (const char *)(X + (size_t)tile_of(u) * R * ldx);
         char *img = lds + (u & 1) * LY::XST;
 #pragma unroll
@@ -170,8 +165,7 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
     bf16x8 w0[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
-        if constexpr (MODE == 4) w0[ks] = bf16x8{};
-        else w0[ks] = *(const bf16x8 *)(W0f + ((size_t)(wave * KS + ks) * 64 + lane) * 8);
+        w0[ks] = *(const bf16x8 *)(W0f + ((size_t)(wave * KS + ks) * 64 + lane) * 8);
     }
     load_img8<H2, H1>(W1, H1, imgW1, wave, lane);
     load_img8<NO, H2>(W2, H2, imgW2, wave, lane);
@@ -195,17 +189,9 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
     /* one stage = front part of tile t (FW) + back part of tile t-1 (BW); FW / BW are
      * compile-time so that, inside every interval, the front MFMAs and the back chain of a
      * wave form ONE basic block the scheduler can interleave */
-    auto mark = [&](int t, int i) {
-        if constexpr (MODE == 9 || MODE == 10) {
-            if (blockIdx.x == 0 && t < 8) {
-                const unsigned long long m = __builtin_amdgcn_s_memtime();
-                if (lane == 0) g_fz_trace[wave][t][i] = m;
-            }
-        }
-    };
     auto stage = [&](int t, auto FWc, auto BWc) {
-        constexpr bool FW = decltype(FWc)::value && MODE != 2;
-        constexpr bool BW = decltype(BWc)::value && MODE != 1;
+        constexpr bool FW = decltype(FWc)::value;
+        constexpr bool BW = decltype(BWc)::value;
         const int tb = t - 1;
         const char *imgX = lds + (t & 1) * LY::XST;
         char *H1w = lds + LY::OFF_H1 + (t & 1) * LY::IMG_H1;       /* front writes tile t  */
@@ -342,47 +328,39 @@ __global__ __launch_bounds__(512, 1) void mlp3_fused_kernel(const __bf16 *__rest
         };
 
         /* ============ interval 0: X chunk 0 | P1 ============ */
-        mark(t, 0);
         if (issuer) wait_vm<W_X0>();
         lds_barrier();
-        mark(t, 1);
         if (issuer) {
             issue_label(t);
             issue_chunk(t + 1, C3{});
         }
-        order([&] { if constexpr (BW && MODE != 8) p1(); }, [&] { front_chunk(C0{}); });
+        order([&] { if constexpr (BW) p1(); }, [&] { front_chunk(C0{}); });
 
         /* ============ interval 1: X chunk 1 | P2 (waves 0, 1) ============ */
-        mark(t, 2);
         if (issuer) wait_vm<W_B1>();
         lds_barrier();
-        mark(t, 3);
         if (issuer) issue_chunk(t + 2, C0{});
-        order([&] { if (BW && MODE != 5 && wave < 2) p2(); }, [&] { front_chunk(C1{}); });
+        order([&] { if (BW && wave < 2) p2(); }, [&] { front_chunk(C1{}); });
 
         /* ============ interval 2: X chunk 2 | P3, P5 ============ */
-        mark(t, 4);
         if (issuer) wait_vm<W_X2>();
         lds_barrier();
-        mark(t, 5);
         if (issuer) issue_chunk(t + 2, C1{});
         order(
             [&] {
-                if constexpr (BW && MODE != 8) p3();
-                if constexpr (BW && MODE != 7) p5();
+                if constexpr (BW) p3();
+                if constexpr (BW) p5();
             },
             [&] { front_chunk(C2{}); });
 
         /* ============ interval 3: X chunk 3 + H1(t) | P4 (waves 0-3), P6 ============ */
-        mark(t, 6);
         if (issuer) wait_vm<W_X3>();
         lds_barrier();
-        mark(t, 7);
         if (issuer) issue_chunk(t + 2, C2{});
         order(
             [&] {
-                if (BW && MODE != 6 && !issuer) p4();
-                if constexpr (BW && MODE != 7) p6();
+                if (BW && !issuer) p4();
+                if constexpr (BW) p6();
             },
             [&] { front_chunk(C3{}); });
         if constexpr (FW) {
@@ -449,38 +427,15 @@ template <int TYPE, bool LABELS, int KS>
 int launch_fused(const void *X, int ldx, const void *W0f, const void *W1, const void *W2, const int *labels,
                  const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab, float *loss_acc,
                  unsigned int *correct, int Bp, int n_valid, int n_out, int grid, int d1fm, hipStream_t stream) {
-    static const int mode = [] { const char *e = getenv("HPNN_FZ_MODE"); return e ? atoi(e) : 0; }();
-#define HPNN_FZL(MD)                                                                                             \
-    do {                                                                                                         \
-        static bool attr = false;                                                                                \
-        if (!attr) {                                                                                             \
-            (void)hipFuncSetAttribute((const void *)mlp3_fused_kernel<TYPE, LABELS, KS, MD>,                     \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, Lay<KS>::TOTAL);               \
-            attr = true;                                                                                         \
-        }                                                                                                        \
-        hipLaunchKernelGGL((mlp3_fused_kernel<TYPE, LABELS, KS, MD>), dim3(grid), dim3(512), Lay<KS>::TOTAL,     \
-                           stream, (const __bf16 *)X, ldx, (const __bf16 *)W0f, (const __bf16 *)W1,              \
-                           (const __bf16 *)W2, labels, T, ldt, t_hi, t_lo, (__bf16 *)D1, gslab, loss_acc, correct, \
-                           Bp / FR, n_valid, n_out, d1fm);                                                       \
-    } while (0)
-    if constexpr (TYPE == 2 && LABELS && KS == 25) {
-        switch (mode) {
-        case 1: HPNN_FZL(1); break;
-        case 2: HPNN_FZL(2); break;
-        case 3: HPNN_FZL(3); break;
-        case 4: HPNN_FZL(4); break;
-        case 5: HPNN_FZL(5); break;
-        case 6: HPNN_FZL(6); break;
-        case 7: HPNN_FZL(7); break;
-        case 8: HPNN_FZL(8); break;
-        case 9: HPNN_FZL(9); break;
-        case 10: HPNN_FZL(10); break;
-        default: HPNN_FZL(0);
-        }
-    } else {
-        HPNN_FZL(0);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)mlp3_fused_kernel<TYPE, LABELS, KS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, Lay<KS>::TOTAL);
+        attr = true;
     }
-#undef HPNN_FZL
+    hipLaunchKernelGGL((mlp3_fused_kernel<TYPE, LABELS, KS>), dim3(grid), dim3(512), Lay<KS>::TOTAL, stream,
+                       (const __bf16 *)X, ldx, (const __bf16 *)W0f, (const __bf16 *)W1, (const __bf16 *)W2, labels, T,
+                       ldt, t_hi, t_lo, (__bf16 *)D1, gslab, loss_acc, correct, Bp / FR, n_valid, n_out, d1fm);
     return hipGetLastError() == hipSuccess ? grid : -5;
 }
 
@@ -503,12 +458,6 @@ int launch_fused_k(const void *X, int ldx, const void *W0f, const void *W1, cons
 #undef HPNN_FZ
 }
 
-/* HPNN_FRONT=f selects the role-split kernel (kernels_mlp3f.hip); default: this one */
-bool front_split() {
-    static const bool v = [] { const char *e = getenv("HPNN_FRONT"); return e && e[0] == 'f'; }();
-    return v;
-}
-
 }  // namespace
 
 extern "C" int hpnn_mlp3_fused_grid(int Bp, int grid) { return Bp > 0 && Bp % FR == 0 ? fused_grid(Bp, grid) : -2; }
@@ -520,10 +469,6 @@ extern "C" int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, 
     if (Bp <= 0 || Bp % FR || n_out > NO || n_out < 1 || ldx % 8 || ldx < K0) return -2;
     if (!labels && !T) return -1;
     grid = fused_grid(Bp, grid);
-    /* HPNN_FRONT=f: the role-split kernel (kernels_mlp3f.hip; row-major delta1 only) */
-    if (front_split() && K0 >= 800 && !d1fm)
-        return hpnn_mlp3_front(X, ldx, K0, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct,
-                               Bp, n_valid, n_out, type, grid, stream);
 #define HPNN_FK(K_)                                                                                             \
     if (K0 == K_)                                                                                               \
     return launch_fused_k<K_ / 32>(X, ldx, W0f, W1, W2, labels, T, ldt, t_hi, t_lo, D1, gslab, loss_acc, correct, \
@@ -535,10 +480,4 @@ extern "C" int hpnn_mlp3_fused(const void *X, int ldx, int K0, const void *W0f, 
     HPNN_FK(896);
 #undef HPNN_FK
     return -3;
-}
-
-/* MODE 9 timeline: out[8 waves][8 stages][8 marks] shader-clock ticks (block 0) */
-extern "C" int hpnn_mlp3_fused_trace(unsigned long long *out) {
-    if (front_split()) return hpnn_mlp3_front_trace(out);
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fz_trace), sizeof(g_fz_trace)) == hipSuccess ? 0 : -5;
 }

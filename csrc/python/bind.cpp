@@ -63,7 +63,6 @@ PYBIND11_MODULE(_native, m) {
                   "output_delta");
         });
     m.def("gemm_nt_set_8ph", [](int on) { hpnn_gemm_nt_set_8ph(on); });
-    m.def("gemm_nt8_set_m32", [](int on) { hpnn_gemm_nt8_set_m32(on); });
     m.def("gemm_tn8_update", [](uptr D, int ldd, uptr H, int ldh, int N, int M, int Bt, uptr W32, uptr V32, uptr Wbf,
                                 uptr Wt, float lr, float alpha, float scale, int momentum, uptr stream) {
         const int rc = hpnn_gemm_tn8_update(P(D), ldd, P(H), ldh, N, M, Bt, (float *)P(W32), (float *)P(V32), P(Wbf),
@@ -127,11 +126,6 @@ PYBIND11_MODULE(_native, m) {
         if (rc <= 0) check(rc ? rc : -1, "mlp3_fused");
         return rc;
     });
-    m.def("mlp3_fused_trace", []() {
-        std::vector<unsigned long long> v(8 * 8 * 8);
-        check(hpnn_mlp3_fused_trace(v.data()), "mlp3_fused_trace");
-        return v;
-    });
     m.def("mlp3_tile", [](uptr Xg, int xu8, float xscale, int K0, uptr W0f, uptr W1, uptr W2, uptr W2t, uptr labels,
                           uptr T, int ldt, float t_hi, float t_lo, uptr D1, uptr gslab, uptr loss, uptr correct, int Bp,
                           int n_valid, int n_out, int type, int grid, uptr stream) {
@@ -166,13 +160,6 @@ PYBIND11_MODULE(_native, m) {
         return v;
     });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
-    m.def("gemm_tn_rs", [](uptr D, int ldd, uptr H, int ldh, int h_u8, float hscale, uptr slab, int ldg, int N, int M,
-                           int Bt, int splits, uptr rslab, int rS, long rstride, long rn, int rgroups, uptr rout,
-                           uptr stream) {
-        check(hpnn_gemm_tn_rs(P(D), ldd, P(H), ldh, h_u8, hscale, (float *)P(slab), ldg, N, M, Bt, splits,
-                              (const float *)P(rslab), rS, rstride, rn, rgroups, (float *)P(rout), S(stream)),
-              "gemm_tn_rs");
-    });
     m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, int h_u8, float hscale, uptr slab, int ldg, int N, int M, int Bt,
                                int splits, uptr stream) {
         check(hpnn_gemm_fm_direct(P(Dg), P(Hg), h_u8, hscale, (float *)P(slab), ldg, N, M, Bt, splits, S(stream)),

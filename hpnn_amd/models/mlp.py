@@ -22,18 +22,6 @@ import torch
 
 from .. import ops
 
-# HPNN_SIDE_REDUCE=1: run the first [G1|G2] reduction pass on a second stream next to the
-# G0 GEMM (fused path); off by default (cross-stream fork/join inside the graph measured
-# slower than back-to-back launches on MI355X)
-_SIDE_REDUCE = os.environ.get("HPNN_SIDE_REDUCE", "0") == "1"
-# HPNN_TAIL_REDUCE=0: separate reduce_groups launch instead of the GEMM's tail workgroups
-_TAIL_REDUCE = os.environ.get("HPNN_TAIL_REDUCE", "1") == "1"
-# HPNN_G0_FM=1, fused "x" path: first-layer gradient from fragment-major operands
-# (csrc/gpu/kernels_g0.hip).  Off by default: in the training step the fragment-major
-# copy of X is cold (the fused front has just streamed the row-major X, which the
-# LDS-staged TN GEMM then re-reads partly from the MALL): 82-83 us/step vs 77.3-77.8
-# (G0 37.8 vs 34.1 us under rocprofv3, scripts/gpu_fm_prof.sh)
-_G0_FM = os.environ.get("HPNN_G0_FM", "0") == "1"
 # uint8 (pixel) input on the fused path: fragment-major 8-bit copy for the G0 kernel
 # (HPNN_G0_FM_U8=0 disables: LDS-staged TN GEMM on the BF16 batch)
 _G0_FM_U8 = os.environ.get("HPNN_G0_FM_U8", "1") == "1"
@@ -43,10 +31,6 @@ PIXEL_SCALE = float(torch.tensor(float(os.environ.get("HPNN_PIXEL_SCALE", str(1.
 # HPNN_TILE=0: the 32-sample pipelined front (mlp3_fused, "x") instead of the 256-sample
 # tile kernel (mlp3_tile, "t") on eligible MNIST-shaped nets
 _TILE = os.environ.get("HPNN_TILE", "1") != "0"
-# HPNN_G0_RS=1: first-layer gradient with the register-staged TN kernel (kernels_g0.hip):
-# 75.46-76.57 us/step vs 75.73-77.32 with the LDS-DMA TN kernel (scripts/gpu_ab_g0.sh),
-# within noise of each other
-_G0_RS = os.environ.get("HPNN_G0_RS", "0") == "1"
 
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
@@ -196,11 +180,6 @@ class MLP:
                 return s
         return 0
 
-    def _side_stream(self):
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        return self._side
-
     def refresh_bf16(self):
         for l in range(self.L):
             ops.cast_weights(self.W32[l], self.Wb[l], self.Wt[l], self.W0f if l == 0 else None)
@@ -219,8 +198,8 @@ class MLP:
         also carries the pixels themselves in fragment-major order (attribute `hpnn_fm`,
         ops.to_fragment_major, one byte per value): the first-layer gradient kernel
         (csrc/gpu/kernels_g0.hip) streams that copy -- half the bytes of the BF16 batch, no
-        LDS transposes -- and converts it exactly as above.  HPNN_G0_FM=1 attaches a
-        fragment-major BF16 copy for float input too (off by default, see _G0_FM)."""
+        LDS transposes -- and converts it exactly as above.  (The tile path, "t", takes the
+        batch itself fragment-major: _prepare_fm.)"""
         Xd = X.to(self.device)
         if self.fused_mode == "t":
             return self._prepare_fm(Xd)
@@ -235,9 +214,6 @@ class MLP:
                 out.hpnn_fm_scale = PIXEL_SCALE
             return out
         ops.pack_bf16(Xd.contiguous(), out)
-        if self.fused_mode == "x" and _G0_FM:
-            out.hpnn_fm = ops.to_fragment_major(out)
-            out.hpnn_fm_scale = 1.0
         return out
 
     def _prepare_fm(self, Xd):
@@ -392,9 +368,6 @@ class MLP:
         if Xg is not None:
             ops.gemm_fm_direct_reduce(self.D[0], Xg, self.Np[0], self.Kp[0], self.S[0], self.slab[0], self.midslab,
                                       self.mid_groups, groups, hscale=getattr(X, "hpnn_fm_scale", 1.0))
-        elif _G0_RS and (self.Kp[0] % 128 == 0 or self.Kp[0] % 160 == 0):
-            ops.gemm_tn_rs(self.D[0], X, self.S[0], self.slab[0], rslab=self.midslab, groups=self.mid_groups,
-                           rout=groups)
         else:
             ops.gemm_tn_reduce(self.D[0], X, self.S[0], self.slab[0], self.midslab, self.mid_groups, groups)
 
@@ -403,28 +376,12 @@ class MLP:
         n_valid = self.Bp if n_valid is None else n_valid
         scale = 1.0 / n_valid
         if self.fused_mode in ("x", "t"):
-            # 4 launches: fused front, then the G0 GEMM and the first [G1|G2] reduction pass
-            # side by side (the reduction forks onto a second stream: it only needs the
-            # fused front's block slabs and fills CUs the memory-bound GEMM leaves idle),
-            # then every layer's update
+            # 3 launches: fused front; the G0 GEMM with the first [G1|G2] reduction pass on
+            # tail workgroups appended to its grid (they fill the CUs the GEMM tiles leave
+            # idle); every layer's update
             self._fused_front(X, labels, T, n_valid)
             groups = self.midtmp[:self.mid_groups * ops.MLP3_SLAB].view(self.mid_groups, ops.MLP3_SLAB)
-            if self._fm_input(X) is not None or _G0_RS:
-                self._g0_reduce(X, groups)
-            elif self.device.type == "cuda" and _SIDE_REDUCE:
-                main = torch.cuda.current_stream(self.device)
-                side = self._side_stream()
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    ops.reduce_groups(self.midslab, self.mid_groups, groups)
-                ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
-                main.wait_stream(side)
-            elif _TAIL_REDUCE:
-                # one launch: the reduction rides on workgroups appended to the GEMM grid
-                ops.gemm_tn_reduce(self.D[0], X, self.S[0], self.slab[0], self.midslab, self.mid_groups, groups)
-            else:
-                ops.gemm_tn(self.D[0], X, splits=self.S[0], out=self.slab[0])
-                ops.reduce_groups(self.midslab, self.mid_groups, groups)
+            self._g0_reduce(X, groups)
             g1, g2 = self._mid_group_views()
             self.update_all(lr, alpha, scale, [self.slab[0], g1, g2])
             return

@@ -105,27 +105,6 @@ def gemm_tn_reduce(D, H, splits, out, rslab, groups, rout):
     return rout
 
 
-def gemm_tn_rs(D, H, splits=1, out=None, rslab=None, groups=1, rout=None, hscale=1.0):
-    """gemm_tn (and optionally reduce_groups(rslab, groups, rout) on tail workgroups) with
-    register-staged operands (csrc/gpu/kernels_g0.hip gemm_tn_rs_kernel).  H may be uint8
-    (pixel data): used as bf16(H * hscale), converted while staging."""
-    Bt, N = D.shape
-    M = H.shape[1]
-    u8 = H.dtype == torch.uint8
-    if out is None:
-        out = torch.empty(splits, N, M, dtype=torch.float32, device=D.device)
-    if _cpu(D):
-        gemm_tn(D, (H.float() * hscale).bfloat16() if u8 else H, splits=splits, out=out)
-        if rslab is not None:
-            reduce_groups(rslab, groups, rout)
-        return out
-    native().gemm_tn_rs(D.data_ptr(), D.stride(0), H.data_ptr(), H.stride(0), int(u8), float(hscale), out.data_ptr(),
-                        out.stride(1), N, M, Bt, splits, _ptr(rslab), rslab.shape[0] if rslab is not None else 0,
-                        rslab.stride(0) if rslab is not None else 0, rslab[0].numel() if rslab is not None else 0,
-                        groups, _ptr(rout), _stream())
-    return out
-
-
 def to_fragment_major(A):
     """[Bt, M] (batch rows) -> fragment-major [Bt/32, M/16, 64, 8]: lane l = 16 g + r of
     fragment (t, rb) holds A[t*32 + 8g + j, rb*16 + r], j < 8 (the MFMA operand layout of a

@@ -43,13 +43,11 @@ def main():
     res = {}
     from hpnn_amd._lib import native
     for rnd in range(2):  # interleaved A/B in one process: 1-phase vs 8-phase 256x256 NT kernel
-        for mode, tag in ((0, "1ph"), (1, "8ph"), (2, "8ph_m32")):
+        for mode, tag in ((0, "1ph"), (1, "8ph")):
             native().gemm_nt_set_8ph(1 if mode else 0)
-            native().gemm_nt8_set_m32(1 if mode == 2 else 0)
             res[f"nt_fwd_act_{tag}_r{rnd}"] = t(lambda: ops.gemm_nt(X, W, ops.EPI_ACT, out=out))
             res[f"nt_bwd_dact_{tag}_r{rnd}"] = t(lambda: ops.gemm_nt(D, Wt, ops.EPI_DACT, aux=X, out=dx))
     native().gemm_nt_set_8ph(1)
-    native().gemm_nt8_set_m32(0)
     S = 1
     slab = torch.empty(S, N, K, dtype=torch.float32, device=dev)
     for rnd in range(2):

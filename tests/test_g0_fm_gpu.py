@@ -60,7 +60,7 @@ def test_fused_front_fragment_major_delta1(gpu, net):
     B = 8192
     m = MLP([784, 128, 64, 10], net, batch=B, seed=2, fused="x")
     X = m.prepare_input(torch.rand(B, 784))
-    X.hpnn_fm = ops.to_fragment_major(X)  # what prepare_input attaches with HPNN_G0_FM=1
+    X.hpnn_fm = ops.to_fragment_major(X)  # a fragment-major copy attached by hand
     assert m._fm_input(X) is not None
     lab = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
     Xrm = X.clone()  # no fragment-major copy attached: row-major delta1
@@ -89,28 +89,12 @@ def test_train_step_fragment_major_matches_tn(gpu):
         for x, lab in zip(xs, labs):
             X = m.prepare_input(x)
             if i == 0:
-                X.hpnn_fm = ops.to_fragment_major(X)  # fragment-major G0 path (HPNN_G0_FM=1)
+                X.hpnn_fm = ops.to_fragment_major(X)  # fragment-major G0 path (copy attached by hand)
             m.train_step(X, labels=lab, lr=0.05, alpha=0.2)
     torch.cuda.synchronize()
     for l in range(3):
         e = (ms[0].W32[l] - ms[1].W32[l]).abs().max().item()
         assert e < 1e-5, (l, e)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("Bt,N,M,S", [(65536, 128, 800, 48), (8192, 128, 512, 8), (4096, 128, 256, 3)])
-def test_gemm_tn_register_staged_matches_fp32(gpu, Bt, N, M, S):
-    torch.manual_seed(Bt + M)
-    D, H = _bf(Bt, N, scale=0.25), _bf(Bt, M)
-    rslab = torch.randn(20, ops.MLP3_SLAB, device="cuda")
-    rout = torch.empty(4, ops.MLP3_SLAB, device="cuda")
-    slab = ops.gemm_tn_rs(D, H, splits=S, rslab=rslab, groups=4, rout=rout)
-    ref_slab = ops.gemm_tn(D, H, splits=S)
-    torch.cuda.synchronize()
-    assert (slab.sum(0) - D.float().t() @ H.float()).abs().max().item() < 1e-5 * Bt ** 0.5 * 4 + 1e-4
-    assert (slab - ref_slab).abs().max().item() < 1e-3  # same split boundaries as the TN kernel
-    for g in range(4):
-        assert (rout[g] - rslab[5 * g:5 * g + 5].sum(0)).abs().max().item() < 1e-4
 
 
 @pytest.mark.gpu

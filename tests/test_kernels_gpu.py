@@ -77,17 +77,12 @@ def test_gemm_nt_big_tile(gpu, M, N, K, epi):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 384), (256, 1024, 1152),
                                    (2304, 256, 640)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
-@pytest.mark.parametrize("m32", [0, 1])
-def test_gemm_nt8(gpu, M, N, K, epi, m32):
+def test_gemm_nt8(gpu, M, N, K, epi):
     """the 8-phase 256x256 kernel (kernels_8ph.hip) called directly at small grids: one
     iteration (K = 128, no restaging), odd iteration counts, a ragged XCD split (9 tiles),
-    padded row strides on every operand; both MFMA shapes (16x16x32, 32x32x16)"""
+    padded row strides on every operand"""
     from hpnn_amd._lib import native
-    native().gemm_nt8_set_m32(m32)
-    try:
-        _check_nt8(native, M, N, K, epi)
-    finally:
-        native().gemm_nt8_set_m32(0)
+    _check_nt8(native, M, N, K, epi)
 
 
 def _check_nt8(native, M, N, K, epi):
@@ -238,17 +233,14 @@ def _sgd_multi_case(momentum, seed=11):
     return layers, refs
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
 @pytest.mark.parametrize("momentum", [False, True])
-def test_sgd_update_multi_wide(gpu, momentum, mode):
-    """many slabs (>= 8): HPNN_UPD_MODE 0 = 8-row sub-tile kernel (default), 1 = one
-    16-wave workgroup per 32x32 tile; same step as the FP64 reference, bitwise repeatable.
-    The mode is read once per process, so each mode runs in a child process whose
-    environment sets HPNN_UPD_MODE explicitly and drops HPNN_UPD_NARROW."""
+def test_sgd_update_multi_wide(gpu, momentum):
+    """many slabs (>= 8): the 8-row sub-tile kernel; same step as the FP64 reference,
+    bitwise repeatable.  Runs in a child process whose environment drops HPNN_UPD_NARROW
+    (read once per process)."""
     import subprocess
     import sys
-    env = {k: v for k, v in os.environ.items() if k not in ("HPNN_UPD_MODE", "HPNN_UPD_NARROW")}
-    env["HPNN_UPD_MODE"] = mode
+    env = {k: v for k, v in os.environ.items() if k not in ("HPNN_UPD_NARROW",)}
     code = ("import sys, importlib.util as u; sys.path.insert(0, %r); "
             "s = u.spec_from_file_location('tk', %r); t = u.module_from_spec(s); s.loader.exec_module(t); "
             "t._sgd_multi_check(%r)" % (ROOT, os.path.abspath(__file__), momentum))
