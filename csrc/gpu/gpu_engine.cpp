@@ -27,6 +27,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <thread>
 #include <vector>
 
 #include "../core/runtime_internal.h"
@@ -551,7 +552,11 @@ struct Batched {
     bool own_flat = false;
     size_t flat_count() const { return goff[L]; }
 
-    BOOL grads(const void *X, const float *T, int ldt, int n_valid) {
+    /* forward + backward into the flat buffer; ready(lo, hi) is called as soon as the
+     * gradients of layers lo..hi (contiguous in gflat) are final -- last layers first --
+     * so the caller can start their all-reduce while the lower layers are computed */
+    template <class Ready>
+    BOOL grads(const void *X, const float *T, int ldt, int n_valid, Ready &&ready) {
         const float t_lo = type == 2 ? 0.f : -1.f;
         int r = 0;
         if (fused) {
@@ -568,10 +573,12 @@ struct Batched {
                                       acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2],
                                       mid_grid, s);
             }
+            /* [G1 | G2] slab rows are exactly layers 1, 2 of the flat buffer: final first */
+            if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, slab_f, slab_f, midtmp, gflat + goff[1], s);
+            if (!r && !ready(1, 2)) r = -8;
             if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
             if (!r) r = hpnn_reduce_slabs(slab[0], S[0], (long)Np[0] * Kp[0], (long)Np[0] * Kp[0], gflat, s);
-            /* [G1 | G2] slab rows are exactly layers 1, 2 of the flat buffer */
-            if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, slab_f, slab_f, midtmp, gflat + goff[1], s);
+            if (!r && !ready(0, 0)) r = -8;
             if (r) NN_ERROR(stderr, "fused gradients failed: %d\n", r);
             return r == 0;
         }
@@ -579,17 +586,32 @@ struct Batched {
         if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
                               (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
             return FALSE;
-        for (int l = L - 1; l >= 1; l--)
-            if (hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp, Np[l - 1],
-                                  Np[l], HPNN_EPI_DACT, 0, s))
+        /* layer by layer from the top: the delta for layer l-1 (pre-update W_l), then
+         * layer l's gradient into its bucket -- its all-reduce overlaps the layers below */
+        for (int l = L - 1; l >= 0; l--) {
+            if (l >= 1 && hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp,
+                                            Np[l - 1], Np[l], HPNN_EPI_DACT, 0, s))
                 return FALSE;
-        for (int l = 0; l < L; l++) {
             const void *Hin = l ? H[l - 1] : X;
-            if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s)) return FALSE;
-            if (hpnn_reduce_slabs(slab[l], S[l], (long)Np[l] * Kp[l], (long)Np[l] * Kp[l], gflat + goff[l], s))
+            if (S[l] == 1) { /* one split: straight into the bucket */
+                if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], gflat + goff[l], Kp[l], Np[l], Kp[l], Bp, 1, s))
+                    return FALSE;
+            } else if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s) ||
+                       hpnn_reduce_slabs(slab[l], S[l], (long)Np[l] * Kp[l], (long)Np[l] * Kp[l], gflat + goff[l], s))
                 return FALSE;
+            if (!ready(l, l)) return FALSE;
         }
         return TRUE;
+    }
+    BOOL grads(const void *X, const float *T, int ldt, int n_valid) {
+        return grads(X, T, ldt, n_valid, [](int, int) { return true; });
+    }
+    /* the (lo, hi) layer buckets grads() reports, in order */
+    std::vector<std::pair<int, int>> buckets() const {
+        std::vector<std::pair<int, int>> v;
+        if (fused) return {{1, 2}, {0, 0}};
+        for (int l = L - 1; l >= 0; l--) v.push_back({l, l});
+        return v;
     }
 
     /* update every layer from a flat gradient buffer G (this replica's gflat after the
@@ -825,12 +847,32 @@ struct BatchedFP {
     }
     size_t flat_count() const { return goff[L]; }
 
-    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid) {
-        if (!backprop(X, Tt, ldt, n_valid)) return FALSE;
-        for (int l = 0; l < L; l++)
-            if (hpnn_reduce_fp(F64, gflat + goff[l], slab[l], S[l], (long)N[l] * M[l], (long)N[l] * M[l], s))
+    template <class Ready>
+    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid, Ready &&ready) {
+        if (!forward(X, Bp)) return FALSE;
+        if (hpnn_output_fp(F64, Z, N[L - 1], Tt, ldt, D[L - 1], N[L - 1], nullptr, 0, nullptr, acc,
+                           (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
+            return FALSE;
+        for (int l = L - 1; l >= 0; l--) {
+            if (l >= 1 && hpnn_gemm_fp(F64, D[l], N[l], 0, W[l], M[l], 1, D[l - 1], N[l - 1], H[l - 1], N[l - 1], Bp,
+                                       M[l], N[l], HPNN_EPI_DACT, 1, 0, s))
                 return FALSE;
+            const T *Hin = l ? H[l - 1] : (const T *)X;
+            if (hpnn_gemm_fp(F64, D[l], N[l], 1, Hin, M[l], 1, slab[l], M[l], nullptr, 0, N[l], M[l], Bp,
+                             HPNN_EPI_NONE, S[l], (long)N[l] * M[l], s) ||
+                hpnn_reduce_fp(F64, gflat + goff[l], slab[l], S[l], (long)N[l] * M[l], (long)N[l] * M[l], s))
+                return FALSE;
+            if (!ready(l, l)) return FALSE;
+        }
         return TRUE;
+    }
+    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid) {
+        return grads(X, Tt, ldt, n_valid, [](int, int) { return true; });
+    }
+    std::vector<std::pair<int, int>> buckets() const {
+        std::vector<std::pair<int, int>> v;
+        for (int l = L - 1; l >= 0; l--) v.push_back({l, l});
+        return v;
     }
 
     BOOL update_flat(const T *G, double lr, double alpha, double scale, bool mom) {
@@ -1093,42 +1135,71 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
             hipSetDevice(dev[g]);
             hipMemsetAsync(nets[g]->acc, 0, Net::ACC_BYTES, str[g]);
         }
-        for (int b = 0; b < n_batches && ok; b++) {
-            const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
-            int total = 0;
-            for (int g = 0; g < G && ok; g++) {
-                const int start = b * B + g * Bg;
-                int nv = end - start;
-                nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
-                total += nv;
-                hipSetDevice(dev[g]);
-                const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * Net::xelem;
-                const TT *tb = Td[g] + (size_t)start * n_out;
-                ok = nets[g]->grads(xb, tb, n_out, nv);
-            }
-            if (!ok) break;
-            if (loopback) {
+        if (loopback) {
+            for (int b = 0; b < n_batches && ok; b++) {
+                const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
+                int total = 0;
+                for (int g = 0; g < G && ok; g++) {
+                    const int start = b * B + g * Bg;
+                    int nv = end - start;
+                    nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
+                    total += nv;
+                    const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * Net::xelem;
+                    const TT *tb = Td[g] + (size_t)start * n_out;
+                    ok = nets[g]->grads(xb, tb, n_out, nv);
+                }
+                if (!ok) break;
                 /* virtual replicas share one stream: sum the G buffers into replica 0's */
                 ok = Net::reduce_sum(lb_flat, G, count, str[0]) == 0;
-            } else {
-                /* one grouped launch: the per-device calls of a single-process communicator
-                 * clique must not block each other */
-                int r = hpnn_comm_group_start();
-                for (int g = 0; g < G && r == 0; g++)
-                    r = hpnn_comm_all_reduce(comms[g], nets[g]->gflat, nets[g]->gflat, (long)count, Net::comm_dt,
-                                             HPNN_OP_SUM, str[g]);
-                const int r2 = hpnn_comm_group_end();
-                if (r || r2) {
-                    NN_ERROR(stderr, "gradient all-reduce failed (%d)\n", r ? r : r2);
-                    ok = FALSE;
-                }
+                const double scale = 1.0 / (double)(total > 0 ? total : 1);
+                for (int g = 0; g < G && ok; g++) ok = nets[g]->update_flat(lb_flat, o->lr, o->alpha, scale, mom);
             }
-            const double scale = 1.0 / (double)(total > 0 ? total : 1);
-            for (int g = 0; g < G && ok; g++) {
-                hipSetDevice(dev[g]);
-                ok = nets[g]->update_flat(loopback ? lb_flat : nets[g]->gflat, o->lr, o->alpha, scale,
-                                          mom);
-            }
+        } else {
+            /* one host thread per GPU for the whole epoch (no serial hipSetDevice + launch
+             * loop over the replicas); each layer's bucket goes into an async all-reduce on
+             * the communicator's side stream as soon as it is final (last layer first), so
+             * it overlaps the backward of the layers below; the update waits on a join */
+            std::vector<int> tok(G, 1);
+            std::vector<std::thread> th;
+            for (int g = 0; g < G; g++)
+                th.emplace_back([&, g]() {
+                    if (hipSetDevice(dev[g]) != hipSuccess) {
+                        tok[g] = 0;
+                        return;
+                    }
+                    Net &net = *nets[g];
+                    for (int b = 0; b < n_batches; b++) {
+                        const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
+                        const int start = b * B + g * Bg;
+                        int nv = end - start;
+                        nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
+                        const int total = end - b * B;
+                        const char *xb = (const char *)Xd[g] + (size_t)start * net.Kp[0] * Net::xelem;
+                        const TT *tb = Td[g] + (size_t)start * n_out;
+                        const std::vector<std::pair<int, int>> seq = net.buckets();
+                        size_t issued = 0;
+                        auto ready = [&](int lo, int hi) {
+                            issued++;
+                            return hpnn_comm_all_reduce_async(comms[g], net.gflat + net.goff[lo],
+                                                              (long)(net.goff[hi + 1] - net.goff[lo]), Net::comm_dt,
+                                                              str[g]) == 0;
+                        };
+                        /* after a local failure every remaining bucket is still all-reduced (same
+                         * sizes, same order on every replica), so no peer is left waiting */
+                        int okb = tok[g] && net.grads(xb, tb, n_out, nv, ready) ? 1 : 0;
+                        for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
+                        okb = (hpnn_comm_join(comms[g], str[g]) == 0) && okb;
+                        const double scale = 1.0 / (double)(total > 0 ? total : 1);
+                        okb = okb && net.update_flat(net.gflat, o->lr, o->alpha, scale, mom);
+                        if (!okb && tok[g]) {
+                            NN_ERROR(stderr, "data-parallel step failed on replica %d\n", g);
+                            tok[g] = 0;
+                        }
+                    }
+                    if (hipStreamSynchronize(str[g]) != hipSuccess) tok[g] = 0;
+                });
+            for (auto &t : th) t.join();
+            for (int g = 0; g < G; g++) ok = ok && tok[g];
         }
         if (!ok) break;
         ep_loss = 0.0;
@@ -1256,11 +1327,25 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
             const char *xb = (const char *)Xd + (size_t)start * net.Kp[0] * Net::xelem;
             const TT *tb = Td + (size_t)start * n_out;
-            ok = net.grads(xb, tb, n_out, nv);
-            if (!ok) break;
-            ok = (use_xar ? hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s)
-                          : hpnn_comm_all_reduce(comm, net.gflat, net.gflat, (long)count, Net::comm_dt, HPNN_OP_SUM,
-                                                 s)) == 0;
+            if (use_xar) {
+                /* small gradients: ONE latency-bound xGMI all-reduce of the whole buffer */
+                ok = net.grads(xb, tb, n_out, nv);
+                if (!ok) break;
+                ok = hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s) == 0;
+            } else {
+                /* RCCL: one bucket per layer on the side stream as soon as it is final
+                 * (overlapping the backward of the layers below); the update joins them */
+                const std::vector<std::pair<int, int>> seq = net.buckets();
+                size_t issued = 0;
+                auto ready = [&](int lo, int hi) {
+                    issued++;
+                    return hpnn_comm_all_reduce_async(comm, net.gflat + net.goff[lo],
+                                                      (long)(net.goff[hi + 1] - net.goff[lo]), Net::comm_dt, s) == 0;
+                };
+                ok = net.grads(xb, tb, n_out, nv, ready);
+                for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
+                ok = (hpnn_comm_join(comm, s) == 0) && ok;
+            }
             const int total = end - b * B;
             if (ok) ok = net.update_flat(net.gflat, o->lr, o->alpha, 1.0 / (double)(total > 0 ? total : 1),
                                          mom);
