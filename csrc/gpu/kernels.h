@@ -173,7 +173,7 @@ int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0
                    float *gslab, float *loss_acc, unsigned int *correct, int Bp, int n_valid, int n_out, int type,
                    int grid, hipStream_t stream);
 int hpnn_mlp3_tile_grid(int Bp, int grid);
-/* profiling (HPNN_TILE_TRACE=1): per-workgroup s_memtime stamps [1024][8] */
+/* profiling (HPNN_TILE_TRACE=1): per-workgroup s_memtime stamps [1024][12] */
 int hpnn_mlp3_tile_trace(unsigned long long *out);
 /* ---- FP64 / FP32 batched engine (kernels_fp.hip): f64 selects double, else float ----
  * gemm_fp: C[M x N] (ldc) = sum_k A(m, k) B(n, k) with A(m, k) = A[m*lda + k] (ta = 0) or

@@ -47,19 +47,9 @@ using hpnn::bf16x8;
 using hpnn::f32x4;
 using hpnn::TnTail;
 
-/* 8 unsigned bytes -> bf16x8 of (byte * scale) (exact for pixel values with scale 1) */
-__device__ __forceinline__ bf16x8 u8x8_bf16(uint2 v, float scale) {
-    bf16x8 r;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        r[e] = (__bf16)((float)((v.x >> (8 * e)) & 0xffu) * scale);
-        r[4 + e] = (__bf16)((float)((v.y >> (8 * e)) & 0xffu) * scale);
-    }
-    return r;
-}
-
 /* Dg: [Bt/32][N/16][64][8], Hg: [Bt/32][M/16][64][8]; nbd = N / 16, nbh = M / 16.
- * HU8: Hg holds unsigned bytes (8 per lane per fragment), used as bf16(h * hscale) */
+ * HU8: Hg holds unsigned bytes (8 per lane per fragment), multiplied as exact integers;
+ * hscale scales the FP32 result (G = hscale * D^T H) */
 template <int WF, int WH, int PD, int KW, bool HU8 = false>
 __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                                   const void *__restrict__ Hg, int nbh, float hscale,
@@ -114,7 +104,7 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
 #pragma unroll
         for (int i = 0; i < WF; i++) {
             bf16x8 a;
-            if constexpr (HU8) a = u8x8_bf16(ra[slot_][i], hscale);
+            if constexpr (HU8) a = hpnn::u8x8_int_bf16(ra[slot_][i].x, ra[slot_][i].y);
             else a = ra[slot_][i];
 #pragma unroll
             for (int j = 0; j < WH; j++)
@@ -165,7 +155,8 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
     for (int i = 0; i < WF; i++)
 #pragma unroll
         for (int j = 0; j < WH; j++)
-            *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) = acc[i][j];
+            *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) =
+                HU8 ? acc[i][j] * hscale : acc[i][j];
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false>

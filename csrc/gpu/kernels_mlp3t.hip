@@ -8,7 +8,8 @@
  *
  * Input: the minibatch in FRAGMENT-MAJOR order ([Bp/32][K0/16][64 lanes][8], lane
  * l = 16 g + r of chunk (t, cb) holding X[32 t + 8 g + j][16 cb + r], j < 8; see
- * ops.to_fragment_major), either 8-bit pixels (used as bf16(byte * xscale)) or BF16.
+ * ops.to_fragment_major), either 8-bit pixels (the exact integers in BF16, the pixel scale
+ * xscale applied to the FP32 accumulator: H1 = f(xscale * X W0^T)) or BF16 (xscale 1).
  * It is the SAME buffer the first-layer gradient kernel (kernels_g0.hip,
  * gemm_fm_direct) streams right after this one, so a step reads the batch from HBM
  * once; the second read is served by the 256 MB Infinity Cache.
@@ -70,17 +71,6 @@ constexpr int LDS_TOTAL = OFF_W1 + IMG_W1;
 static_assert(TS * H2 * 2 <= 2 * IMG_XT, "H2 aliases the X^T stages");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
 
-/* 8 unsigned bytes -> bf16x8 of (byte * scale); the same rounding as gemm_fm_direct */
-__device__ __forceinline__ bf16x8 u8x8_to_bf16(unsigned int lo, unsigned int hi, float scale) {
-    bf16x8 r;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        r[e] = (__bf16)((float)((lo >> (8 * e)) & 0xffu) * scale);
-        r[4 + e] = (__bf16)((float)((hi >> (8 * e)) & 0xffu) * scale);
-    }
-    return r;
-}
-
 /* within-wave ordering of LDS writes before other lanes' reads (one wave's LDS
  * instructions execute in order; this keeps the compiler from moving them) */
 __device__ __forceinline__ void wave_lds_fence() {
@@ -91,7 +81,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 /* HPNN_TILE_TRACE=1 (profiling only): s_memtime stamps of every workgroup's wave 0 at the
  * phase boundaries, [block][mark]; read back with hpnn_mlp3_tile_trace */
-constexpr int TR_BLOCKS = 1024, TR_MARKS = 8;
+constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false>
@@ -130,7 +120,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         constexpr int PIECES = (H1 / 32) * (H2 / 16);
         for (int p = wave; p < PIECES; p += 8) glds_t32_piece<H2>((const char *)W1, (size_t)H1 * 2, imgW1, p, lane);
     }
-    __builtin_amdgcn_s_waitcnt(0xF70); /* vmcnt(0): W1 pieces landed (their DMA is inline asm) */
+    /* no wait here: the W1 pieces are this wave's oldest vector-memory ops, so phase A's
+     * first counted wait (for X(0)) covers them, and its barriers publish them */
     mark(1);
 
     f32x4 g1acc[4], g2acc; /* G1: h1 tile = wave, h2 tiles 0..3; G2: h2 tile w&3, o tile w>>2 */
@@ -181,8 +172,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             char *img = lds + OFF_XT + (s & 1) * IMG_XT;
             bf16x8 v[2];
             if constexpr (XU8) {
-                v[0] = u8x8_to_bf16(xr[s][0].x, xr[s][0].y, xscale);
-                v[1] = u8x8_to_bf16(xr[s][0].z, xr[s][0].w, xscale);
+                v[0] = u8x8_int_bf16(xr[s][0].x, xr[s][0].y);
+                v[1] = u8x8_int_bf16(xr[s][0].z, xr[s][0].w);
             } else {
                 v[0] = __builtin_bit_cast(bf16x8, xr[s][0]);
                 v[1] = __builtin_bit_cast(bf16x8, xr[s][1]);
@@ -234,7 +225,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             for (int st = 0; st < 8; st++) {
                 bf16x4 o;
 #pragma unroll
-                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r]);
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
                 *(bf16x4 *)wr_ptr<TS>(imgH1, lo, 128 * sh + 16 * st, 32 * ng + 16 * i) = o;
             }
         lds_barrier();
@@ -281,6 +272,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 *(bf16x4 *)wr_ptr<TS>(imgH2, lo, r0, 16 * ht) = o;
             }
         }
+        mark(5);
         wave_lds_fence();
         /* P2: logits, output activation, loss, delta3 -> D3 image */
 #pragma unroll
@@ -302,6 +294,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                                                   r0, lane, inv_nout, my_loss, my_hit);
             }
         }
+        mark(6);
         wave_lds_fence();
         /* P3: delta2^T [h2][sample] = (W2^T delta3^T) * f'(H2) */
 #pragma unroll
@@ -318,6 +311,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 *(bf16x4 *)wr_ptr<TS>(imgD2, lo, r0, 16 * ht) = o;
             }
         }
+        mark(7);
         wave_lds_fence();
         /* P4: delta1 [sample][h1] = (delta2 W1) * f'(H1) -> HBM, fragment-major:
          * chunk (32-sample row, h1 block) = [g][r][j] = delta1[32 t + 8 g + j][16 hb + r] */
@@ -343,7 +337,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 }
             }
         }
-        mark(5);
+        mark(8);
         lds_barrier();
 
         /* ================= phase C: G1, G2 over the tile's 256 samples ================= */
@@ -360,7 +354,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         }
     }
 
-    mark(6);
+    mark(9);
     /* ---- the block's [G1 (H2 x H1) | G2 (NO x H2)] slab ---- */
     float *slab = gslab + (size_t)blockIdx.x * SLAB;
 #pragma unroll
@@ -389,7 +383,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         if (loss_acc) atomicAdd(loss_acc + HPNN_STAT_SLOT(blockIdx.x), a);
         if (correct) atomicAdd(correct + HPNN_STAT_SLOT(blockIdx.x), h);
     }
-    mark(7);
+    mark(10);
 }
 
 int g_tile_cus = 0;
@@ -482,7 +476,8 @@ extern "C" int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, con
     return -3;
 }
 
-/* HPNN_TILE_TRACE=1 stamps: out[TR_BLOCKS][TR_MARKS] shader-clock ticks */
+/* HPNN_TILE_TRACE=1 stamps: out[TR_BLOCKS][TR_MARKS] shader-clock ticks (wave 0 of each
+ * workgroup; s_memtime counts per XCD, so only intervals within a workgroup compare) */
 extern "C" int hpnn_mlp3_tile_trace(unsigned long long *out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_trace), sizeof(g_tile_trace)) == hipSuccess ? 0 : -5;
 }

@@ -30,6 +30,23 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
+/* 8 unsigned bytes (pixels 0..255) -> the same 8 integers in BF16, exactly: v_cvt_f32_ubyteN
+ * gives the integer as f32, whose low 16 bits are zero (at most 8 significant bits), so
+ * v_perm_b32 packs the high halves of two of them into a bf16x2 -- 1.5 VALU per pixel.
+ * A pixel scale (e.g. 1/255) is applied to the FP32 MFMA accumulator instead. */
+__device__ __forceinline__ unsigned int pk_hi16(float lo, float hi) {
+    return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+__device__ __forceinline__ bf16x8 u8x8_int_bf16(unsigned int a, unsigned int b) {
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    u32x4 r;
+    r[0] = pk_hi16((float)((a >> 0) & 0xffu), (float)((a >> 8) & 0xffu));
+    r[1] = pk_hi16((float)((a >> 16) & 0xffu), (float)((a >> 24) & 0xffu));
+    r[2] = pk_hi16((float)((b >> 0) & 0xffu), (float)((b >> 8) & 0xffu));
+    r[3] = pk_hi16((float)((b >> 16) & 0xffu), (float)((b >> 24) & 0xffu));
+    return __builtin_bit_cast(bf16x8, r);
+}
+
 /* f(x) = 2/(1+e^-x) - 1 with the hardware exp / reciprocal (bf16 outputs) */
 __device__ __forceinline__ float bipolar(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-x)) - 1.0f; }
 __device__ __forceinline__ float dbipolar(float y) { return -0.5f * (y * y - 1.0f); }

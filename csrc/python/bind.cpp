@@ -155,7 +155,7 @@ PYBIND11_MODULE(_native, m) {
     });
     m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
     m.def("mlp3_tile_trace", []() {
-        std::vector<unsigned long long> v(1024 * 8);
+        std::vector<unsigned long long> v(1024 * 12);
         check(hpnn_mlp3_tile_trace(v.data()), "mlp3_tile_trace");
         return v;
     });

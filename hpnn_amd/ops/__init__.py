@@ -121,15 +121,19 @@ def from_fragment_major(Ag, rows, cols):
 def gemm_fm_direct(Dg, Hg, N, M, splits=1, out=None, hscale=1.0):
     """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m] (gemm_tn) with D, H
     given fragment-major (to_fragment_major), direct-to-register loads
-    (csrc/gpu/kernels_g0.hip).  Hg may be uint8 (pixel data): used as bf16(H * hscale)."""
+    (csrc/gpu/kernels_g0.hip).  Hg may be uint8 (pixel data): multiplied as exact integers,
+    the result scaled by hscale."""
     Bt = Dg.numel() // N
     u8 = Hg.dtype == torch.uint8
     if out is None:
         out = torch.empty(splits, N, M, dtype=torch.float32, device=Dg.device)
     if _cpu(Dg):
+        # u8: the exact integers (BF16 holds 0..255 exactly), hscale on the FP32 result
         H = from_fragment_major(Hg, Bt, M)
-        return gemm_tn(from_fragment_major(Dg, Bt, N), (H.float() * hscale).bfloat16() if u8 else H, splits=splits,
-                       out=out)
+        gemm_tn(from_fragment_major(Dg, Bt, N), H.bfloat16() if u8 else H, splits=splits, out=out)
+        if u8:
+            out *= hscale
+        return out
     native().gemm_fm_direct(Dg.data_ptr(), Hg.data_ptr(), int(u8), float(hscale), out.data_ptr(), out.stride(1), N, M,
                             Bt, splits, _stream())
     return out
@@ -261,7 +265,7 @@ def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=
               n_valid=None, loss_acc=None, correct=None, xscale=1.0):
     """The n_in-128-64-(<=32) step up to delta1 with 256-sample tiles
     (csrc/gpu/kernels_mlp3t.hip): Xg fragment-major [Bp/32, K0/16, 64, 8] (to_fragment_major)
-    uint8 (used as bf16(x * xscale)) or bf16 -> delta1 fragment-major into D1g
+    uint8 (exact integers, H1 = f(xscale * X W0^T)) or bf16 -> delta1 fragment-major into D1g
     [Bp/32, 8, 64, 8] bf16, per-block [G1 | G2] slabs into gslab [grid, MLP3_SLAB],
     loss / hits.  W0f: fragment-major BF16 W0 (frag_major); W0 (row-major) is used by the
     CPU emulation only; W2t: W2^T [64, 32] BF16."""
@@ -270,8 +274,7 @@ def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=
     u8 = Xg.dtype == torch.uint8
     if _cpu(Xg):
         X = from_fragment_major(Xg, Bp, K0)
-        Xb = (X.float() * xscale).bfloat16() if u8 else X
-        H1 = bipolar(Xb.float() @ W0.float().t()).bfloat16()
+        H1 = bipolar((X.float() @ W0.float().t()) * xscale).bfloat16()
         D1 = torch.empty(Bp, 128, dtype=torch.bfloat16)
         _cpu_mlp3_mid(H1, W1, None, W2, None, D1, gslab, n_out, net_type, labels, T, t_hi, t_lo, n_valid, loss_acc,
                       correct)

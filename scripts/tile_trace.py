@@ -11,8 +11,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hpnn_amd._lib import native  # noqa: E402
 from hpnn_amd.models import MLP  # noqa: E402
 
-NAMES = ["W1 load", "prologue (X(0), W0 ring)", "phase A (25 k-steps)", "H1 epilogue + barrier",
-         "chain P1-P4", "phase C (G1, G2)", "slab + stats"]
+NAMES = ["W1 DMA issue", "prologue (X(0), W0 ring)", "phase A (25 k-steps)", "H1 epilogue + barrier",
+         "P1 (H2)", "P2 (output, loss, delta3)", "P3 (delta2)", "P4 (delta1 -> HBM) + barrier",
+         "phase C (G1, G2)", "slab + stats"]
 
 
 def main():
@@ -27,16 +28,15 @@ def main():
     m._fused_front(Xs[1], labels=lab, T=None, n_valid=m.Bp)
     torch.cuda.synchronize()
     G = m.midslab.shape[0]
-    t = torch.tensor(native().mlp3_tile_trace(), dtype=torch.float64).view(1024, 8)[:G]
-    start = t[:, 0].min()
-    print(f"workgroups {G}; kernel span {float(t[:, 7].max() - start):.0f} ticks; "
-          f"start skew {float(t[:, 0].max() - start):.0f}")
+    t = torch.tensor(native().mlp3_tile_trace(), dtype=torch.float64).view(1024, 12)[:G]
+    tot = t[:, 10] - t[:, 0]
+    print(f"workgroups {G}; per-workgroup span median {float(tot.median()):.0f} ticks "
+          f"(s_memtime is per XCD: only intervals within a workgroup are compared)")
     for i, n in enumerate(NAMES):
         d = t[:, i + 1] - t[:, i]
         q = torch.quantile(d, torch.tensor([0.1, 0.5, 0.9], dtype=torch.float64))
         print(f"{n:28s} p10 {q[0]:8.0f}  median {q[1]:8.0f}  p90 {q[2]:8.0f} ticks")
-    fin = t[:, 7] - start
-    print(f"end times: min {float(fin.min()):.0f} median {float(fin.median()):.0f} max {float(fin.max()):.0f}")
+
 
 
 if __name__ == "__main__":
