@@ -58,6 +58,17 @@ struct GpuModel {
     long xch_bytes = 0;
     bool device_newer = false; /* device weights not yet copied to host */
     bool host_newer = true;    /* host weights not yet uploaded         */
+    /* online training over several devices (or virtual slots on one device): slot 0 is
+     * this model, slots[s - 1] the others; each slot's W holds valid values only in the rows
+     * its workgroups own (see hpnn_online_args); the exchange buffer and control words are
+     * one fine-grained allocation on slot 0's device that every slot maps */
+    std::vector<GpuModel *> slots;
+    int n_slots = 1, sgrid = 0;
+    bool sloop = false;
+    double *sxch = nullptr;
+    unsigned int *sctl = nullptr;
+    long sxch_bytes = 0;
+    hipStream_t sstream = nullptr;
 };
 
 std::mutex g_mu;
@@ -67,7 +78,12 @@ layer_ann *layer_of(kernel_ann *k, int l) { return l < (int)k->n_hiddens ? &k->h
 
 void free_model(GpuModel *g) {
     if (!g) return;
+    for (GpuModel *s : g->slots) free_model(s);
+    g->slots.clear();
     hipSetDevice(g->dev);
+    if (g->sxch) hipFree(g->sxch);
+    if (g->sctl) hipFree(g->sctl);
+    if (g->sstream) hipStreamDestroy(g->sstream);
     for (int l = 0; l < 16; l++) {
         if (g->W[l]) hpnn_dev_free(g->W[l]);
         if (g->dW[l]) hpnn_dev_free(g->dW[l]);
@@ -89,9 +105,14 @@ void destroy_hook(kernel_ann *k) {
     g_models.erase(k);
 }
 
-BOOL ensure_model(kernel_ann *k, UINT gpu) {
+void gather_host(kernel_ann *k);
+
+/* keep_slots: the caller trains on the slots; otherwise slot 0's partial rows are made
+ * whole first (the single-device paths read every row of W) */
+BOOL ensure_model(kernel_ann *k, UINT gpu, bool keep_slots = false) {
     hpnn_gpu_model_destroy_hook = destroy_hook;
     GpuModel *g = (GpuModel *)k->gpu;
+    if (g && !keep_slots && g->n_slots > 1 && g->device_newer) gather_host(k);
     const int L = (int)k->n_hiddens + 1;
     if (L > 16) {
         NN_ERROR(stderr, "GPU engine supports at most 15 hidden layers\n");
@@ -118,7 +139,7 @@ BOOL ensure_model(kernel_ann *k, UINT gpu) {
         g_models.insert(k);
     }
     HIPCHK(hipSetDevice(g->dev));
-    if (g->host_newer) {
+    if (g->host_newer && !(keep_slots && g->device_newer)) {
         for (int l = 0; l < L; l++) {
             layer_ann *ly = layer_of(k, l);
             HIPCHK(hipMemcpy(g->W[l], ly->weights, sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs,
@@ -167,15 +188,8 @@ void hpnn_rt_release_device_state(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     for (kernel_ann *k : g_models) {
         GpuModel *g = (GpuModel *)k->gpu;
-        if (g && g->device_newer) {
-            /* keep the host master current before the device goes away */
-            hipSetDevice(g->dev);
-            for (int l = 0; l < g->L; l++) {
-                layer_ann *ly = layer_of(k, l);
-                hipMemcpy(ly->weights, g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs,
-                          hipMemcpyDeviceToHost);
-            }
-        }
+        /* keep the host master current before the device goes away */
+        if (g && g->device_newer) gather_host(k);
         free_model(g);
         k->gpu = nullptr;
     }
@@ -184,17 +198,41 @@ void hpnn_rt_release_device_state(void) {
 
 extern "C" BOOL hpnn_gpu_online_prepare(kernel_ann *k, UINT gpu) { return ensure_model(k, gpu); }
 
-extern "C" void hpnn_gpu_sync_host(kernel_ann *k) {
-    if (!k || !k->gpu) return;
+namespace {
+void gather_host(kernel_ann *k) {
     GpuModel *g = (GpuModel *)k->gpu;
-    if (!g->device_newer) return;
     hipSetDevice(g->dev);
     hipStreamSynchronize(hpnn_rt_stream(0, 0));
     for (int l = 0; l < g->L; l++) {
         layer_ann *ly = layer_of(k, l);
         hipMemcpy(ly->weights, g->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs, hipMemcpyDeviceToHost);
     }
+    if (g->n_slots > 1) {
+        /* every row from the slot whose workgroups own it: row j -> workgroup j % total */
+        const int total = g->n_slots * g->sgrid;
+        for (int s = 1; s < g->n_slots; s++) {
+            GpuModel *m = g->slots[s - 1];
+            hipSetDevice(m->dev);
+            for (int l = 0; l < g->L; l++) {
+                layer_ann *ly = layer_of(k, l);
+                const size_t M = ly->n_inputs;
+                std::vector<double> tmp((size_t)ly->n_neurons * M);
+                hipMemcpy(tmp.data(), m->W[l], sizeof(double) * tmp.size(), hipMemcpyDeviceToHost);
+                for (UINT j = 0; j < ly->n_neurons; j++)
+                    if ((int)(j % total) / g->sgrid == s) memcpy(ly->weights + j * M, tmp.data() + j * M, 8 * M);
+            }
+        }
+        hipSetDevice(g->dev);
+        /* the single-device paths read slot 0's W: it must be whole again */
+        g->host_newer = true;
+    }
     g->device_newer = false;
+}
+}  // namespace
+
+extern "C" void hpnn_gpu_sync_host(kernel_ann *k) {
+    if (!k || !k->gpu || !((GpuModel *)k->gpu)->device_newer) return;
+    gather_host(k);
 }
 
 extern "C" void hpnn_gpu_mark_host_dirty(kernel_ann *k) {
@@ -202,9 +240,183 @@ extern "C" void hpnn_gpu_mark_host_dirty(kernel_ann *k) {
     ((GpuModel *)k->gpu)->host_newer = true;
 }
 
+namespace {
+
+/* slot models for online training over S devices (or S virtual slots on device 0) */
+BOOL ensure_slots(kernel_ann *k, int S, bool loopback) {
+    GpuModel *g = (GpuModel *)k->gpu;
+    if (g->n_slots == S && g->sloop == loopback) return TRUE;
+    for (GpuModel *m : g->slots) free_model(m);
+    g->slots.clear();
+    g->n_slots = 1;
+    g->sgrid = 0;
+    if (S <= 1) return TRUE;
+    for (int s = 1; s < S; s++) {
+        GpuModel *m = new GpuModel();
+        m->dev = loopback ? g->dev : hpnn_rt_device((UINT)s);
+        m->L = g->L;
+        g->slots.push_back(m);
+        HIPCHK(hipSetDevice(m->dev));
+        for (int l = 0; l < g->L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            HIPCHK(hpnn_dev_malloc(&m->W[l], sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs));
+        }
+        HIPCHK(hpnn_dev_malloc(&m->x, sizeof(double) * k->n_inputs));
+        HIPCHK(hpnn_dev_malloc(&m->t, sizeof(double) * k->n_outputs));
+        HIPCHK(hpnn_dev_malloc(&m->out, sizeof(double) * k->n_outputs));
+        HIPCHK(hpnn_dev_malloc(&m->result, sizeof(double) * 8));
+        HIPCHK(hpnn_dev_malloc(&m->scratch, sizeof(double) * 8));
+        HIPCHK(hipStreamCreateWithFlags(&m->sstream, hipStreamNonBlocking));
+    }
+    HIPCHK(hipSetDevice(g->dev));
+    if (!g->sstream) HIPCHK(hipStreamCreateWithFlags(&g->sstream, hipStreamNonBlocking));
+    g->n_slots = S;
+    g->sgrid = 0;
+    g->sloop = loopback;
+    g->host_newer = true; /* every slot takes the host weights */
+    return TRUE;
+}
+
+BOOL upload_slots(kernel_ann *k) {
+    GpuModel *g = (GpuModel *)k->gpu;
+    for (GpuModel *m : g->slots) {
+        HIPCHK(hipSetDevice(m->dev));
+        for (int l = 0; l < g->L; l++) {
+            layer_ann *ly = layer_of(k, l);
+            HIPCHK(hipMemcpy(m->W[l], ly->weights, sizeof(double) * (size_t)ly->n_neurons * ly->n_inputs,
+                             hipMemcpyHostToDevice));
+        }
+    }
+    HIPCHK(hipSetDevice(g->dev));
+    return TRUE;
+}
+
+/* One sample of the reference's online training on a cooperative grid spanning S slots
+ * (the reference shards every layer's rows over n_gpu x n_streams, cuda_ann.cu:533-1275,
+ * with hub copies and a device sync per layer; here one persistent kernel per device
+ * exchanges the layer outputs and delta partials through fine-grained memory inside the
+ * convergence loop).  Returns FALSE when the net does not suit the cooperative kernel. */
+BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBLE *in, const DOUBLE *out, DOUBLE lr,
+                        DOUBLE alpha, DOUBLE delta, double res[5], bool *timed_out) {
+    GpuModel *g = (GpuModel *)k->gpu;
+    const int S = g->n_slots;
+    const bool mom = train == NN_TRAIN_BPM;
+    hpnn_online_args a0;
+    fill_args(k, g, type, &a0);
+    const int grid = hpnn_online_coop_grid_slots(&a0, S, g->sloop ? 128 / S : 128);
+    if (grid <= 0) return FALSE;
+    const int total = grid * S;
+    g->sgrid = grid; /* fixed for a net and S: the row ownership gather_host relies on */
+    const long need = hpnn_online_coop_xch_bytes(&a0, total);
+    HIPCHK(hipSetDevice(g->dev));
+    if (need > g->sxch_bytes) {
+        if (g->sxch) HIPCHK(hipFree(g->sxch));
+        g->sxch = nullptr;
+        HIPCHK(hipExtMallocWithFlags((void **)&g->sxch, (size_t)need, hipDeviceMallocUncached));
+        g->sxch_bytes = need;
+    }
+    if (!g->sctl) HIPCHK(hipExtMallocWithFlags((void **)&g->sctl, HPNN_ONLINE_CTL_BYTES, hipDeviceMallocUncached));
+    HIPCHK(hipMemset(g->sctl, 0, HPNN_ONLINE_CTL_BYTES));
+    if (mom && !ensure_momentum(k)) return FALSE;
+    for (int s = 0; s < S; s++) {
+        GpuModel *m = s ? g->slots[s - 1] : g;
+        HIPCHK(hipSetDevice(m->dev));
+        if (mom)
+            for (int l = 0; l < g->L; l++) {
+                layer_ann *ly = layer_of(k, l);
+                const size_t nw = (size_t)ly->n_neurons * ly->n_inputs;
+                if (!m->dW[l]) HIPCHK(hpnn_dev_malloc(&m->dW[l], sizeof(double) * nw));
+                HIPCHK(hipMemsetAsync(m->dW[l], 0, sizeof(double) * nw, m->sstream));
+            }
+        HIPCHK(hipMemcpyAsync(m->x, in, sizeof(double) * k->n_inputs, hipMemcpyHostToDevice, m->sstream));
+        HIPCHK(hipMemcpyAsync(m->t, out, sizeof(double) * k->n_outputs, hipMemcpyHostToDevice, m->sstream));
+    }
+    /* every slot's copies are in place before any slot starts spinning on the others */
+    for (int s = 0; s < S; s++) {
+        GpuModel *m = s ? g->slots[s - 1] : g;
+        HIPCHK(hipSetDevice(m->dev));
+        HIPCHK(hipStreamSynchronize(m->sstream));
+    }
+    for (int s = 0; s < S; s++) {
+        GpuModel *m = s ? g->slots[s - 1] : g;
+        HIPCHK(hipSetDevice(m->dev));
+        hpnn_online_args a;
+        fill_args(k, m, type, &a);
+        a.momentum = mom;
+        a.lr = lr;
+        a.alpha = alpha;
+        a.delta = delta > 0 ? delta : (mom ? DELTA_BPM : DELTA_BP);
+        a.min_iter = mom ? MIN_BPM_ITER : MIN_BP_ITER;
+        a.max_iter = mom ? MAX_BPM_ITER : MAX_BP_ITER;
+        a.forward_only = 0;
+        a.xch = g->sxch;
+        a.ctl = g->sctl;
+        a.dev_slot = s;
+        a.n_slots = S;
+        if (hpnn_online_coop_launch(&a, grid, m->sstream) != 0) {
+            NN_ERROR(stderr, "online kernel launch failed on slot %d\n", s);
+            return FALSE;
+        }
+    }
+    for (int s = S - 1; s >= 0; s--) {
+        GpuModel *m = s ? g->slots[s - 1] : g;
+        HIPCHK(hipSetDevice(m->dev));
+        HIPCHK(hipStreamSynchronize(m->sstream));
+    }
+    HIPCHK(hipSetDevice(g->dev));
+    HIPCHK(hipMemcpy(res, g->result, sizeof(double) * 5, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(k->output.vec, g->out, sizeof(double) * k->n_outputs, hipMemcpyDeviceToHost));
+    unsigned int err = 0;
+    HIPCHK(hipMemcpy(&err, (const char *)g->sctl + 128 * sizeof(unsigned int), sizeof err, hipMemcpyDeviceToHost));
+    *timed_out = err != 0;
+    return TRUE;
+}
+
+/* online slots: HPNN_ONLINE_SLOTS=S runs S virtual slots on device 0 (tests of the
+ * device-spanning protocol on one GPU); else the runtime's GPU count (train_nn -G N) */
+int online_slots(bool *loopback) {
+    const char *e = getenv("HPNN_ONLINE_SLOTS");
+    const int v = e ? atoi(e) : 0;
+    *loopback = v > 1;
+    if (v > 1) return v;
+    const nn_runtime *rt = hpnn_rt_get();
+    return rt && rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
+}
+
+}  // namespace
+
 extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train train, const DOUBLE *in,
                                         const DOUBLE *out, DOUBLE lr, DOUBLE alpha, DOUBLE delta, UINT *n_iter,
                                         BOOL *ok, DOUBLE *init_err, BOOL *first_ok) {
+    {
+        bool loop = false;
+        const int S = online_slots(&loop);
+        if (S > 1) {
+            if (!k->gpu && !ensure_model(k, 0, true)) return 0.0;
+            GpuModel *g = (GpuModel *)k->gpu;
+            /* a different slot layout: the host takes the current rows first */
+            if (g->device_newer && (g->n_slots != S || g->sloop != loop)) gather_host(k);
+            if (!ensure_slots(k, S, loop)) return 0.0;
+            if (g->host_newer && !(ensure_model(k, 0, true) && upload_slots(k))) return 0.0;
+            double res[5] = {0, 0, 0, 0, 0};
+            bool to = false;
+            if (train_sample_slots(k, type, train, in, out, lr, alpha, delta, res, &to)) {
+                g->device_newer = true;
+                if (to) {
+                    NN_ERROR(stderr, "device-spanning online kernel: a grid barrier timed out\n");
+                    if (ok) *ok = FALSE;
+                    return 0.0;
+                }
+                if (n_iter) *n_iter = (UINT)res[2];
+                if (ok) *ok = res[3] != 0.0;
+                if (init_err) *init_err = res[1];
+                if (first_ok) *first_ok = res[4] != 0.0;
+                return res[0];
+            }
+            /* the net does not suit the cooperative kernel: one device */
+            ensure_slots(k, 1, false);
+        }
+    }
     if (!ensure_model(k, 0)) return 0.0;
     GpuModel *g = (GpuModel *)k->gpu;
     hipStream_t s = hpnn_rt_stream(0, 0);

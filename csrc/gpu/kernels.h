@@ -232,6 +232,15 @@ typedef struct {
      * (hpnn_online_coop_xch_bytes) and the control words (HPNN_ONLINE_CTL_BYTES) */
     double *xch;
     unsigned int *ctl;
+    /* device-spanning cooperative grid (online training over several GPUs, the reference's
+     * row sharding of cuda_ann.cu:533-1275 over n_gpu x n_streams): this launch is slot
+     * `dev_slot` of `n_slots` launches of `grid` workgroups each (one per GPU, or several
+     * virtual slots on one GPU); workgroup g = dev_slot * grid + blockIdx.x of
+     * n_slots * grid owns rows j == g (mod n_slots * grid) of every layer, and only those
+     * rows of its slot's W / dW are read or written.  xch / ctl are ONE allocation that
+     * every slot's device maps (fine-grained), accessed at system scope.  n_slots <= 1:
+     * the single-device kernel. */
+    int dev_slot, n_slots;
 } hpnn_online_args;
 
 #define HPNN_ONLINE_CTL_BYTES 1024
@@ -242,6 +251,9 @@ long hpnn_online_coop_xch_bytes(const hpnn_online_args *a, int grid);
  * workgroups, vectors and delta partials are exchanged through write-through stores and
  * a counter barrier; returns 0, or < 0 (launch error) */
 int hpnn_online_coop_launch(const hpnn_online_args *a, int grid, hipStream_t stream);
+/* device-spanning form: workgroups per slot for n_slots slots (0: not applicable);
+ * per_device_cap bounds one device's share of resident workgroups */
+int hpnn_online_coop_grid_slots(const hpnn_online_args *a, int n_slots, int per_device_cap);
 /* 0, or -1 when a barrier of the last cooperative launch timed out (ctl read back) */
 int hpnn_online_coop_status(const hpnn_online_args *a);
 

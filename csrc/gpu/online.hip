@@ -382,11 +382,18 @@ constexpr unsigned long long COOP_TIMEOUT = 2000000000ULL; /* wall-clock ticks (
 typedef __attribute__((address_space(1))) double gdbl;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
+/* SYS: the grid spans several devices (exchange buffer and counters in fine-grained memory
+ * every device maps): system-scope accesses, i.e. write-through to memory and reads that
+ * bypass every cache on the way */
+template <bool SYS>
 __device__ __forceinline__ void xpub(double *p, size_t i, double v) {
-    __hip_atomic_store((gdbl *)p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (SYS) __hip_atomic_store((gdbl *)p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store((gdbl *)p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+template <bool SYS>
 __device__ __forceinline__ double xget(const double *p, size_t i) {
-    return __hip_atomic_load((const gdbl *)p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (SYS) return __hip_atomic_load((const gdbl *)p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else return __hip_atomic_load((const gdbl *)p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* counter barrier: every wave drains its write-through stores, one lane adds, one lane
@@ -395,23 +402,23 @@ __device__ __forceinline__ double xget(const double *p, size_t i) {
  * not serialize on one address; the poller sums the 8.  Counters are never reset inside a
  * launch (zeroed by the launcher's memset); the timeout word is ctl[COOP_ERR]. */
 constexpr int COOP_SUB = 8, COOP_LINE = 16, COOP_ERR = COOP_SUB * COOP_LINE;
-__device__ __forceinline__ void coop_barrier(unsigned int *ctl, unsigned int target) {
+template <bool SYS>
+__device__ __forceinline__ void coop_barrier(unsigned int *ctl, unsigned int target, int g) {
+    constexpr int SC = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         gu32 *c = (gu32 *)ctl;
-        __hip_atomic_fetch_add(c + (blockIdx.x % COOP_SUB) * COOP_LINE, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(c + (g % COOP_SUB) * COOP_LINE, 1u, __ATOMIC_RELAXED, SC);
         const unsigned long long t0 = wall_clock64();
         for (;;) {
             unsigned int sum = 0;
 #pragma unroll
-            for (int k = 0; k < COOP_SUB; k++)
-                sum += __hip_atomic_load(c + k * COOP_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 0; k < COOP_SUB; k++) sum += __hip_atomic_load(c + k * COOP_LINE, __ATOMIC_RELAXED, SC);
             if (sum >= target) break;
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > COOP_TIMEOUT) {
-                __hip_atomic_store(c + COOP_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(c + COOP_ERR, 1u, __ATOMIC_RELAXED, SC);
                 break;
             }
         }
@@ -524,11 +531,13 @@ __host__ __device__ inline CoopLayout coop_layout(const hpnn_online_args &a, int
     return c;
 }
 
+template <bool SYS>
 __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
     extern __shared__ __attribute__((aligned(16))) double cs[];
     __shared__ double red[CNW], sval[CNW];
     __shared__ int sidx[2 * CNW];
-    const int G = gridDim.x, g = blockIdx.x;
+    const int slots = a.n_slots > 1 ? a.n_slots : 1;
+    const int G = (int)gridDim.x * slots, g = (slots > 1 ? a.dev_slot : 0) * (int)gridDim.x + (int)blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int L = a.L, n_out = a.N[L - 1];
     const CoopLayout X = coop_layout(a, G);
@@ -566,10 +575,10 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
                 double s = 0.0;
                 for (int i = lane; i < M; i += 64) s += gld(w, i) * in[i];
                 s = wave_sum(s);
-                if (lane == 0) xpub(a.xch, X.hv[gen][l] + j, use_act ? act(s) : s);
+                if (lane == 0) xpub<SYS>(a.xch, X.hv[gen][l] + j, use_act ? act(s) : s);
             }
-            coop_barrier(a.ctl, (++phase) * G);
-            for (int i = threadIdx.x; i < N; i += CNT) h[gen][l][i] = xget(a.xch, X.hv[gen][l] + i);
+            coop_barrier<SYS>(a.ctl, (++phase) * G, g);
+            for (int i = threadIdx.x; i < N; i += CNT) h[gen][l][i] = xget<SYS>(a.xch, X.hv[gen][l] + i);
             __syncthreads();
         }
         if (a.type == 2) c_softmax(h[gen][L - 1], n_out, red);
@@ -604,16 +613,16 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
                     for (int m = threadIdx.x; m < M; m += CNT) {
                         double s = 0.0;
                         for (int j = g; j < N; j += G) s += gld(a.W[l], (size_t)j * M + m) * d[l][j];
-                        xpub(a.xch, X.part[l] + (long)g * M + m, s);
+                        xpub<SYS>(a.xch, X.part[l] + (long)g * M + m, s);
                     }
                 }
-                coop_barrier(a.ctl, (++phase) * G);
+                coop_barrier<SYS>(a.ctl, (++phase) * G, g);
                 /* own rows m of layer l-1: sum the partials in workgroup order */
                 const int Gp = G < N ? G : N;
                 for (int r = wave; g + (long)G * r < M; r += CNW) {
                     const int m = g + G * r;
                     double s = 0.0;
-                    for (int q = lane; q < Gp; q += 64) s += xget(a.xch, X.part[l] + (long)q * M + m);
+                    for (int q = lane; q < Gp; q += 64) s += xget<SYS>(a.xch, X.part[l] + (long)q * M + m);
                     s = wave_sum(s);
                     if (lane == 0) d[l - 1][m] = s * dact(h[cur][l - 1][m]);
                 }
@@ -649,10 +658,10 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
                     }
                 }
                 s = wave_sum(s);
-                if (lane == 0) xpub(a.xch, X.hv[nxt][l] + j, use_act ? act(s) : s);
+                if (lane == 0) xpub<SYS>(a.xch, X.hv[nxt][l] + j, use_act ? act(s) : s);
             }
-            coop_barrier(a.ctl, (++phase) * G);
-            for (int i = threadIdx.x; i < N; i += CNT) h[nxt][l][i] = xget(a.xch, X.hv[nxt][l] + i);
+            coop_barrier<SYS>(a.ctl, (++phase) * G, g);
+            for (int i = threadIdx.x; i < N; i += CNT) h[nxt][l][i] = xget<SYS>(a.xch, X.hv[nxt][l] + i);
             __syncthreads();
         }
         if (a.type == 2) c_softmax(h[nxt][L - 1], n_out, red);
@@ -674,7 +683,9 @@ __global__ __launch_bounds__(CNT) void online_coop_kernel(hpnn_online_args a) {
         is_ok = ok;
         /* every workgroup holds the same values: the same decision everywhere; a timed-out
          * barrier (ctl[1]) ends the loop on every workgroup that sees it */
-        if (__hip_atomic_load((gu32 *)a.ctl + COOP_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) stop = 1;
+        if (__hip_atomic_load((gu32 *)a.ctl + COOP_ERR, __ATOMIC_RELAXED,
+                              SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT))
+            stop = 1;
         if (stop) break;
     }
     if (g == 0) {
@@ -707,20 +718,42 @@ extern "C" int hpnn_online_coop_grid(const hpnn_online_args *a) {
     return G >= 8 ? G : 0;
 }
 
+extern "C" int hpnn_online_coop_grid_slots(const hpnn_online_args *a, int n_slots, int per_device_cap) {
+    if (n_slots <= 1) return hpnn_online_coop_grid(a);
+    if (a->L < 1 || a->L > 16) return 0;
+    int maxn = 0;
+    long lds = a->n_in + a->N[a->L - 1];
+    for (int l = 0; l < a->L; l++) {
+        maxn = a->N[l] > maxn ? a->N[l] : maxn;
+        lds += 3L * a->N[l];
+    }
+    if (lds * 8 > 150 * 1024) return 0;
+    /* one row per wave per pass over all slots' workgroups */
+    int g = (maxn + CNW * n_slots - 1) / (CNW * n_slots);
+    const int cap = per_device_cap < COOP_MAX_GRID ? per_device_cap : COOP_MAX_GRID;
+    if (g > cap) g = cap;
+    return g >= 1 ? g : 0;
+}
+
+/* grid: the TOTAL number of workgroups (n_slots x per-slot grid) */
 extern "C" long hpnn_online_coop_xch_bytes(const hpnn_online_args *a, int grid) {
     return coop_layout(*a, grid).total * (long)sizeof(double);
 }
 
+/* n_slots > 1: the caller zeroes ctl once, before any slot is launched */
 extern "C" int hpnn_online_coop_launch(const hpnn_online_args *a, int grid, hipStream_t stream) {
     if (grid < 1 || grid > COOP_MAX_GRID || !a->xch || !a->ctl) return -1;
     long lds = a->n_in + a->N[a->L - 1];
     for (int l = 0; l < a->L; l++) lds += 3L * a->N[l];
     const unsigned bytes = (unsigned)(lds * 8);
-    if (bytes > 48 * 1024)
-        (void)hipFuncSetAttribute((const void *)online_coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)bytes);
-    if (hipMemsetAsync(a->ctl, 0, HPNN_ONLINE_CTL_BYTES, stream) != hipSuccess) return -5;
-    hipLaunchKernelGGL(online_coop_kernel, dim3(grid), dim3(CNT), bytes, stream, *a);
+    const bool sys = a->n_slots > 1;
+    const void *fn = sys ? (const void *)online_coop_kernel<true> : (const void *)online_coop_kernel<false>;
+    if (bytes > 48 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (!sys && hipMemsetAsync(a->ctl, 0, HPNN_ONLINE_CTL_BYTES, stream) != hipSuccess) return -5;
+    if (sys)
+        hipLaunchKernelGGL(online_coop_kernel<true>, dim3(grid), dim3(CNT), bytes, stream, *a);
+    else
+        hipLaunchKernelGGL(online_coop_kernel<false>, dim3(grid), dim3(CNT), bytes, stream, *a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

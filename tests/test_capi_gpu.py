@@ -158,3 +158,28 @@ def test_batched_gpu_tn_update_matches_separate(tmp_path):
         assert np.linalg.norm(ds) > 0
         rel = np.linalg.norm(df - ds) / np.linalg.norm(ds)
         assert rel < 1e-3, rel
+
+
+@pytest.mark.parametrize("net,train,dims,slots", [("SNN", "BPM", (120, [64, 40], 10), 2),
+                                                  ("ANN", "BPM", (70, [48, 200, 33], 7), 3),
+                                                  ("SNN", "BP", (300, [700], 40), 2)])
+def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots):
+    """The online engine with its cooperative grid spread over several slots (one per GPU
+    with train_nn -G N; here HPNN_ONLINE_SLOTS virtual slots on the box's one GPU, each its
+    own launch on its own stream with its own copy of W, exchanging through fine-grained
+    memory at system scope) == the one-device engine and the FP64 CPU engine to 1e-9.
+    Every slot owns the rows j with (j mod total workgroups) in its range; the host gathers
+    each row from its owner when the kernel is dumped."""
+    n_in, hid, n_out = dims
+    runs = {"cpu": (True, None), "one": (False, None), "slots": (False, {"HPNN_ONLINE_SLOTS": str(slots)})}
+    for tag, (cpu, env) in runs.items():
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 3, n_in, n_out, net == "SNN", seed=7)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=9, inputs=n_in, hiddens=hid,
+                           outputs=n_out, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, cpu=cpu, extra_env=env)
+        assert out.count("TRAINING FILE") == 3
+    ks = {t: formats.read_kernel(str(tmp_path / t / "kernel.opt"))["weights"] for t in runs}
+    for a, b, c in zip(ks["cpu"], ks["one"], ks["slots"]):
+        assert np.abs(c - b).max() < 1e-9, np.abs(c - b).max()
+        assert np.abs(c - a).max() < 1e-9, np.abs(c - a).max()
