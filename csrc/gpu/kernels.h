@@ -175,6 +175,29 @@ int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0
 int hpnn_mlp3_tile_grid(int Bp, int grid);
 /* profiling (HPNN_TILE_TRACE=1): per-workgroup s_memtime stamps [1024][12] */
 int hpnn_mlp3_tile_trace(unsigned long long *out);
+/* ---- wide-input one-hidden-layer front (kernels_wide.hip): K0 (4096) -> 256 -> 256 ----
+ * X [Bp][ldx] bf16 row-major, W0 [256][K0], W1 / W1t [256][256] bf16; outputs H0, D2 (delta
+ * of the output layer), D1 (delta of the hidden layer), all [Bp][256] bf16 row-major; labels
+ * or T [Bp][ldt]; with 2 workgroups per 128-sample tile (hpnn_wide2_ksplit) pbuf
+ * (hpnn_wide2_pbuf_bytes), cnt / flag (Bp / 128 words each, zero once, self-resetting) and
+ * err (one word, set on a hand-over timeout) are required. */
+typedef struct {
+    const void *X, *W0, *W1, *W1t;
+    int ldx, K0;
+    const int *labels;
+    const float *T;
+    int ldt;
+    float t_hi, t_lo;
+    void *H0, *D2, *D1, *pbuf;
+    unsigned int *cnt, *flag, *err;
+    float *loss_acc;
+    unsigned int *correct;
+    int Bp, n_valid, n_out, type;
+    int ksplit; /* workgroups per tile: 1, 2, or 0 = hpnn_wide2_ksplit */
+} hpnn_wide2_args;
+int hpnn_wide2_front(const hpnn_wide2_args *a, hipStream_t stream);
+int hpnn_wide2_ksplit(int Bp, int K0);
+long hpnn_wide2_pbuf_bytes(int Bp);
 /* ---- FP64 / FP32 batched engine (kernels_fp.hip): f64 selects double, else float ----
  * gemm_fp: C[M x N] (ldc) = sum_k A(m, k) B(n, k) with A(m, k) = A[m*lda + k] (ta = 0) or
  * A[k*lda + m] (ta = 1), B(n, k) = B[n*ldb + k] (tb = 0) or B[k*ldb + n] (tb = 1), on the FP64 /

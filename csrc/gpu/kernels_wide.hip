@@ -1,0 +1,525 @@
+/*
+ * wide2_front: the training step of a wide-input one-hidden-layer net, K0 -> 256 -> 256
+ * (padded; the RRUFF XRD shape 4096-230-230 of BASELINE.json), up to the deltas, in one
+ * launch (gfx950).
+ *
+ * Reference: the per-sample GEMV chain of snn_kernel_train / ann_kernel_train
+ * (snn.c:280-335, 481-794; ann.c:883-888, 1279-1592; cuda_snn.cu:156-976 softmax,
+ * 2726-3717 train_momentum), batched.  Replaces the per-layer sequence gemm_nt (layer 0)
+ * -> gemm_nt (layer 1) -> output_delta -> gemm_nt (delta back-propagation) of the
+ * generic path: four launches and three HBM round trips of [Bp, 256] activations.
+ *
+ * Work split.  A 128-sample tile is computed by KSPLIT workgroups (8 waves each), each
+ * over one K0 / KSPLIT slice of the input features, so that a 16384-sample batch gives
+ * 256 workgroups (one per CU) while every workgroup still holds the whole hidden row of
+ * its tile (the output layer needs it):
+ *
+ *  A  acc[256 x 128] = W0[:, slice] X[tile, slice]^T.  Wave w owns neurons 32w..32w+31
+ *     for all 128 samples (16 MFMA 16x16x32 per 32 features, 64 accumulator registers):
+ *     each W0 element is read once per workgroup, straight from the L2 into registers
+ *     (the XCD's workgroups share a K slice: tile = block / 2, slice = block % 2, and
+ *     blocks b, b + 8 share an XCD).  The X slice streams through a 4-stage LDS ring by
+ *     LDS-DMA (8 rows x 128 B per instruction: whole cache lines), 16 KiB per 64 features,
+ *     read back conflict-free with ds_read_b128.  One barrier per stage.
+ *  X  KSPLIT = 2: the first of the two workgroups of a tile to finish (a self-resetting
+ *     atomicInc per tile) hands its FP32 partial over through memory with write-through
+ *     (sc1) stores and an sc1 flag, and exits; the second adds it (a + b == b + a: the
+ *     result does not depend on which finished first) and runs the chain.  The second
+ *     only waits for a workgroup that is already past its last dependency, so nothing
+ *     relies on co-residency.  (MI355X_MICROARCH.md, "Valid forms", first sc1 row.)
+ *  B  chain, 8 waves on the tile, images in LDS (T32 layout of mfma_common.h):
+ *     H0 = f(acc) -> LDS (and HBM, for the layer-1 weight gradient);
+ *     Z = H0 W1^T, wave w owning outputs 32w..; softmax / sigmoid / linear with the
+ *     per-sample max and denominator combined across the 8 waves through LDS; loss,
+ *     argmax hits, delta2 -> LDS (and HBM);
+ *     delta1 = (delta2 W1) f'(H0), wave w owning hidden units 32w.., written over H0 in
+ *     place -> HBM.
+ *     HBM copies leave through coalesced 16-byte row stores from the LDS images.
+ *
+ * Outputs are row-major [Bp][256] BF16 (the buffers of the per-layer path, so the weight
+ * gradients and updates that follow are unchanged): H0, delta2, delta1; loss / hits into
+ * the HPNN_STAT_SLOT slots.
+ *
+ * LDS: phase A ring 4 x 16 KiB (aliased by the chain) | chain: H0 / delta1 image 64 KiB,
+ * delta2 image 64 KiB, cross-wave reduction words 20 KiB.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "kernels.h"
+#include "mfma_common.h"
+#include "mlp3_common.h"
+
+using namespace hpnn;
+using namespace hpnn::mlp3;
+
+namespace {
+
+constexpr int TS = 128;                /* samples per tile */
+constexpr int HW = 256;                /* hidden / output width (padded) */
+constexpr int STG = TS * 64 * 2;       /* one 64-feature stage of X: 16 KiB */
+constexpr int P = 4, DIST = P - 1;     /* ring stages, stages issued ahead */
+constexpr int IMG = TS * HW * 2;       /* [128][256] bf16 image: 64 KiB */
+constexpr int OFF_H = 0, OFF_D2 = IMG, OFF_RED = 2 * IMG;
+constexpr int RED_W = 8 * TS;          /* floats per reduction array ([wave][sample]) */
+constexpr int LDS_TOTAL = OFF_RED + 5 * RED_W * 4 + 16;
+static_assert(P * STG <= OFF_RED, "ring aliases the chain images");
+static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
+constexpr unsigned long long XCH_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
+
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+/* 16-byte write-through store / L1-bypassing load (global_*_dwordx4 ... sc1); the loads
+ * are issued in a batch and drained by the caller's s_waitcnt vmcnt(0) */
+__device__ __forceinline__ void st_sc1(void *p, const f32x4 &v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_sc1(const void *p) {
+    f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+template <int TYPE, bool LABELS, int NS, int KSPLIT>
+__global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X, int ldx,
+                                                    const __bf16 *__restrict__ W0, int K0,
+                                                    const __bf16 *__restrict__ W1,
+                                                    const __bf16 *__restrict__ W1t,
+                                                    const int *__restrict__ labels, const float *__restrict__ T,
+                                                    int ldt, float t_hi, float t_lo, __bf16 *__restrict__ H0out,
+                                                    __bf16 *__restrict__ D2out, __bf16 *__restrict__ D1out,
+                                                    f32x4 *__restrict__ pbuf, unsigned int *cnt,
+                                                    unsigned int *flag, unsigned int *err,
+                                                    float *__restrict__ loss_acc, unsigned int *__restrict__ correct,
+                                                    int n_valid, int n_out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const LaneOff lo = lane_offsets(lane);
+    const int b = blockIdx.x;
+    const int tile = KSPLIT == 2 ? (b >> 1) : b, half = KSPLIT == 2 ? (b & 1) : 0;
+    const int kbeg = half * NS * 64;
+    const size_t row0 = (size_t)tile * TS;
+
+    /* ================= phase A: acc = W0[:, slice] X[tile, slice]^T ================= */
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) acc[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+        const char *xg = (const char *)(X + row0 * ldx + kbeg);
+        const unsigned int ldb = (unsigned int)ldx * 2u;
+        const __bf16 *wg = W0 + (size_t)(32 * wave + r16) * K0 + kbeg + 8 * q;
+        bf16x8 wr[P][2][2];
+        auto issue = [&](int s, int slot) {
+            char *img = lds + slot * STG;
+            glds_x_piece_sv<TS, 1>(xg + (size_t)s * 128, ldb, img, 2 * wave, lane);
+            glds_x_piece_sv<TS, 1>(xg + (size_t)s * 128, ldb, img, 2 * wave + 1, lane);
+            unsigned int z = 0;
+            asm volatile("" : "+s"(z));
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int kk = 0; kk < 2; kk++)
+                    wr[slot][i][kk] = *(const bf16x8 *)(wg + z + (size_t)i * 16 * K0 + (size_t)s * 64 + 32 * kk);
+        };
+        auto compute = [&](int slot) {
+            const char *img = lds + slot * STG;
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                bf16x8 bb[8];
+#pragma unroll
+                for (int sf = 0; sf < 8; sf++) bb[sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
+#pragma unroll
+                for (int sf = 0; sf < 8; sf++) {
+                    acc[0][sf] = mfma(wr[slot][0][kk], bb[sf], acc[0][sf]);
+                    acc[1][sf] = mfma(wr[slot][1][kk], bb[sf], acc[1][sf]);
+                }
+            }
+        };
+        /* 6 vector-memory ops per stage and wave (2 LDS-DMA + 4 W0 loads), completed in
+         * order: waiting for stage s leaves the later issued stages in flight */
+        auto step = [&](int s, auto Jc, auto LASTc) {
+            constexpr int j = decltype(Jc)::value;
+            constexpr bool last = decltype(LASTc)::value;
+            constexpr int ahead = last ? ((DIST - j) < (DIST - 1) ? (DIST - j) : (DIST - 1)) : (DIST - 1);
+            wait_vm<6 * ahead>();
+            lds_barrier(); /* stage s landed for every wave; stage s - 1 read by every wave */
+            if (!last || j + DIST < P) issue(s + DIST, (j + DIST) % P);
+            compute(j);
+        };
+        static_assert(NS % P == 0 && NS >= P, "stages");
+#pragma unroll
+        for (int s = 0; s < DIST; s++) issue(s, s);
+        for (int s0 = 0; s0 < NS - P; s0 += P) {
+            step(s0 + 0, std::integral_constant<int, 0>(), std::false_type());
+            step(s0 + 1, std::integral_constant<int, 1>(), std::false_type());
+            step(s0 + 2, std::integral_constant<int, 2>(), std::false_type());
+            step(s0 + 3, std::integral_constant<int, 3>(), std::false_type());
+        }
+        step(NS - 4, std::integral_constant<int, 0>(), std::true_type());
+        step(NS - 3, std::integral_constant<int, 1>(), std::true_type());
+        step(NS - 2, std::integral_constant<int, 2>(), std::true_type());
+        step(NS - 1, std::integral_constant<int, 3>(), std::true_type());
+        static_assert(P == 4, "step unroll");
+    }
+
+    int *role = (int *)(lds + OFF_RED + 5 * RED_W * 4);
+    /* ================= X: the two K slices of the tile meet ================= */
+    if constexpr (KSPLIT == 2) {
+        if (tid == 0) *role = (int)atomicInc(cnt + tile, 1u); /* 0: first, 1: second (and reset) */
+        __syncthreads();
+        f32x4 *pb = pbuf + ((size_t)tile * 8 + wave) * 16 * 64 + lane;
+        if (*role == 0) {
+#pragma unroll
+            for (int e = 0; e < 16; e++) st_sc1(pb + e * 64, acc[e >> 3][e & 7]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (tid == 0) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load((gu32 *)flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > XCH_TIMEOUT) {
+                    __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        f32x4 v[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) v[e] = ld_sc1(pb + e * 64);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int e = 0; e < 16; e++) acc[e >> 3][e & 7] += v[e];
+        if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    /* ================= B: the chain on the tile ================= */
+    char *imgH = lds + OFF_H, *imgD2 = lds + OFF_D2;
+    float *red_max = (float *)(lds + OFF_RED), *red_den = red_max + RED_W, *red_bt = red_den + RED_W;
+    float *red_zt = red_bt + RED_W;
+    int *red_it = (int *)(red_zt + RED_W);
+    /* layer-1 operand fragments (L2-resident), for the 32 outputs / hidden units of this wave */
+    bf16x8 wf[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) wf[i][ks] = *(const bf16x8 *)(W1 + (size_t)(32 * wave + 16 * i + r16) * HW + 32 * ks + 8 * q);
+    lds_barrier(); /* every wave is done with the phase-A ring */
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) {
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][sf][r]);
+            *(bf16x4 *)wr_ptr<TS>(imgH, lo, 16 * sf, 32 * wave + 16 * i) = o;
+        }
+    lds_barrier();
+    auto copy_out = [&](const char *img, __bf16 *out) {
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+            const int idx = tid + 512 * it, r = idx >> 5, c = (idx & 31) * 8;
+            *(uint4 *)(out + (row0 + r) * HW + c) = *(const uint4 *)(img + t32<TS>(r, c));
+        }
+    };
+    copy_out(imgH, H0out);
+
+    /* Z^T [o][s] = W1 H0^T: lane holds o = 32w + 16i + 4q + r, s = 16sf + r16 */
+    f32x4 z[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) z[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ks++) {
+        bf16x8 bb[8];
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) bb[sf] = rd_row<TS>(imgH, lo, 16 * sf, 32 * ks);
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) {
+            z[0][sf] = mfma(wf[0][ks], bb[sf], z[0][sf]);
+            z[1][sf] = mfma(wf[1][ks], bb[sf], z[1][sf]);
+        }
+    }
+
+    /* ---- output layer: per-sample max (and softmax denominator) across the 8 waves ---- */
+    float cm[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) cm[i][r] = (32 * wave + 16 * i + 4 * q + r < n_out) ? 1.f : 0.f;
+#pragma unroll
+    for (int sf = 0; sf < 8; sf++) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) m = cm[i][r] != 0.f ? fmaxf(m, z[i][sf][r]) : m;
+        m = rows_max(m);
+        if (q == 0) red_max[wave * TS + 16 * sf + r16] = m;
+    }
+    __syncthreads();
+    float gmax[8];
+#pragma unroll
+    for (int sf = 0; sf < 8; sf++) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 8; w++) m = fmaxf(m, red_max[w * TS + 16 * sf + r16]);
+        gmax[sf] = m;
+    }
+    /* hits, on the logits (before the softmax below overwrites z) */
+    float my_loss = 0.f;
+    unsigned int my_hit = 0;
+    int lab[8];
+#pragma unroll
+    for (int sf = 0; sf < 8; sf++) {
+        const size_t s = row0 + 16 * sf + r16;
+        const bool valid = (long)s < (long)n_valid;
+        lab[sf] = -1;
+        if constexpr (LABELS) {
+            lab[sf] = labels[valid ? s : (n_valid > 0 ? n_valid - 1 : 0)];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (valid && 32 * wave + 16 * i + 4 * q + r == lab[sf] && z[i][sf][r] >= gmax[sf]) my_hit++;
+        } else {
+            /* dense targets: the first max-target column of the sample, across the waves */
+            float bt = -INFINITY, zt = -INFINITY;
+            int ibt = 1 << 30;
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int c = 32 * wave + 16 * i + 4 * q + r;
+                    const float t = (valid && c < n_out) ? T[s * ldt + c] : -INFINITY;
+                    if (t > bt) { /* c ascends within a lane: strict > keeps the first */
+                        bt = t;
+                        ibt = c;
+                        zt = z[i][sf][r];
+                    }
+                }
+#pragma unroll
+            for (int hop = 0; hop < 2; hop++) { /* across q: the lower column wins ties */
+                const float ob = hop ? shfl_xor32(bt, lane) : shfl_xor16(bt, lane);
+                const float oz = hop ? shfl_xor32(zt, lane) : shfl_xor16(zt, lane);
+                const int oi = hop ? shfl_xor32(ibt, lane) : shfl_xor16(ibt, lane);
+                if (ob > bt || (ob == bt && oi < ibt)) {
+                    bt = ob;
+                    ibt = oi;
+                    zt = oz;
+                }
+            }
+            if (q == 0) {
+                red_bt[wave * TS + 16 * sf + r16] = bt;
+                red_zt[wave * TS + 16 * sf + r16] = zt;
+                red_it[wave * TS + 16 * sf + r16] = ibt;
+            }
+        }
+    }
+    float inv[8];
+    if constexpr (TYPE == 2) {
+#pragma unroll
+        for (int sf = 0; sf < 8; sf++) {
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float e = __expf(z[i][sf][r] - gmax[sf]) * cm[i][r];
+                    z[i][sf][r] = e; /* z holds e^{z - zmax} from here on */
+                    d += e;
+                }
+            d = rows_sum(d);
+            if (q == 0) red_den[wave * TS + 16 * sf + r16] = d;
+        }
+    }
+    __syncthreads();
+    const float inv_nout = 1.0f / (float)n_out;
+#pragma unroll
+    for (int sf = 0; sf < 8; sf++) {
+        const size_t s = row0 + 16 * sf + r16;
+        const bool valid = (long)s < (long)n_valid;
+        if constexpr (TYPE == 2) {
+            float d = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; w++) d += red_den[w * TS + 16 * sf + r16];
+            /* TINY in the shifted frame: 1e-14 * e^{1 - zmax}; ln(1e-14) = -32.2361913 */
+            d += __expf(fminf(-32.236191301916641f + 1.0f - gmax[sf], 80.f));
+            inv[sf] = __builtin_amdgcn_rcpf(d);
+        }
+        float l = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            bf16x4 dv;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int c = 32 * wave + 16 * i + 4 * q + r;
+                const float m = valid ? cm[i][r] : 0.f;
+                float t;
+                if constexpr (LABELS) t = (c == lab[sf]) ? t_hi : t_lo;
+                else t = (m != 0.f) ? T[s * ldt + c] : 0.f;
+                float o;
+                if constexpr (TYPE == 2) o = z[i][sf][r] * inv[sf];
+                else if constexpr (TYPE == 0) o = bipolar(z[i][sf][r]);
+                else o = z[i][sf][r];
+                float d;
+                if constexpr (TYPE == 0) d = (t - o) * dbipolar(o);
+                else d = t - o;
+                d *= m;
+                if constexpr (TYPE == 2) {
+                    if (m != 0.f && t != 0.f && o > 0.f) l += t * __logf(o + TINY);
+                } else {
+                    l += m * (t - o) * (t - o);
+                }
+                dv[r] = (__bf16)d;
+            }
+            *(bf16x4 *)wr_ptr<TS>(imgD2, lo, 16 * sf, 32 * wave + 16 * i) = dv;
+        }
+        if (valid) my_loss += (TYPE == 2) ? -l * inv_nout : 0.5f * l;
+        if constexpr (!LABELS) {
+            if (wave == 0 && q == 0 && valid) {
+                float bt = -INFINITY, zt = -INFINITY;
+                int ibt = 1 << 30;
+#pragma unroll
+                for (int w = 0; w < 8; w++) {
+                    const float ob = red_bt[w * TS + 16 * sf + r16];
+                    const int oi = red_it[w * TS + 16 * sf + r16];
+                    if (ob > bt || (ob == bt && oi < ibt)) {
+                        bt = ob;
+                        ibt = oi;
+                        zt = red_zt[w * TS + 16 * sf + r16];
+                    }
+                }
+                if (zt >= gmax[sf]) my_hit++;
+            }
+        }
+    }
+    /* W1^T fragments for delta1 (L2-resident) */
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) wf[i][ks] = *(const bf16x8 *)(W1t + (size_t)(32 * wave + 16 * i + r16) * HW + 32 * ks + 8 * q);
+    lds_barrier();
+    copy_out(imgD2, D2out);
+
+    /* ---- delta1 [s][h] = (delta2 W1)[s][h] f'(H0): lane holds h = 32w + 16i + 4q + r ---- */
+    {
+        f32x4 a[2][8];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int sf = 0; sf < 8; sf++) a[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) {
+            bf16x8 bb[8];
+#pragma unroll
+            for (int sf = 0; sf < 8; sf++) bb[sf] = rd_row<TS>(imgD2, lo, 16 * sf, 32 * ks);
+#pragma unroll
+            for (int sf = 0; sf < 8; sf++) {
+                a[0][sf] = mfma(wf[0][ks], bb[sf], a[0][sf]);
+                a[1][sf] = mfma(wf[1][ks], bb[sf], a[1][sf]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int sf = 0; sf < 8; sf++) {
+                bf16x4 *p = (bf16x4 *)wr_ptr<TS>(imgH, lo, 16 * sf, 32 * wave + 16 * i);
+                const bf16x4 hv = *p;
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[i][sf][r] * dbipolar((float)hv[r]));
+                *p = o; /* in place: only this lane reads these 8 bytes */
+            }
+    }
+    lds_barrier();
+    copy_out(imgH, D1out);
+
+    /* ---- loss / hits ---- */
+    my_loss = wave_sum(my_loss);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) my_hit += __shfl_xor(my_hit, o, 64);
+    float *sl = red_max;
+    unsigned int *shh = (unsigned int *)(red_max + 16);
+    if (lane == 0) {
+        sl[wave] = my_loss;
+        shh[wave] = my_hit;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float s = 0.f;
+        unsigned int h = 0;
+        for (int w = 0; w < 8; w++) {
+            s += sl[w];
+            h += shh[w];
+        }
+        if (loss_acc) atomicAdd(loss_acc + HPNN_STAT_SLOT(tile), s);
+        if (correct) atomicAdd(correct + HPNN_STAT_SLOT(tile), h);
+    }
+}
+
+template <int TYPE, bool LABELS, int NS, int KSPLIT>
+int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
+    auto kern = wide2_kernel<TYPE, LABELS, NS, KSPLIT>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
+        attr = true;
+    }
+    const int n_tiles = a.Bp / TS;
+    hipLaunchKernelGGL(kern, dim3(n_tiles * KSPLIT), dim3(512), LDS_TOTAL, stream, (const __bf16 *)a.X, a.ldx,
+                       (const __bf16 *)a.W0, a.K0, (const __bf16 *)a.W1, (const __bf16 *)a.W1t, a.labels, a.T, a.ldt,
+                       a.t_hi, a.t_lo, (__bf16 *)a.H0, (__bf16 *)a.D2, (__bf16 *)a.D1, (f32x4 *)a.pbuf, a.cnt,
+                       a.flag, a.err, a.loss_acc, a.correct, a.n_valid, a.n_out);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+template <int NS, int KSPLIT>
+int dispatch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
+    if (a.labels) {
+        if (a.type == 2) return launch_wide<2, true, NS, KSPLIT>(a, stream);
+        if (a.type == 0) return launch_wide<0, true, NS, KSPLIT>(a, stream);
+        return launch_wide<1, true, NS, KSPLIT>(a, stream);
+    }
+    if (a.type == 2) return launch_wide<2, false, NS, KSPLIT>(a, stream);
+    if (a.type == 0) return launch_wide<0, false, NS, KSPLIT>(a, stream);
+    return launch_wide<1, false, NS, KSPLIT>(a, stream);
+}
+
+}  // namespace
+
+/* KSPLIT (1 or 2) workgroups per 128-sample tile; HPNN_WIDE_KSPLIT forces one */
+extern "C" int hpnn_wide2_ksplit(int Bp, int K0) {
+    static const int forced = [] { const char *e = getenv("HPNN_WIDE_KSPLIT"); return e ? atoi(e) : 0; }();
+    if (Bp <= 0 || Bp % TS) return 0;
+    if (K0 != 4096) return 0;
+    if (forced == 1 || forced == 2) return forced;
+    return 2;
+}
+
+extern "C" long hpnn_wide2_pbuf_bytes(int Bp) { return (long)(Bp / TS) * 8 * 16 * 64 * 16; }
+
+extern "C" int hpnn_wide2_front(const hpnn_wide2_args *a, hipStream_t stream) {
+    if (!a || a->Bp <= 0 || a->Bp % TS || a->n_out < 1 || a->n_out > HW || a->n_valid > a->Bp) return -2;
+    if (!a->labels && !a->T) return -1;
+    if (a->ldx < a->K0 || a->ldx % 8) return -2;
+    if (((uintptr_t)a->X | (uintptr_t)a->W0 | (uintptr_t)a->W1 | (uintptr_t)a->W1t | (uintptr_t)a->H0 |
+         (uintptr_t)a->D2 | (uintptr_t)a->D1 | (uintptr_t)a->pbuf) & 15)
+        return -4;
+    const int ks = a->ksplit ? a->ksplit : hpnn_wide2_ksplit(a->Bp, a->K0);
+    if (hpnn_wide2_ksplit(a->Bp, a->K0) == 0 || (ks != 1 && ks != 2)) return -3;
+    if (ks == 2 && (!a->pbuf || !a->cnt || !a->flag || !a->err)) return -1;
+    if (ks == 2) return dispatch_wide<32, 2>(*a, stream);
+    return dispatch_wide<64, 1>(*a, stream);
+}

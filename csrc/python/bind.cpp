@@ -153,6 +153,24 @@ PYBIND11_MODULE(_native, m) {
         check(hpnn_update_fp(f64, P(W), P(V), P(G), Sn, gstride, n, lr, alpha, scale, momentum, S(stream)),
               "update_fp");
     });
+    m.def("wide2_front", [](uptr X, int ldx, int K0, uptr W0, uptr W1, uptr W1t, uptr labels, uptr T, int ldt,
+                            float t_hi, float t_lo, uptr H0, uptr D2, uptr D1, uptr pbuf, uptr cnt, uptr flag, uptr err,
+                            uptr loss, uptr correct, int Bp, int n_valid, int n_out, int type, int ksplit,
+                            uptr stream) {
+        hpnn_wide2_args a;
+        a.X = P(X), a.W0 = P(W0), a.W1 = P(W1), a.W1t = P(W1t);
+        a.ldx = ldx, a.K0 = K0;
+        a.labels = (const int *)P(labels);
+        a.T = (const float *)P(T);
+        a.ldt = ldt, a.t_hi = t_hi, a.t_lo = t_lo;
+        a.H0 = P(H0), a.D2 = P(D2), a.D1 = P(D1), a.pbuf = P(pbuf);
+        a.cnt = (unsigned int *)P(cnt), a.flag = (unsigned int *)P(flag), a.err = (unsigned int *)P(err);
+        a.loss_acc = (float *)P(loss), a.correct = (unsigned int *)P(correct);
+        a.Bp = Bp, a.n_valid = n_valid, a.n_out = n_out, a.type = type, a.ksplit = ksplit;
+        check(hpnn_wide2_front(&a, S(stream)), "wide2_front");
+    });
+    m.def("wide2_ksplit", [](int Bp, int K0) { return hpnn_wide2_ksplit(Bp, K0); });
+    m.def("wide2_pbuf_bytes", [](int Bp) { return hpnn_wide2_pbuf_bytes(Bp); });
     m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
     m.def("mlp3_tile_trace", []() {
         std::vector<unsigned long long> v(1024 * 12);

@@ -31,6 +31,9 @@ PIXEL_SCALE = float(torch.tensor(float(os.environ.get("HPNN_PIXEL_SCALE", str(1.
 # HPNN_TILE=0: the 32-sample pipelined front (mlp3_fused, "x") instead of the 256-sample
 # tile kernel (mlp3_tile, "t") on eligible MNIST-shaped nets
 _TILE = os.environ.get("HPNN_TILE", "1") != "0"
+# HPNN_WIDE=0: the per-layer kernels instead of the wide-input front ("w") for
+# 4096 -> 256 -> 256 (padded) nets
+_WIDE = os.environ.get("HPNN_WIDE", "1") != "0"
 
 TYPES = {"ANN": ops.TYPE_ANN, "LNN": ops.TYPE_LNN, "SNN": ops.TYPE_SNN}
 
@@ -116,12 +119,17 @@ class MLP:
         eligible = self.L == 3 and tuple(self.Np) == ops.MLP3_DIMS
         x_ok = eligible and self.Kp[0] in ops.MLP3F_K0
         t_ok = eligible and self.Kp[0] in ops.MLP3T_K0 and self.Bp % ops.MLP3T_TILE == 0
+        #   "w"   : wide2_front (K0 = 4096 -> 256 -> 256: X -> H0, delta2, delta1 in one kernel)
+        w_ok = (self.L == 2 and tuple(self.Np) == (256, 256) and self.Kp[0] in ops.WIDE2_K0
+                and self.Bp % ops.WIDE2_TILE == 0)
         if fused is None or fused is True:
             mode = "t" if (t_ok and _TILE) else ("x" if x_ok else ("mid" if eligible else None))
+            if mode is None and w_ok and _WIDE:
+                mode = "w"
             if fused is True and mode is None:
                 raise ValueError(f"fused path needs padded dims {ops.MLP3_DIMS}, got {self.Np}")
-        elif fused in ("x", "mid", "t"):
-            if not {"x": x_ok, "mid": eligible, "t": t_ok}[fused]:
+        elif fused in ("x", "mid", "t", "w"):
+            if not {"x": x_ok, "mid": eligible, "t": t_ok, "w": w_ok}[fused]:
                 raise ValueError(f"fused={fused!r} not available for dims {self.Kp[0]}-{self.Np}")
             mode = fused
         else:
@@ -129,6 +137,7 @@ class MLP:
         self.fused_mode = mode
         self.fused = mode is not None
         self.W0f = None
+        self.wide_ws = ops.Wide2Workspace(self.Bp, self.Kp[0], dev) if mode == "w" else None
         if mode == "mid":
             grid = max(1, min(mid_grid, self.Bp // 64))
             self.midslab = torch.empty(grid, ops.MLP3_SLAB, dtype=torch.float32, device=dev)
@@ -324,6 +333,13 @@ class MLP:
         buckets).  on_ready(l) is called as soon as layer l's gradient is final (layers
         become ready from the last to the first)."""
         n_valid = self.Bp if n_valid is None else n_valid
+        if self.fused_mode == "w":
+            self._fused_front(X, labels, T, n_valid)
+            for l in (1, 0):
+                self.grad_layer(l, X, reduce=reduce)
+                if on_ready:
+                    on_ready(l)
+            return
         if self.fused:
             self._fused_front(X, labels, T, n_valid)
             # G1 | G2 are contiguous in grad_flat, exactly the per-block slab layout
@@ -350,7 +366,10 @@ class MLP:
         t_hi, t_lo = self._t_hilo()
         kw = dict(labels=labels, T=T, t_hi=t_hi, t_lo=t_lo, n_valid=n_valid, loss_acc=self.stats[0, 0:1],
                   correct=self.stats[0, 1:2])
-        if self.fused_mode == "t":
+        if self.fused_mode == "w":
+            ops.wide2_front(X, self.Wb[0], self.Wb[1], self.Wt[1], self.H[0], self.D[1], self.D[0], self.wide_ws,
+                            self.n_out, self.type, **kw)
+        elif self.fused_mode == "t":
             ops.mlp3_tile(X, self.Kp[0], self.Wb[0], self.W0f, self.Wb[1], self.Wb[2], self.Wt[2], self.D[0],
                           self.midslab, self.n_out, self.type, xscale=getattr(X, "hpnn_fm_scale", 1.0), **kw)
         elif self.fused_mode == "x":
@@ -385,6 +404,11 @@ class MLP:
             g1, g2 = self._mid_group_views()
             self.update_all(lr, alpha, scale, [self.slab[0], g1, g2])
             return
+        if self.fused_mode == "w":
+            # one launch up to the deltas, then the per-layer weight gradients and steps
+            self._fused_front(X, labels, T, n_valid)
+            self._grads_and_steps(X, lr, alpha, scale)
+            return
         if self.fused:
             self.backward_grads(X, labels=labels, T=T, n_valid=n_valid)
             self.update_layer(0, lr, alpha, scale)
@@ -393,8 +417,13 @@ class MLP:
             return
         self.forward(X)
         self.output(labels=labels, T=T, n_valid=n_valid)
+        self._grads_and_steps(X, lr, alpha, scale, backprop=True)
+
+    def _grads_and_steps(self, X, lr, alpha, scale, backprop=False):
+        """from the last layer to the first: (backprop: the delta of the layer below, with the
+        pre-update W_l^T), the weight gradient and the optimizer step"""
         for l in range(self.L - 1, -1, -1):
-            if l > 0:
+            if backprop and l > 0:
                 self.backward_layer(l)  # pre-update W_l^T, before layer l's step below
             Hin = X if l == 0 else self.H[l - 1]
             if self._tn_update_ok(l) and ops.gemm_tn_update(self.D[l], Hin, self.W32[l], self.V32[l], self.Wb[l],

@@ -287,6 +287,55 @@ def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=
     return D1g
 
 
+WIDE2_K0 = (4096,)  # first-layer input widths of hpnn_wide2_front
+WIDE2_TILE = 128  # samples per tile (the batch must be a multiple)
+
+
+class Wide2Workspace:
+    """hand-over state of hpnn_wide2_front with two workgroups per tile: the FP32 partial
+    buffer and the per-tile counter / flag words (zeroed once, self-resetting) plus an
+    error word (set if a hand-over ever timed out)."""
+
+    def __init__(self, Bp, K0, device, ksplit=None):
+        if torch.device(device).type != "cuda":
+            self.ksplit = 1
+        else:
+            self.ksplit = int(ksplit) if ksplit else native().wide2_ksplit(int(Bp), int(K0))
+        n_tiles = Bp // WIDE2_TILE
+        nb = native().wide2_pbuf_bytes(int(Bp)) if self.ksplit == 2 else 16
+        self.pbuf = torch.empty(nb // 4, dtype=torch.float32, device=device)
+        self.words = torch.zeros(2 * n_tiles + 4, dtype=torch.int32, device=device)
+        self.cnt, self.flag = self.words[:n_tiles], self.words[n_tiles:2 * n_tiles]
+        self.err = self.words[2 * n_tiles:2 * n_tiles + 1]
+
+    def check(self):
+        if int(self.err.item()) != 0:
+            raise RuntimeError("wide2_front: a partial-sum hand-over timed out")
+
+
+def wide2_front(X, W0, W1, W1t, H0, D2, D1, ws, n_out, net_type, labels=None, T=None, t_hi=1.0, t_lo=0.0,
+                n_valid=None, loss_acc=None, correct=None):
+    """The K0 (4096) -> 256 -> 256 step up to the deltas in one launch
+    (csrc/gpu/kernels_wide.hip): X [Bp, K0] bf16 -> H0 = f(X W0^T), delta2 (output layer)
+    and delta1 = (delta2 W1) f'(H0), all [Bp, 256] bf16, plus loss / hits.  ws: a
+    Wide2Workspace.  CPU tensors: the same rounding points in PyTorch."""
+    Bp, K0 = X.shape[0], W0.shape[1]
+    n_valid = Bp if n_valid is None else int(n_valid)
+    if _cpu(X):
+        h = bipolar(X[:, :K0].float() @ W0.float().t()).bfloat16()
+        H0.copy_(h)
+        Z = h.float() @ W1.float().t()
+        _cpu_output_delta(Z, n_out, net_type, D2, labels, T, t_hi, t_lo, n_valid, None, loss_acc, correct)
+        D1.copy_(((D2.float() @ W1.float()) * dbipolar(h.float())).bfloat16())
+        return D1
+    native().wide2_front(X.data_ptr(), X.stride(0), K0, W0.data_ptr(), W1.data_ptr(), W1t.data_ptr(), _ptr(labels),
+                         _ptr(T), T.stride(0) if T is not None else 0, float(t_hi), float(t_lo), H0.data_ptr(),
+                         D2.data_ptr(), D1.data_ptr(), ws.pbuf.data_ptr(), ws.cnt.data_ptr(), ws.flag.data_ptr(),
+                         ws.err.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid, n_out, net_type, ws.ksplit,
+                         _stream())
+    return D1
+
+
 def frag_major(W):
     """[N, K] -> flat MFMA-fragment-major copy (layout of hpnn_sgd_update_multi's Wf):
     element (n, k) at (((n//16)*(K//32) + k//32)*64 + n%16 + 16*((k//8)%4))*8 + k%8."""
