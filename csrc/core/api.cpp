@@ -241,6 +241,10 @@ extern "C" nn_def *_NN(load, conf)(const CHAR *filename) {
         } else if (is("epochs")) {
             conf->epochs = (UINT)strtoul(v.c_str(), NULL, 10);
             if (!conf->epochs) conf->epochs = 1;
+        } else if (is("parallel")) {
+            std::string u = v;
+            for (auto &ch : u) ch = (char)tolower(ch);
+            conf->parallel = u == "tp" ? NN_PARALLEL_TP : NN_PARALLEL_DP;
         } else if (is("lr")) {
             conf->lr = strtod(v.c_str(), NULL);
         } else if (is("momentum")) {
@@ -301,6 +305,7 @@ extern "C" void _NN(dump, conf)(nn_def *conf, FILE *fp) {
         static const char *dn[] = {"f64", "f32", "bf16"};
         _OUT(fp, "[mode] batched\n[batch] %u\n[epochs] %u\n[dtype] %s\n", conf->batch, conf->epochs,
              dn[conf->dtype]);
+        if (conf->parallel == NN_PARALLEL_TP) _OUT(fp, "[parallel] tp\n");
     }
     if (conf->lr > 0) _OUT(fp, "[lr] %.17g\n", conf->lr);
     if (conf->momentum >= 0) _OUT(fp, "[momentum] %.17g\n", conf->momentum);
@@ -519,6 +524,10 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
         UINT ng = 1;
         _NN(get, n_gpu)(&ng);
         o.n_gpu = ng ? ng : 1;
+        {
+            const char *pe = getenv("HPNN_PARALLEL");
+            o.tp = (pe ? (pe[0] == 't' || pe[0] == 'T') : conf->parallel == NN_PARALLEL_TP) ? 1 : 0;
+        }
         hpnn_batched_stats st;
         memset(&st, 0, sizeof(st));
         BOOL ok;

@@ -45,6 +45,7 @@ typedef struct {
     UINT n_gpu;       /* data-parallel replicas driven by this process */
     BOOL resume;      /* BPM: start from the momentum in k->dw (exact resume)  */
     UINT epoch0;      /* epochs completed before this call (metrics numbering) */
+    UINT tp;          /* 1: row-sharded tensor parallelism ([parallel] tp; f64 / f32) */
 } hpnn_batched_opts;
 
 typedef struct {
@@ -60,6 +61,10 @@ typedef struct {
  * k->dw (allocated if needed) so that nn_dump_state can save it. */
 BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n,
                             const hpnn_batched_opts *o, hpnn_batched_stats *st);
+/* the same with every hidden layer's rows sharded over the ranks (tp_engine.cpp): ranks =
+ * HPNN_LOOPBACK_RANKS threads on GPU 0, the launcher's processes, or o->n_gpu GPUs */
+BOOL hpnn_gpu_train_tp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                       hpnn_batched_stats *st);
 /* batched inference: Y = net(X), n x n_out (host) */
 BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
                             DOUBLE *Y);

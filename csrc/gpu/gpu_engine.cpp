@@ -373,7 +373,9 @@ BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBL
 }
 
 /* online slots: HPNN_ONLINE_SLOTS=S runs S virtual slots on device 0 (tests of the
- * device-spanning protocol on one GPU); else the runtime's GPU count (train_nn -G N) */
+ * device-spanning protocol on one GPU; S = 2: every slot's persistent launch needs a
+ * hardware queue of its own to run concurrently, and a process gets GPU_MAX_HW_QUEUES = 4
+ * of them); else the runtime's GPU count (train_nn -G N) */
 int online_slots(bool *loopback) {
     const char *e = getenv("HPNN_ONLINE_SLOTS");
     const int v = e ? atoi(e) : 0;
@@ -1155,6 +1157,7 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         NN_ERROR(stderr, "GPU batched engine: unsupported dtype %d\n", (int)o->dtype);
         return FALSE;
     }
+    if (o->tp) return hpnn_gpu_train_tp(k, X, T, n, o, st);
     const char *lb = getenv("HPNN_LOOPBACK_RANKS");
     const int lbr = lb ? atoi(lb) : 0;
     const char *fr = getenv("HPNN_FORCE_RCCL");

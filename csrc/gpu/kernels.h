@@ -218,6 +218,8 @@ int hpnn_update_fp(int f64, void *W, void *V, const void *G, int S, long gstride
                    double scale, int momentum, hipStream_t stream);
 /* out = sum_s G[s] */
 int hpnn_reduce_fp(int f64, void *out, const void *G, int S, long gstride, long n, hipStream_t stream);
+/* out[i] = in[i] * f'(aux[i]) (in place allowed): f' applied to reduced partial deltas */
+int hpnn_dact_fp(int f64, void *out, const void *in, const void *aux, long n, hipStream_t stream);
 
 /* floats per block slab written by hpnn_mlp3_mid */
 int hpnn_mlp3_slab_floats(void);

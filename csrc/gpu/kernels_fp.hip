@@ -253,6 +253,13 @@ __global__ __launch_bounds__(256) void reduce_fp_kernel(T *__restrict__ out, con
 }
 
 template <typename T>
+__global__ __launch_bounds__(256) void dact_fp_kernel(T *__restrict__ out, const T *__restrict__ in,
+                                                      const T *__restrict__ aux, long n) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        out[i] = in[i] * dact_fp<T>(aux[i]);
+}
+
+template <typename T>
 int gemm_fp(const void *A, int lda, int ta, const void *B, int ldb, int tb, void *C, int ldc, const void *aux,
             int ldaux, int M, int N, int K, int epi, int splits, long slab_stride, hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -2;
@@ -319,6 +326,19 @@ extern "C" int hpnn_update_fp(int f64, void *W, void *V, const void *G, int S, l
     else
         hipLaunchKernelGGL(update_fp_kernel<float>, grid, dim3(256), 0, stream, (float *)W, (float *)V,
                            (const float *)G, S, gstride, n, (float)lr, (float)alpha, (float)scale, momentum);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_dact_fp(int f64, void *out, const void *in, const void *aux, long n, hipStream_t stream) {
+    if (n <= 0) return -2;
+    long blocks = (n + 255) / 256;
+    const dim3 grid(blocks < 4096 ? blocks : 4096);
+    if (f64)
+        hipLaunchKernelGGL(dact_fp_kernel<double>, grid, dim3(256), 0, stream, (double *)out, (const double *)in,
+                           (const double *)aux, n);
+    else
+        hipLaunchKernelGGL(dact_fp_kernel<float>, grid, dim3(256), 0, stream, (float *)out, (const float *)in,
+                           (const float *)aux, n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

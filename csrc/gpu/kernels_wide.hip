@@ -18,9 +18,11 @@
  *     for all 128 samples (16 MFMA 16x16x32 per 32 features, 64 accumulator registers):
  *     each W0 element is read once per workgroup, straight from the L2 into registers
  *     (the XCD's workgroups share a K slice: tile = block / 2, slice = block % 2, and
- *     blocks b, b + 8 share an XCD).  The X slice streams through a 4-stage LDS ring by
- *     LDS-DMA (8 rows x 128 B per instruction: whole cache lines), 16 KiB per 64 features,
- *     read back conflict-free with ds_read_b128.  One barrier per stage.
+ *     blocks b, b + 8 share an XCD).  The X slice is register-staged, 4 stages of 64
+ *     features ahead (32 B per thread per stage, whole 128-B rows per 4 threads), into a
+ *     2 x 16 KiB LDS double buffer read back conflict-free with ds_read_b128; one barrier
+ *     per stage.  (An LDS-DMA ring measured slower here: the compiler cannot count the
+ *     DMA in its vmcnt waits for the W0 register loads, which then drained the ring.)
  *  X  KSPLIT = 2: the first of the two workgroups of a tile to finish (a self-resetting
  *     atomicInc per tile) hands its FP32 partial over through memory with write-through
  *     (sc1) stores and an sc1 flag, and exits; the second adds it (a + b == b + a: the
@@ -40,7 +42,7 @@
  * gradients and updates that follow are unchanged): H0, delta2, delta1; loss / hits into
  * the HPNN_STAT_SLOT slots.
  *
- * LDS: phase A ring 4 x 16 KiB (aliased by the chain) | chain: H0 / delta1 image 64 KiB,
+ * LDS: phase A double buffer 2 x 16 KiB (aliased by the chain) | chain: H0 / delta1 image 64 KiB,
  * delta2 image 64 KiB, cross-wave reduction words 20 KiB.
  */
 #include <hip/hip_runtime.h>
@@ -61,12 +63,11 @@ namespace {
 constexpr int TS = 128;                /* samples per tile */
 constexpr int HW = 256;                /* hidden / output width (padded) */
 constexpr int STG = TS * 64 * 2;       /* one 64-feature stage of X: 16 KiB */
-constexpr int P = 4, DIST = P - 1;     /* ring stages, stages issued ahead */
 constexpr int IMG = TS * HW * 2;       /* [128][256] bf16 image: 64 KiB */
 constexpr int OFF_H = 0, OFF_D2 = IMG, OFF_RED = 2 * IMG;
 constexpr int RED_W = 8 * TS;          /* floats per reduction array ([wave][sample]) */
 constexpr int LDS_TOTAL = OFF_RED + 5 * RED_W * 4 + 16;
-static_assert(P * STG <= OFF_RED, "ring aliases the chain images");
+static_assert(2 * STG <= OFF_RED, "the X double buffer aliases the chain images");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
 constexpr unsigned long long XCH_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
@@ -112,24 +113,34 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 #pragma unroll
         for (int sf = 0; sf < 8; sf++) acc[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-        const char *xg = (const char *)(X + row0 * ldx + kbeg);
-        const unsigned int ldb = (unsigned int)ldx * 2u;
+        /* X: register-staged (every load is the compiler's, so its vmcnt waits are exact):
+         * thread t fetches 32 B of row t/4 per stage, 4 stages ahead, and writes them into
+         * the other half of a 2 x 16 KiB LDS double buffer one stage ahead of their use.
+         * W0: this wave's 4 fragments per stage straight into registers, 3 stages ahead. */
+        const int xr_row = tid >> 2, xc0 = (tid & 3) * 2;
+        const char *xrow = (const char *)(X + (row0 + xr_row) * ldx + kbeg) + xc0 * 16;
         const __bf16 *wg = W0 + (size_t)(32 * wave + r16) * K0 + kbeg + 8 * q;
-        bf16x8 wr[P][2][2];
-        auto issue = [&](int s, int slot) {
-            char *img = lds + slot * STG;
-            glds_x_piece_sv<TS, 1>(xg + (size_t)s * 128, ldb, img, 2 * wave, lane);
-            glds_x_piece_sv<TS, 1>(xg + (size_t)s * 128, ldb, img, 2 * wave + 1, lane);
-            unsigned int z = 0;
-            asm volatile("" : "+s"(z));
+        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+        u32x4 xr[4][2]; /* native vectors: promoted to registers (HIP's uint4 struct was not) */
+        bf16x8 wr[4][2][2];
+        auto load_x = [&](int s, int slot) {
+            xr[slot][0] = *(const u32x4 *)(xrow + (size_t)s * 128);
+            xr[slot][1] = *(const u32x4 *)(xrow + (size_t)s * 128 + 16);
+        };
+        auto load_w = [&](int s, int slot) {
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
                 for (int kk = 0; kk < 2; kk++)
-                    wr[slot][i][kk] = *(const bf16x8 *)(wg + z + (size_t)i * 16 * K0 + (size_t)s * 64 + 32 * kk);
+                    wr[slot][i][kk] = *(const bf16x8 *)(wg + (size_t)i * 16 * K0 + (size_t)s * 64 + 32 * kk);
         };
-        auto compute = [&](int slot) {
-            const char *img = lds + slot * STG;
+        auto store_x = [&](int slot, int lslot) {
+            char *img = lds + lslot * STG;
+            *(u32x4 *)(img + w128_off(xr_row, xc0)) = xr[slot][0];
+            *(u32x4 *)(img + w128_off(xr_row, xc0 + 1)) = xr[slot][1];
+        };
+        auto compute = [&](int wslot, int lslot) {
+            const char *img = lds + lslot * STG;
 #pragma unroll
             for (int kk = 0; kk < 2; kk++) {
                 bf16x8 bb[8];
@@ -137,36 +148,27 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
                 for (int sf = 0; sf < 8; sf++) bb[sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
 #pragma unroll
                 for (int sf = 0; sf < 8; sf++) {
-                    acc[0][sf] = mfma(wr[slot][0][kk], bb[sf], acc[0][sf]);
-                    acc[1][sf] = mfma(wr[slot][1][kk], bb[sf], acc[1][sf]);
+                    acc[0][sf] = mfma(wr[wslot][0][kk], bb[sf], acc[0][sf]);
+                    acc[1][sf] = mfma(wr[wslot][1][kk], bb[sf], acc[1][sf]);
                 }
             }
         };
-        /* 6 vector-memory ops per stage and wave (2 LDS-DMA + 4 W0 loads), completed in
-         * order: waiting for stage s leaves the later issued stages in flight */
-        auto step = [&](int s, auto Jc, auto LASTc) {
-            constexpr int j = decltype(Jc)::value;
-            constexpr bool last = decltype(LASTc)::value;
-            constexpr int ahead = last ? ((DIST - j) < (DIST - 1) ? (DIST - j) : (DIST - 1)) : (DIST - 1);
-            wait_vm<6 * ahead>();
-            lds_barrier(); /* stage s landed for every wave; stage s - 1 read by every wave */
-            if (!last || j + DIST < P) issue(s + DIST, (j + DIST) % P);
-            compute(j);
-        };
-        static_assert(NS % P == 0 && NS >= P, "stages");
+        static_assert(NS % 4 == 0, "stages");
 #pragma unroll
-        for (int s = 0; s < DIST; s++) issue(s, s);
-        for (int s0 = 0; s0 < NS - P; s0 += P) {
-            step(s0 + 0, std::integral_constant<int, 0>(), std::false_type());
-            step(s0 + 1, std::integral_constant<int, 1>(), std::false_type());
-            step(s0 + 2, std::integral_constant<int, 2>(), std::false_type());
-            step(s0 + 3, std::integral_constant<int, 3>(), std::false_type());
+        for (int s = 0; s < 4; s++) load_x(s, s);
+#pragma unroll
+        for (int s = 0; s < 3; s++) load_w(s, s);
+        store_x(0, 0);
+        lds_barrier();
+        /* fully unrolled: every ring index static (register arrays stay in registers) */
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            if (s + 4 < NS) load_x(s + 4, s & 3);       /* slot of stage s: already in LDS */
+            if (s + 3 < NS) load_w(s + 3, (s + 3) & 3); /* slot of stage s - 1: consumed */
+            compute(s & 3, s & 1);
+            if (s + 1 < NS) store_x((s + 1) & 3, (s + 1) & 1); /* stage s + 1, other buffer */
+            lds_barrier();
         }
-        step(NS - 4, std::integral_constant<int, 0>(), std::true_type());
-        step(NS - 3, std::integral_constant<int, 1>(), std::true_type());
-        step(NS - 2, std::integral_constant<int, 2>(), std::true_type());
-        step(NS - 1, std::integral_constant<int, 3>(), std::true_type());
-        static_assert(P == 4, "step unroll");
     }
 
     int *role = (int *)(lds + OFF_RED + 5 * RED_W * 4);

@@ -416,6 +416,8 @@ __device__ __forceinline__ void coop_barrier(unsigned int *ctl, unsigned int tar
 #pragma unroll
             for (int k = 0; k < COOP_SUB; k++) sum += __hip_atomic_load(c + k * COOP_LINE, __ATOMIC_RELAXED, SC);
             if (sum >= target) break;
+            /* another workgroup already timed out: every later barrier gives up at once */
+            if (__hip_atomic_load(c + COOP_ERR, __ATOMIC_RELAXED, SC)) break;
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > COOP_TIMEOUT) {
                 __hip_atomic_store(c + COOP_ERR, 1u, __ATOMIC_RELAXED, SC);

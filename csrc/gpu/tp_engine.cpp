@@ -1,0 +1,619 @@
+/*
+ * Row-sharded tensor parallelism for the FP64 / FP32 batched GPU engine ([parallel] tp,
+ * [dtype] f64 | f32): the reference's model-parallel scheme (every layer's neuron rows
+ * split over MPI ranks / GPUs, ann.c:912-1236 with MPI_Allgather at ann.c:925, 957, 990;
+ * cuda_ann.cu:533-1275 over n_gpu x n_streams), with the whole minibatch on every rank.
+ *
+ * Activations are kept FEATURE-MAJOR (H^T [features][batch]): rank r owns the feature rows
+ * [r n_l, (r+1) n_l) of every hidden layer, so an all-gather of the local rows IS the full
+ * H^T, with no re-ordering.  Per step, rank r:
+ *
+ *   forward   H_l^T[R_r] = f(W_l[R_r] H_{l-1}^T)            FP64/FP32 MFMA GEMM, local
+ *             H_l^T      = all_gather(H_l^T[R_r])            n_l x B elements per rank
+ *   output    the output layer is replicated (it is narrow: n_out <= a few hundred):
+ *             Z = H_{L-1} W_L^T, softmax / loss / delta_L on every rank, bit-identical
+ *   backward  delta_{L-1}^T[R_r] = (W_L[:, R_r])^T delta_L^T * f'(H)   local, no comm
+ *             G_l[R_r] = delta_l^T[R_r] H_{l-1}                          local
+ *             P^T = W_l[R_r]^T delta_l^T[R_r]  (this rank's share of every input's delta)
+ *             delta_{l-1}^T[R_r] = reduce_scatter(P^T) * f'(H_{l-1}^T[R_r])
+ *                                  (the f' epilogue runs on the reduced rows: hpnn_dact_fp)
+ *   update    local rows only (the replicated output layer: the same update everywhere)
+ *
+ * so the weights are never moved (the reference all-gathered every N_l x M_l weight
+ * matrix after each update); a step moves B x (sum of hidden widths) activations and
+ * partial deltas.  Rows are padded to P x ceil(N_l / P) with zero weights, which keep
+ * their activations, deltas and gradients at zero.
+ *
+ * Collectives: RCCL (one process per GPU under a launcher, or one host thread per GPU of
+ * this process with train_nn -G N) or, with HPNN_LOOPBACK_RANKS = P, P host threads on ONE
+ * GPU exchanging through a device staging buffer (tests and CI without a multi-GPU node).
+ */
+#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
+#include <libhpnn/ann.h>
+#include <libhpnn/bootstrap.h>
+#include <libhpnn/comm.h>
+#include <libhpnn/devmem.h>
+#include <libhpnn/observe.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../core/runtime_internal.h"
+#include "engine.h"
+#include "kernels.h"
+
+#define TPCHK(x)                                                                                  \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
+            NN_ERROR(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return FALSE;                                                                         \
+        }                                                                                         \
+    } while (0)
+
+namespace {
+
+layer_ann *layer_at(kernel_ann *k, int l) { return l < (int)k->n_hiddens ? &k->hiddens[l] : &k->output; }
+constexpr size_t ACC_BYTES = (size_t)HPNN_STAT_SLOTS * HPNN_STAT_STRIDE * 4;
+
+/* ---------------------------------------------------------------- collectives */
+template <typename T>
+struct TpColl {
+    virtual ~TpColl() {}
+    /* recv [P][count] <- every rank's send [count] */
+    virtual bool all_gather(const T *send, T *recv, long count, hipStream_t s) = 0;
+    /* recv [count] <- sum over ranks of their send[r * count ...] (send: [P][count]) */
+    virtual bool reduce_scatter(const T *send, T *recv, long count, hipStream_t s) = 0;
+    /* full weights for the host copy: same as all_gather, off the hot path */
+    virtual bool gather_rows(const T *send, T *recv, long count, hipStream_t s) { return all_gather(send, recv, count, s); }
+    virtual void abort() {}
+};
+
+template <typename T>
+struct RcclColl : TpColl<T> {
+    hpnn_comm *c;
+    static constexpr hpnn_comm_dtype DT = sizeof(T) == 8 ? HPNN_DT_F64 : HPNN_DT_F32;
+    explicit RcclColl(hpnn_comm *cc) : c(cc) {}
+    bool all_gather(const T *send, T *recv, long count, hipStream_t s) override {
+        return hpnn_comm_all_gather(c, send, recv, count, DT, s) == 0;
+    }
+    bool reduce_scatter(const T *send, T *recv, long count, hipStream_t s) override {
+        return hpnn_comm_reduce_scatter(c, send, recv, count, DT, HPNN_OP_SUM, s) == 0;
+    }
+};
+
+/* host-thread ranks on one device: a generation barrier (abortable, so one failing rank
+ * cannot leave the others waiting) and a device staging buffer */
+struct HostBarrier {
+    std::mutex m;
+    std::condition_variable cv;
+    int P = 1, count = 0;
+    unsigned gen = 0;
+    bool aborted = false;
+    bool wait() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
+        const unsigned g = gen;
+        if (++count == P) {
+            count = 0;
+            gen++;
+            cv.notify_all();
+            return true;
+        }
+        cv.wait(lk, [&] { return gen != g || aborted; });
+        return !aborted;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+template <typename T>
+struct HostShared {
+    int P = 1;
+    T *stage = nullptr;
+    HostBarrier bar;
+    ~HostShared() { hpnn_dev_free(stage); }
+};
+
+template <typename T>
+struct HostColl : TpColl<T> {
+    HostShared<T> *sh;
+    int r;
+    HostColl(HostShared<T> *s_, int rank) : sh(s_), r(rank) {}
+    bool all_gather(const T *send, T *recv, long count, hipStream_t s) override {
+        const size_t b = (size_t)count * sizeof(T);
+        if (hipMemcpyAsync(sh->stage + (size_t)r * count, send, b, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || !sh->bar.wait())
+            return false;
+        if (hipMemcpyAsync(recv, sh->stage, b * sh->P, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return false;
+        return sh->bar.wait();
+    }
+    bool reduce_scatter(const T *send, T *recv, long count, hipStream_t s) override {
+        const long blk = (long)sh->P * count; /* rank q's whole send at stage + q * blk */
+        if (hipMemcpyAsync(sh->stage + (size_t)r * blk, send, (size_t)blk * sizeof(T), hipMemcpyDeviceToDevice, s) !=
+                hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || !sh->bar.wait())
+            return false;
+        /* sum in rank order: deterministic */
+        if (hpnn_reduce_fp(sizeof(T) == 8, recv, sh->stage + (size_t)r * count, sh->P, blk, count, s) != 0 ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return false;
+        return sh->bar.wait();
+    }
+    void abort() override { sh->bar.abort(); }
+};
+
+/* ---------------------------------------------------------------- one rank's shard */
+template <typename T>
+struct TpNet {
+    static constexpr int F64 = sizeof(T) == 8 ? 1 : 0;
+    int L = 0, P = 1, r = 0, Bp = 0, n_out = 0, type = 2;
+    int Ntrue[16], Mtrue[16], n[16], Mp[16], S[16];
+    T *W[16] = {0}, *V[16] = {0}, *slab[16] = {0}, *Hloc[16] = {0}, *Hfull[16] = {0}, *Dloc[16] = {0};
+    T *DL = nullptr, *Z = nullptr, *part = nullptr;
+    float *acc = nullptr;
+    hipStream_t s = nullptr;
+    TpColl<T> *coll = nullptr;
+
+    ~TpNet() {
+        if (s) hipStreamSynchronize(s);
+        for (int l = 0; l < 16; l++) {
+            hpnn_dev_free(W[l]);
+            hpnn_dev_free(V[l]);
+            hpnn_dev_free(slab[l]);
+            hpnn_dev_free(Hloc[l]);
+            hpnn_dev_free(Hfull[l]);
+            hpnn_dev_free(Dloc[l]);
+        }
+        hpnn_dev_free(DL);
+        hpnn_dev_free(Z);
+        hpnn_dev_free(part);
+        hpnn_dev_free(acc);
+    }
+
+    static int pick(int Nn, int Mm, int B) {
+        const int tiles = ((Nn + 63) / 64) * ((Mm + 63) / 64);
+        int sp = (256 + tiles - 1) / tiles;
+        const int maxs = B / 256 > 0 ? B / 256 : 1;
+        sp = sp < maxs ? sp : maxs;
+        return hpnn_gemm_fp_splits(B, sp < 1 ? 1 : sp);
+    }
+
+    /* rows of layer l this rank holds in the host weights: global row of local row j */
+    int grow(int l, int j) const { return l < L - 1 ? r * n[l] + j : j; }
+
+    BOOL init(kernel_ann *k, int P_, int r_, int B, nn_type t, bool momentum, hipStream_t st, TpColl<T> *c) {
+        P = P_, r = r_, s = st, coll = c, Bp = B;
+        L = (int)k->n_hiddens + 1;
+        n_out = (int)k->n_outputs;
+        type = t == NN_TYPE_ANN ? 0 : (t == NN_TYPE_LNN ? 1 : 2);
+        size_t part_elems = 0;
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_at(k, l);
+            Ntrue[l] = (int)ly->n_neurons;
+            Mtrue[l] = (int)ly->n_inputs;
+            n[l] = l < L - 1 ? (Ntrue[l] + P - 1) / P : Ntrue[l];
+            Mp[l] = l == 0 ? Mtrue[0] : (l - 1 < L - 1 ? P * n[l - 1] : Mtrue[l]);
+            S[l] = pick(n[l], Mp[l], Bp);
+            const size_t nw = (size_t)n[l] * Mp[l];
+            TPCHK(hpnn_dev_malloc(&W[l], nw * sizeof(T)));
+            TPCHK(hpnn_dev_malloc(&slab[l], nw * sizeof(T) * S[l]));
+            if (momentum) {
+                TPCHK(hpnn_dev_malloc(&V[l], nw * sizeof(T)));
+                TPCHK(hipMemsetAsync(V[l], 0, nw * sizeof(T), s));
+            }
+            if (l < L - 1) {
+                TPCHK(hpnn_dev_malloc(&Hloc[l], (size_t)n[l] * Bp * sizeof(T)));
+                TPCHK(hpnn_dev_malloc(&Hfull[l], (size_t)P * n[l] * Bp * sizeof(T)));
+                TPCHK(hpnn_dev_malloc(&Dloc[l], (size_t)n[l] * Bp * sizeof(T)));
+            }
+            if (l >= 1 && l < L - 1) part_elems = std::max(part_elems, (size_t)Mp[l] * Bp);
+            std::vector<T> tmp(nw, (T)0);
+            for (int j = 0; j < n[l]; j++) {
+                const int g = grow(l, j);
+                if (g >= Ntrue[l]) continue;
+                for (int m = 0; m < Mtrue[l]; m++) tmp[(size_t)j * Mp[l] + m] = (T)ly->weights[(size_t)g * Mtrue[l] + m];
+            }
+            TPCHK(hipMemcpyAsync(W[l], tmp.data(), nw * sizeof(T), hipMemcpyHostToDevice, s));
+            TPCHK(hipStreamSynchronize(s));
+        }
+        TPCHK(hpnn_dev_malloc(&Z, (size_t)Bp * n_out * sizeof(T)));
+        TPCHK(hpnn_dev_malloc(&DL, (size_t)Bp * n_out * sizeof(T)));
+        if (part_elems) TPCHK(hpnn_dev_malloc(&part, part_elems * sizeof(T)));
+        TPCHK(hpnn_dev_malloc(&acc, ACC_BYTES));
+        TPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
+        return TRUE;
+    }
+
+    BOOL upload_momentum(const kernel_ann *k) {
+        if (!k->dw) return TRUE;
+        for (int l = 0; l < L; l++) {
+            if (!V[l]) continue;
+            std::vector<T> tmp((size_t)n[l] * Mp[l], (T)0);
+            for (int j = 0; j < n[l]; j++) {
+                const int g = grow(l, j);
+                if (g >= Ntrue[l]) continue;
+                for (int m = 0; m < Mtrue[l]; m++) tmp[(size_t)j * Mp[l] + m] = (T)k->dw[l][(size_t)g * Mtrue[l] + m];
+            }
+            TPCHK(hipMemcpyAsync(V[l], tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice, s));
+            TPCHK(hipStreamSynchronize(s));
+        }
+        return TRUE;
+    }
+
+#define TPK(call, what)                                                 \
+    do {                                                                \
+        const int rc_ = (call);                                         \
+        if (rc_) {                                                      \
+            NN_ERROR(stderr, "tensor-parallel %s failed (%d)\n", what, rc_); \
+            return FALSE;                                               \
+        }                                                               \
+    } while (0)
+
+    /* one minibatch: Xt = X^T columns of this batch (ldx = row pitch of the uploaded X^T),
+     * Tt [Bp][n_out] targets, nv valid samples */
+    BOOL step(const T *Xt, int ldx, const T *Tt, int nv, double lr, double alpha, bool mom) {
+        auto hin = [&](int l, int *ld) -> const T * {
+            if (l == 0) {
+                *ld = ldx;
+                return Xt;
+            }
+            *ld = Bp;
+            return Hfull[l - 1];
+        };
+        /* forward of the sharded hidden layers */
+        for (int l = 0; l < L - 1; l++) {
+            int ld;
+            const T *A = hin(l, &ld);
+            TPK(hpnn_gemm_fp(F64, W[l], Mp[l], 0, A, ld, 1, Hloc[l], Bp, nullptr, 0, n[l], Bp, Mp[l], HPNN_EPI_ACT, 1,
+                             0, s),
+                "forward GEMM");
+            if (!coll->all_gather(Hloc[l], Hfull[l], (long)n[l] * Bp, s)) return FALSE;
+        }
+        /* replicated output layer */
+        const int o = L - 1;
+        int ldo;
+        const T *Ho = hin(o, &ldo);
+        TPK(hpnn_gemm_fp(F64, Ho, ldo, 1, W[o], Mp[o], 0, Z, n_out, nullptr, 0, Bp, n_out, Mp[o], HPNN_EPI_NONE, 1, 0,
+                         s),
+            "output GEMM");
+        TPK(hpnn_output_fp(F64, Z, n_out, Tt, n_out, DL, n_out, nullptr, 0, nullptr, acc, (unsigned int *)(acc + 1),
+                           Bp, nv, n_out, type, s),
+            "output layer");
+        /* output layer gradient (replicated) and the local rows of the last hidden delta */
+        TPK(hpnn_gemm_fp(F64, DL, n_out, 1, Ho, ldo, 0, slab[o], Mp[o], nullptr, 0, n_out, Mp[o], Bp, HPNN_EPI_NONE,
+                         S[o], (long)n_out * Mp[o], s),
+            "output gradient");
+        if (L >= 2) {
+            const int h = L - 2;
+            TPK(hpnn_gemm_fp(F64, W[o] + (size_t)r * n[h], Mp[o], 1, DL, n_out, 0, Dloc[h], Bp, Hloc[h], Bp, n[h], Bp,
+                             n_out, HPNN_EPI_DACT, 1, 0, s),
+                "delta GEMM");
+        }
+        for (int l = L - 2; l >= 0; l--) {
+            int ld;
+            const T *A = hin(l, &ld);
+            TPK(hpnn_gemm_fp(F64, Dloc[l], Bp, 0, A, ld, 0, slab[l], Mp[l], nullptr, 0, n[l], Mp[l], Bp, HPNN_EPI_NONE,
+                             S[l], (long)n[l] * Mp[l], s),
+                "weight gradient");
+            if (l > 0) {
+                /* this rank's share of every input's delta, summed over ranks for the local rows */
+                TPK(hpnn_gemm_fp(F64, W[l], Mp[l], 1, Dloc[l], Bp, 1, part, Bp, nullptr, 0, Mp[l], Bp, n[l],
+                                 HPNN_EPI_NONE, 1, 0, s),
+                    "partial delta GEMM");
+                if (!coll->reduce_scatter(part, Dloc[l - 1], (long)n[l - 1] * Bp, s)) return FALSE;
+                TPK(hpnn_dact_fp(F64, Dloc[l - 1], Dloc[l - 1], Hloc[l - 1], (long)n[l - 1] * Bp, s), "f' epilogue");
+            }
+        }
+        const double scale = 1.0 / (double)(nv > 0 ? nv : 1);
+        for (int l = 0; l < L; l++)
+            TPK(hpnn_update_fp(F64, W[l], V[l], slab[l], S[l], (long)n[l] * Mp[l], (long)n[l] * Mp[l], lr, alpha, scale,
+                               mom ? 1 : 0, s),
+                "update");
+        return hpnn_debug_check("tensor-parallel step") == 0;
+    }
+#undef TPK
+
+    BOOL read_stats(double *loss, unsigned int *hits) {
+        std::vector<float> h(ACC_BYTES / 4);
+        TPCHK(hipMemcpyAsync(h.data(), acc, ACC_BYTES, hipMemcpyDeviceToHost, s));
+        TPCHK(hipStreamSynchronize(s));
+        double l = 0.0;
+        unsigned int c = 0;
+        for (int i = 0; i < HPNN_STAT_SLOTS; i++) {
+            l += h[(size_t)i * HPNN_STAT_STRIDE];
+            unsigned int u;
+            memcpy(&u, &h[(size_t)i * HPNN_STAT_STRIDE + 1], 4);
+            c += u;
+        }
+        *loss = l;
+        *hits = c;
+        return TRUE;
+    }
+
+    /* this rank's rows -> the host kernel (rows of other ranks untouched) */
+    BOOL download_rows(kernel_ann *k, int rank_rows_of, const T *const *Wsrc, const T *const *Vsrc) {
+        for (int l = 0; l < L; l++) {
+            layer_ann *ly = layer_at(k, l);
+            const int rr = rank_rows_of;
+            const size_t nw = (size_t)n[l] * Mp[l];
+            std::vector<T> tmp(nw);
+            for (int pass = 0; pass < 2; pass++) {
+                const T *src = pass ? (Vsrc ? Vsrc[l] : nullptr) : Wsrc[l];
+                if (!src) continue;
+                DOUBLE *dst = pass ? k->dw[l] : ly->weights;
+                TPCHK(hipMemcpyAsync(tmp.data(), src, nw * sizeof(T), hipMemcpyDeviceToHost, s));
+                TPCHK(hipStreamSynchronize(s));
+                for (int j = 0; j < n[l]; j++) {
+                    const int g = l < L - 1 ? rr * n[l] + j : j;
+                    if (g >= Ntrue[l]) continue;
+                    for (int m = 0; m < Mtrue[l]; m++) dst[(size_t)g * Mtrue[l] + m] = (DOUBLE)tmp[(size_t)j * Mp[l] + m];
+                }
+            }
+        }
+        return TRUE;
+    }
+};
+
+/* X^T and T of the whole sample set on this rank's device: X^T [n_in][cols] with batch b
+ * at columns b*B (cols = n_batches*B + Bp - B ... padded to read Bp columns per batch) */
+template <typename T>
+BOOL upload_xt(const DOUBLE *X, const DOUBLE *Tg, UINT n, int n_in, int n_out, int cols, T **Xt, T **Td,
+               hipStream_t s) {
+    std::vector<T> h((size_t)n_in * cols, (T)0);
+    for (UINT i = 0; i < n; i++)
+        for (int c = 0; c < n_in; c++) h[(size_t)c * cols + i] = (T)X[(size_t)i * n_in + c];
+    TPCHK(hpnn_dev_malloc(Xt, h.size() * sizeof(T)));
+    TPCHK(hipMemcpyAsync(*Xt, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    std::vector<T> t((size_t)cols * n_out, (T)0);
+    for (size_t i = 0; i < (size_t)n * n_out; i++) t[i] = (T)Tg[i];
+    TPCHK(hpnn_dev_malloc(Td, t.size() * sizeof(T)));
+    TPCHK(hipMemcpyAsync(*Td, t.data(), t.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    TPCHK(hipStreamSynchronize(s));
+    return TRUE;
+}
+
+/* the epoch loop of one rank */
+template <typename T>
+BOOL run_rank(TpNet<T> &net, const T *Xt, const T *Td, int cols, UINT n, const hpnn_batched_opts *o, int B,
+              double *ep_loss, unsigned int *ep_hits) {
+    const bool mom = o->train == NN_TRAIN_BPM;
+    const int n_batches = (int)((n + B - 1) / B);
+    for (UINT e = 0; e < o->epochs; e++) {
+        TPCHK(hipMemsetAsync(net.acc, 0, ACC_BYTES, net.s));
+        for (int b = 0; b < n_batches; b++) {
+            const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
+            if (!net.step(Xt + (size_t)b * B, cols, Td + (size_t)b * B * net.n_out, nv, o->lr, o->alpha, mom))
+                return FALSE;
+        }
+        if (!net.read_stats(ep_loss, ep_hits)) return FALSE;
+        if (net.r == 0 && hpnn_metrics_active())
+            hpnn_metrics_epoch("gpu-tp", o->epoch0 + e + 1, *ep_loss / (double)n, *ep_hits, n, 0.0,
+                               (UINT64)n * (e + 1));
+    }
+    TPCHK(hipStreamSynchronize(net.s));
+    return TRUE;
+}
+
+/* P ranks as host threads of this process: loopback (all on device 0, staging-buffer
+ * collectives) or one per GPU (RCCL) */
+template <typename T>
+BOOL train_tp_threads(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, const hpnn_batched_opts *o,
+                      hpnn_batched_stats *st, int P, bool loopback) {
+    const int B = (int)(o->batch ? o->batch : 256);
+    const int n_batches = (int)((n + B - 1) / B);
+    const int cols = n_batches * B;
+    const bool mom = o->train == NN_TRAIN_BPM;
+    std::vector<int> dev(P);
+    std::vector<hipStream_t> str(P);
+    for (int g = 0; g < P; g++) {
+        dev[g] = loopback ? hpnn_rt_device(0) : hpnn_rt_device((UINT)g);
+        str[g] = loopback ? nullptr : hpnn_rt_stream((UINT)g, 0);
+    }
+    HostShared<T> shared;
+    shared.P = P;
+    shared.bar.P = P;
+    std::vector<hpnn_comm *> comms(P, nullptr);
+    std::vector<std::unique_ptr<TpColl<T>>> colls(P);
+    if (!loopback) {
+        if (!hpnn_comm_available() || hpnn_comm_init_all(comms.data(), P, dev.data()) != 0) {
+            NN_ERROR(stderr, "tensor parallelism over %d GPUs needs RCCL\n", P);
+            return FALSE;
+        }
+        for (int g = 0; g < P; g++) colls[g].reset(new RcclColl<T>(comms[g]));
+    } else {
+        for (int g = 0; g < P; g++) colls[g].reset(new HostColl<T>(&shared, g));
+    }
+    std::vector<std::unique_ptr<TpNet<T>>> nets(P);
+    std::vector<T *> Xt(P, nullptr), Td(P, nullptr);
+    std::vector<int> tok(P, 1);
+    std::vector<double> losses(P, 0.0);
+    std::vector<unsigned int> hits(P, 0);
+    if (mom) ann_momentum_init(k);
+    BOOL ok = TRUE;
+    /* setup (serial: allocation sizes of the staging buffer depend on every shard) */
+    for (int g = 0; g < P && ok; g++) {
+        if (hipSetDevice(dev[g]) != hipSuccess) ok = FALSE;
+        if (ok && loopback && hipStreamCreateWithFlags(&str[g], hipStreamNonBlocking) != hipSuccess) ok = FALSE;
+        if (!ok) break;
+        nets[g].reset(new TpNet<T>());
+        ok = nets[g]->init(k, P, g, B, o->type, mom, str[g], colls[g].get());
+        if (ok && mom && o->resume) ok = nets[g]->upload_momentum(k);
+        if (ok) ok = upload_xt<T>(X, Tg, n, (int)k->n_inputs, (int)k->n_outputs, cols + B, &Xt[g], &Td[g], str[g]);
+    }
+    if (ok && loopback) {
+        size_t stage = 0;
+        const TpNet<T> &n0 = *nets[0];
+        for (int l = 0; l < n0.L - 1; l++) {
+            stage = std::max(stage, (size_t)P * n0.n[l] * n0.Bp);                 /* all-gather */
+            if (l + 1 < n0.L - 1) stage = std::max(stage, (size_t)P * n0.Mp[l + 1] * n0.Bp); /* reduce-scatter */
+        }
+        for (int l = 0; l < n0.L; l++) stage = std::max(stage, (size_t)P * n0.n[l] * n0.Mp[l]); /* weights */
+        hipSetDevice(dev[0]);
+        if (hpnn_dev_malloc(&shared.stage, (stage ? stage : 1) * sizeof(T)) != hipSuccess) ok = FALSE;
+    }
+    NN_OUT(stdout, "tensor-parallel batched training: %d ranks (%s, %s), rows of every hidden layer sharded, "
+                   "%d samples per step\n",
+           P, loopback ? "loopback on one GPU" : "RCCL", sizeof(T) == 8 ? "f64" : "f32", B);
+    auto t0 = std::chrono::steady_clock::now();
+    if (ok) {
+        std::vector<std::thread> th;
+        for (int g = 0; g < P; g++)
+            th.emplace_back([&, g]() {
+                if (hipSetDevice(dev[g]) != hipSuccess ||
+                    !run_rank<T>(*nets[g], Xt[g], Td[g], cols + B, n, o, B, &losses[g], &hits[g])) {
+                    tok[g] = 0;
+                    colls[g]->abort();
+                }
+            });
+        for (auto &t : th) t.join();
+        for (int g = 0; g < P; g++) ok = ok && tok[g];
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (ok && !loopback)
+        for (int g = 0; g < P; g++) ok = ok && hpnn_comm_check(comms[g]) == 0;
+    /* every rank's rows -> the host kernel */
+    for (int g = 0; g < P && ok; g++) {
+        hipSetDevice(dev[g]);
+        ok = nets[g]->download_rows(k, g, nets[g]->W, mom ? nets[g]->V : nullptr);
+    }
+    if (ok && st) {
+        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->samples = (UINT64)n * o->epochs;
+        st->epoch_loss = losses[0] / (double)n;
+        st->correct = hits[0];
+        st->last_loss = st->epoch_loss;
+    }
+    for (int g = 0; g < P; g++) {
+        hipSetDevice(dev[g]);
+        nets[g].reset();
+        hpnn_dev_free(Xt[g]);
+        hpnn_dev_free(Td[g]);
+        if (loopback && str[g]) hipStreamDestroy(str[g]);
+        if (comms[g]) hpnn_comm_destroy(comms[g]);
+    }
+    hipSetDevice(hpnn_rt_device(0));
+    return ok;
+}
+
+/* one process per GPU under a launcher (RANK / WORLD_SIZE / LOCAL_RANK): RCCL collectives;
+ * every rank ends with the full weights in its host kernel (all-gather of the rows) */
+template <typename T>
+BOOL train_tp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, const hpnn_batched_opts *o,
+                 hpnn_batched_stats *st) {
+    const int W = hpnn_boot_world(), R = hpnn_boot_rank();
+    const int dev = hpnn_rt_device(0);
+    TPCHK(hipSetDevice(dev));
+    hipStream_t s = hpnn_rt_stream(0, 0);
+    if (!hpnn_comm_available()) {
+        NN_ERROR(stderr, "tensor parallelism across processes needs RCCL\n");
+        return FALSE;
+    }
+    unsigned char id[HPNN_COMM_ID_BYTES] = {0};
+    std::vector<unsigned char> all((size_t)W * HPNN_COMM_ID_BYTES);
+    if (R == 0 && hpnn_comm_unique_id(id) != 0) return FALSE;
+    if (hpnn_boot_allgather(id, sizeof id, all.data()) != 0) return FALSE;
+    hpnn_comm *comm = hpnn_comm_init_rank(all.data(), W, R, dev);
+    if (!comm) return FALSE;
+    RcclColl<T> coll(comm);
+    const int B = (int)(o->batch ? o->batch : 256);
+    const int n_batches = (int)((n + B - 1) / B);
+    const int cols = n_batches * B + B;
+    const bool mom = o->train == NN_TRAIN_BPM;
+    if (mom) ann_momentum_init(k);
+    TpNet<T> net;
+    T *Xt = nullptr, *Td = nullptr;
+    BOOL ok = net.init(k, W, R, B, o->type, mom, s, &coll);
+    if (ok && mom && o->resume) ok = net.upload_momentum(k);
+    if (ok) ok = upload_xt<T>(X, Tg, n, (int)k->n_inputs, (int)k->n_outputs, cols, &Xt, &Td, s);
+    NN_OUT(stdout, "tensor-parallel batched training: %d processes (RCCL, %s), %d samples per step\n", W,
+           sizeof(T) == 8 ? "f64" : "f32", B);
+    double loss = 0.0;
+    unsigned int hits = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    if (ok) ok = run_rank<T>(net, Xt, Td, cols, n, o, B, &loss, &hits);
+    auto t1 = std::chrono::steady_clock::now();
+    if (ok) ok = hpnn_comm_check(comm) == 0;
+    /* all ranks agree before the weights are gathered (a failed rank issues no collective) */
+    int okv = ok ? 1 : 0;
+    std::vector<int> oks(W);
+    if (hpnn_boot_allgather(&okv, sizeof okv, oks.data()) != 0) ok = FALSE;
+    for (int v : oks) ok = ok && v;
+    if (ok) {
+        for (int l = 0; l < net.L && ok; l++) {
+            const long cnt = (long)net.n[l] * net.Mp[l];
+            T *full = nullptr;
+            const int sh = l < net.L - 1 ? W : 1;
+            for (int pass = 0; pass < (mom ? 2 : 1) && ok; pass++) {
+                const T *src = pass ? net.V[l] : net.W[l];
+                ok = hpnn_dev_malloc(&full, (size_t)cnt * sh * sizeof(T)) == hipSuccess;
+                if (ok && sh > 1) ok = coll.gather_rows(src, full, cnt, s);
+                else if (ok) ok = hipMemcpyAsync(full, src, cnt * sizeof(T), hipMemcpyDeviceToDevice, s) == hipSuccess;
+                std::vector<T> h((size_t)cnt * sh);
+                if (ok) ok = hipMemcpyAsync(h.data(), full, h.size() * sizeof(T), hipMemcpyDeviceToHost, s) ==
+                             hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+                hpnn_dev_free(full);
+                full = nullptr;
+                if (!ok) break;
+                layer_ann *ly = layer_at(k, l);
+                DOUBLE *dst = pass ? k->dw[l] : ly->weights;
+                const int rows = sh * net.n[l];
+                for (int g = 0; g < rows && g < net.Ntrue[l]; g++)
+                    for (int m = 0; m < net.Mtrue[l]; m++)
+                        dst[(size_t)g * net.Mtrue[l] + m] = (DOUBLE)h[(size_t)g * net.Mp[l] + m];
+            }
+        }
+    }
+    if (ok && st) {
+        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->samples = (UINT64)n * o->epochs;
+        st->epoch_loss = loss / (double)n;
+        st->correct = hits;
+        st->last_loss = st->epoch_loss;
+    }
+    hipStreamSynchronize(s);
+    hpnn_boot_finish();
+    hpnn_dev_free(Xt);
+    hpnn_dev_free(Td);
+    hpnn_comm_destroy(comm);
+    return ok;
+}
+
+template <typename T>
+BOOL train_tp(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, const hpnn_batched_opts *o,
+              hpnn_batched_stats *st) {
+    if (k->n_hiddens + 1 > 16) return FALSE;
+    hpnn_gpu_sync_host(k);
+    const char *lb = getenv("HPNN_LOOPBACK_RANKS");
+    const int lbr = lb ? atoi(lb) : 0;
+    BOOL ok;
+    if (lbr >= 2) ok = train_tp_threads<T>(k, X, Tg, n, o, st, lbr, true);
+    else if (hpnn_boot_world() > 1) ok = train_tp_mp<T>(k, X, Tg, n, o, st);
+    else if (o->n_gpu > 1) ok = train_tp_threads<T>(k, X, Tg, n, o, st, (int)o->n_gpu, false);
+    else ok = train_tp_threads<T>(k, X, Tg, n, o, st, 1, true);
+    if (ok) hpnn_gpu_mark_host_dirty(k);
+    return ok;
+}
+
+}  // namespace
+
+extern "C" BOOL hpnn_gpu_train_tp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
+                                  hpnn_batched_stats *st) {
+    if (o->dtype == NN_DTYPE_F64) return train_tp<double>(k, X, T, n, o, st);
+    if (o->dtype == NN_DTYPE_F32) return train_tp<float>(k, X, T, n, o, st);
+    NN_ERROR(stderr, "[parallel] tp needs [dtype] f64 or f32 (the BF16 engine is data-parallel only)\n");
+    return FALSE;
+}

@@ -88,6 +88,11 @@ typedef enum {
     NN_DEVICE_GPU = 2,
 } nn_device;
 
+typedef enum {
+    NN_PARALLEL_DP = 0,
+    NN_PARALLEL_TP = 1,
+} nn_parallel;
+
 typedef struct {
     nn_runtime *rr;  /* link to the runtime parameters */
     CHAR *name;
@@ -111,6 +116,9 @@ typedef struct {
     UINT epochs_done;    /* batched epochs completed on this kernel       */
     UINT64 samples_seen; /* training samples processed on this kernel     */
     BOOL resume;         /* start batched training from the saved momentum */
+    /* -- batched multi-GPU layout: [parallel] dp (replicas) | tp (rows of every hidden
+     *    layer sharded over the GPUs / ranks; [dtype] f64 or f32) -- */
+    nn_parallel parallel;
 } nn_def;
 
 #define _NN(a, b) nn_##a##_##b

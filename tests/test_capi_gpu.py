@@ -161,13 +161,15 @@ def test_batched_gpu_tn_update_matches_separate(tmp_path):
 
 
 @pytest.mark.parametrize("net,train,dims,slots", [("SNN", "BPM", (120, [64, 40], 10), 2),
-                                                  ("ANN", "BPM", (70, [48, 200, 33], 7), 3),
+                                                  ("ANN", "BPM", (70, [48, 200, 33], 7), 2),
                                                   ("SNN", "BP", (300, [700], 40), 2)])
 def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots):
     """The online engine with its cooperative grid spread over several slots (one per GPU
     with train_nn -G N; here HPNN_ONLINE_SLOTS virtual slots on the box's one GPU, each its
     own launch on its own stream with its own copy of W, exchanging through fine-grained
     memory at system scope) == the one-device engine and the FP64 CPU engine to 1e-9.
+    (Two slots: the slots' launches must run concurrently, and on one device more
+    streams than hardware queues (GPU_MAX_HW_QUEUES = 4) would serialise them.)
     Every slot owns the rows j with (j mod total workgroups) in its range; the host gathers
     each row from its owner when the kernel is dumped."""
     n_in, hid, n_out = dims
@@ -183,3 +185,43 @@ def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots
     for a, b, c in zip(ks["cpu"], ks["one"], ks["slots"]):
         assert np.abs(c - b).max() < 1e-9, np.abs(c - b).max()
         assert np.abs(c - a).max() < 1e-9, np.abs(c - a).max()
+
+
+@pytest.mark.parametrize("dtype,ranks,dims", [("f64", 2, (100, [48, 37], 7)), ("f64", 3, (64, [50], 9)),
+                                              ("f32", 2, (100, [48, 37], 7)), ("f64", 4, (30, [20, 11, 13], 5))])
+def test_batched_tensor_parallel_matches_single(tmp_path, dtype, ranks, dims):
+    """[parallel] tp (csrc/gpu/tp_engine.cpp): every hidden layer's rows sharded over the
+    ranks (here HPNN_LOOPBACK_RANKS host threads on the box's one GPU, exchanging through a
+    device staging buffer; RCCL on a multi-GPU node), activations all-gathered, partial
+    deltas reduce-scattered with f' applied on the reduced rows, the output layer
+    replicated -> the same training as one GPU: f64 to summation order (1e-12), f32 1e-5.
+    Uneven shards (48 / 37 / 11 / 13 rows over 2-4 ranks) exercise the zero padding."""
+    n_in, hid, n_out = dims
+    res = {}
+    for tag, env, par in (("single", {}, "dp"), ("tp", {"HPNN_LOOPBACK_RANKS": str(ranks)}, "tp")):
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 300, n_in, n_out, True, seed=6)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=n_in, hiddens=hid,
+                           outputs=n_out, train="BPM", sample_dir="./samples", test_dir="./samples",
+                           mode="batched", batch=128, epochs=2, lr=0.05, dtype=dtype, parallel=par)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, extra_env=env)
+        assert ("tensor-parallel batched training" in out) == (tag == "tp"), out[-2000:]
+        res[tag] = (formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"],
+                    formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"])
+    for (w0, ws, wt) in zip(res["single"][0], res["single"][1], res["tp"][1]):
+        ds, dt = ws - w0, wt - w0
+        rel = np.linalg.norm(ds - dt) / (np.linalg.norm(ds) + 1e-30)
+        assert rel < (1e-12 if dtype == "f64" else 1e-5), rel
+
+
+def test_tensor_parallel_refuses_bf16(tmp_path):
+    d = str(tmp_path)
+    _data(os.path.join(d, "samples"), 20, 10, 3, True)
+    formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=10, hiddens=[8],
+                       outputs=3, train="BP", sample_dir="./samples", test_dir="./samples", mode="batched",
+                       batch=16, dtype="bf16", parallel="tp")
+    env = dict(os.environ)
+    env.pop("HPNN_FORCE_CPU", None)
+    r = subprocess.run([os.path.join(BIN, "train_nn"), "nn.conf"], cwd=d, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert "[parallel] tp needs [dtype] f64 or f32" in r.stdout + r.stderr
