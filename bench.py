@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--input", choices=["u8", "float"], default="u8",
                     help="synthetic images as 8-bit pixels (MNIST's format; the net sees pixel/255 in BF16) "
                          "or as uniform floats in [0, 1)")
+    ap.add_argument("--grad-comm", choices=["fp32", "bf16rs"], default="fp32",
+                    help="data-parallel gradient exchange: FP32 all-reduce, or BF16 reduce-scatter + sharded "
+                         "optimizer step + BF16 weight all-gather (half the bytes; per-layer models only)")
     args = ap.parse_args()
 
     # HPNN_BENCH_REHEARSE=1: rehearse the N > 1 path with several ranks on ONE GPU -- gloo
@@ -84,7 +87,8 @@ def main():
         args.batch = batch // world if scaling == "strong" else batch
     m = MLP(sizes, net, batch=args.batch, device=dev, momentum=True, seed=10958,
             init="reference" if args.model == "mnist" else "fast")
-    dp = DataParallel(m, comm="xar" if rehearse and world > 1 else "auto")
+    dp = DataParallel(m, comm="xar" if rehearse and world > 1 else "auto",
+                      grad_comm=args.grad_comm if m.fused_mode is None else "fp32")
     dp.broadcast_parameters()
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -248,6 +252,7 @@ def main():
                 "grad_allreduce": ("none" if not dp.active else
                                    (("xgmi+rccl" if dp.native.h else "xgmi") if dp.native is not None and dp.native.xar else
                                     ("rccl-native" if dp.native is not None else "torch.distributed"))),
+                "grad_exchange": "bf16 reduce-scatter + sharded update + bf16 all-gather" if dp.sharded else "fp32",
                 "steps_per_graph": min(gsteps, args.steps) if use_graph else 0,
             },
             "train_loss_mean": loss_sum / max(1, samples // world),

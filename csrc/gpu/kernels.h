@@ -198,6 +198,8 @@ typedef struct {
 int hpnn_wide2_front(const hpnn_wide2_args *a, hipStream_t stream);
 int hpnn_wide2_ksplit(int Bp, int K0);
 long hpnn_wide2_pbuf_bytes(int Bp);
+/* profiling (HPNN_WIDE_TRACE=1): per-workgroup s_memtime stamps [512][12] */
+int hpnn_wide2_trace(unsigned long long *out);
 /* ---- FP64 / FP32 batched engine (kernels_fp.hip): f64 selects double, else float ----
  * gemm_fp: C[M x N] (ldc) = sum_k A(m, k) B(n, k) with A(m, k) = A[m*lda + k] (ta = 0) or
  * A[k*lda + m] (ta = 1), B(n, k) = B[n*ldb + k] (tb = 0) or B[k*ldb + n] (tb = 1), on the FP64 /

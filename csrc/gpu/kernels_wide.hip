@@ -84,7 +84,12 @@ __device__ __forceinline__ f32x4 ld_sc1(const void *p) {
     return v;
 }
 
-template <int TYPE, bool LABELS, int NS, int KSPLIT>
+/* HPNN_WIDE_TRACE=1 (profiling only): s_memtime stamps of every workgroup's wave 0 at the
+ * phase boundaries, [block][mark]; read back with hpnn_wide2_trace */
+constexpr int TR_BLOCKS = 512, TR_MARKS = 12;
+__device__ unsigned long long g_wide_trace[TR_BLOCKS][TR_MARKS];
+
+template <int TYPE, bool LABELS, int NS, int KSPLIT, bool TRACE = false>
 __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X, int ldx,
                                                     const __bf16 *__restrict__ W0, int K0,
                                                     const __bf16 *__restrict__ W1,
@@ -105,6 +110,13 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     const int tile = KSPLIT == 2 ? (b >> 1) : b, half = KSPLIT == 2 ? (b & 1) : 0;
     const int kbeg = half * NS * 64;
     const size_t row0 = (size_t)tile * TS;
+    auto mark = [&](int i) {
+        if constexpr (TRACE) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (tid == 0 && b < TR_BLOCKS) g_wide_trace[b][i] = t;
+        }
+    };
+    mark(0);
 
     /* ================= phase A: acc = W0[:, slice] X[tile, slice]^T ================= */
     f32x4 acc[2][8];
@@ -114,15 +126,18 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         for (int sf = 0; sf < 8; sf++) acc[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
         /* X: register-staged (every load is the compiler's, so its vmcnt waits are exact):
-         * thread t fetches 32 B of row t/4 per stage, 4 stages ahead, and writes them into
+         * thread t fetches 32 B of row t/4 per stage, 3 stages ahead, and writes them into
          * the other half of a 2 x 16 KiB LDS double buffer one stage ahead of their use.
-         * W0: this wave's 4 fragments per stage straight into registers, 3 stages ahead. */
+         * W0: this wave's 4 fragments per stage straight into registers, 2 stages ahead.
+         * Per stage all 16 X fragments are read before the 32 MFMAs (a scheduling barrier
+         * keeps the compiler from interleaving them 2 by 2, which exposed the LDS latency
+         * on every pair). */
         const int xr_row = tid >> 2, xc0 = (tid & 3) * 2;
         const char *xrow = (const char *)(X + (row0 + xr_row) * ldx + kbeg) + xc0 * 16;
         const __bf16 *wg = W0 + (size_t)(32 * wave + r16) * K0 + kbeg + 8 * q;
         typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-        u32x4 xr[4][2]; /* native vectors: promoted to registers (HIP's uint4 struct was not) */
-        bf16x8 wr[4][2][2];
+        u32x4 xr[3][2]; /* native vectors: promoted to registers (HIP's uint4 struct was not) */
+        bf16x8 wr[3][2][2];
         auto load_x = [&](int s, int slot) {
             xr[slot][0] = *(const u32x4 *)(xrow + (size_t)s * 128);
             xr[slot][1] = *(const u32x4 *)(xrow + (size_t)s * 128 + 16);
@@ -141,36 +156,41 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         };
         auto compute = [&](int wslot, int lslot) {
             const char *img = lds + lslot * STG;
+            bf16x8 bb[2][8];
 #pragma unroll
-            for (int kk = 0; kk < 2; kk++) {
-                bf16x8 bb[8];
+            for (int kk = 0; kk < 2; kk++)
 #pragma unroll
-                for (int sf = 0; sf < 8; sf++) bb[sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
+                for (int sf = 0; sf < 8; sf++) bb[kk][sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++)
 #pragma unroll
                 for (int sf = 0; sf < 8; sf++) {
-                    acc[0][sf] = mfma(wr[wslot][0][kk], bb[sf], acc[0][sf]);
-                    acc[1][sf] = mfma(wr[wslot][1][kk], bb[sf], acc[1][sf]);
+                    acc[0][sf] = mfma(wr[wslot][0][kk], bb[kk][sf], acc[0][sf]);
+                    acc[1][sf] = mfma(wr[wslot][1][kk], bb[kk][sf], acc[1][sf]);
                 }
-            }
         };
-        static_assert(NS % 4 == 0, "stages");
 #pragma unroll
-        for (int s = 0; s < 4; s++) load_x(s, s);
+        for (int s = 0; s < 3; s++) load_x(s, s);
 #pragma unroll
-        for (int s = 0; s < 3; s++) load_w(s, s);
+        for (int s = 0; s < 2; s++) load_w(s, s);
         store_x(0, 0);
         lds_barrier();
+        mark(1);
         /* fully unrolled: every ring index static (register arrays stay in registers) */
 #pragma unroll
         for (int s = 0; s < NS; s++) {
-            if (s + 4 < NS) load_x(s + 4, s & 3);       /* slot of stage s: already in LDS */
-            if (s + 3 < NS) load_w(s + 3, (s + 3) & 3); /* slot of stage s - 1: consumed */
-            compute(s & 3, s & 1);
-            if (s + 1 < NS) store_x((s + 1) & 3, (s + 1) & 1); /* stage s + 1, other buffer */
+            if (s + 3 < NS) load_x(s + 3, s % 3);             /* slot of stage s: already in LDS */
+            if (s + 2 < NS) load_w(s + 2, (s + 2) % 3);       /* slot of stage s - 1: consumed */
+            __builtin_amdgcn_sched_barrier(0);
+            compute(s % 3, s & 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (s + 1 < NS) store_x((s + 1) % 3, (s + 1) & 1); /* stage s + 1, other buffer */
             lds_barrier();
         }
     }
 
+    mark(2);
     int *role = (int *)(lds + OFF_RED + 5 * RED_W * 4);
     /* ================= X: the two K slices of the tile meet ================= */
     if constexpr (KSPLIT == 2) {
@@ -183,6 +203,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mark(3);
             return;
         }
         if (tid == 0) {
@@ -205,11 +226,22 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
+    mark(3);
     /* ================= B: the chain on the tile ================= */
     char *imgH = lds + OFF_H, *imgD2 = lds + OFF_D2;
     float *red_max = (float *)(lds + OFF_RED), *red_den = red_max + RED_W, *red_bt = red_den + RED_W;
     float *red_zt = red_bt + RED_W;
     int *red_it = (int *)(red_zt + RED_W);
+    /* labels of the tile's samples (this lane's 8), issued early */
+    int lab[8];
+#pragma unroll
+    for (int sf = 0; sf < 8; sf++) {
+        lab[sf] = -1;
+        if constexpr (LABELS) {
+            const long s = (long)row0 + 16 * sf + r16;
+            lab[sf] = labels[s < n_valid ? s : (n_valid > 0 ? n_valid - 1 : 0)];
+        }
+    }
     /* layer-1 operand fragments (L2-resident), for the 32 outputs / hidden units of this wave */
     bf16x8 wf[2][8];
 #pragma unroll
@@ -235,6 +267,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         }
     };
     copy_out(imgH, H0out);
+    mark(4);
 
     /* Z^T [o][s] = W1 H0^T: lane holds o = 32w + 16i + 4q + r, s = 16sf + r16 */
     f32x4 z[2][8];
@@ -254,6 +287,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         }
     }
 
+    mark(5);
     /* ---- output layer: per-sample max (and softmax denominator) across the 8 waves ---- */
     float cm[2][4];
 #pragma unroll
@@ -270,7 +304,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         m = rows_max(m);
         if (q == 0) red_max[wave * TS + 16 * sf + r16] = m;
     }
-    __syncthreads();
+    lds_barrier();
     float gmax[8];
 #pragma unroll
     for (int sf = 0; sf < 8; sf++) {
@@ -282,14 +316,11 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     /* hits, on the logits (before the softmax below overwrites z) */
     float my_loss = 0.f;
     unsigned int my_hit = 0;
-    int lab[8];
 #pragma unroll
     for (int sf = 0; sf < 8; sf++) {
         const size_t s = row0 + 16 * sf + r16;
         const bool valid = (long)s < (long)n_valid;
-        lab[sf] = -1;
         if constexpr (LABELS) {
-            lab[sf] = labels[valid ? s : (n_valid > 0 ? n_valid - 1 : 0)];
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -346,7 +377,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
             if (q == 0) red_den[wave * TS + 16 * sf + r16] = d;
         }
     }
-    __syncthreads();
+    lds_barrier();
     const float inv_nout = 1.0f / (float)n_out;
 #pragma unroll
     for (int sf = 0; sf < 8; sf++) {
@@ -412,8 +443,10 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int ks = 0; ks < 8; ks++) wf[i][ks] = *(const bf16x8 *)(W1t + (size_t)(32 * wave + 16 * i + r16) * HW + 32 * ks + 8 * q);
+    mark(6);
     lds_barrier();
     copy_out(imgD2, D2out);
+    mark(7);
 
     /* ---- delta1 [s][h] = (delta2 W1)[s][h] f'(H0): lane holds h = 32w + 16i + 4q + r ---- */
     {
@@ -445,8 +478,10 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
                 *p = o; /* in place: only this lane reads these 8 bytes */
             }
     }
+    mark(8);
     lds_barrier();
     copy_out(imgH, D1out);
+    mark(9);
 
     /* ---- loss / hits ---- */
     my_loss = wave_sum(my_loss);
@@ -458,7 +493,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         sl[wave] = my_loss;
         shh[wave] = my_hit;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
         float s = 0.f;
         unsigned int h = 0;
@@ -469,15 +504,20 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         if (loss_acc) atomicAdd(loss_acc + HPNN_STAT_SLOT(tile), s);
         if (correct) atomicAdd(correct + HPNN_STAT_SLOT(tile), h);
     }
+    mark(10);
 }
 
 template <int TYPE, bool LABELS, int NS, int KSPLIT>
 int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
+    static const bool trace = [] { const char *e = getenv("HPNN_WIDE_TRACE"); return e && e[0] == '1'; }();
     auto kern = wide2_kernel<TYPE, LABELS, NS, KSPLIT>;
-    static bool attr = false;
-    if (!attr) {
+    if constexpr (TYPE == 2 && LABELS && KSPLIT == 2)
+        if (trace) kern = wide2_kernel<TYPE, LABELS, NS, KSPLIT, true>;
+    static bool attr[2] = {false, false};
+    const int ti = kern == wide2_kernel<TYPE, LABELS, NS, KSPLIT> ? 0 : 1;
+    if (!attr[ti]) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
-        attr = true;
+        attr[ti] = true;
     }
     const int n_tiles = a.Bp / TS;
     hipLaunchKernelGGL(kern, dim3(n_tiles * KSPLIT), dim3(512), LDS_TOTAL, stream, (const __bf16 *)a.X, a.ldx,
@@ -524,4 +564,9 @@ extern "C" int hpnn_wide2_front(const hpnn_wide2_args *a, hipStream_t stream) {
     if (ks == 2 && (!a->pbuf || !a->cnt || !a->flag || !a->err)) return -1;
     if (ks == 2) return dispatch_wide<32, 2>(*a, stream);
     return dispatch_wide<64, 1>(*a, stream);
+}
+
+/* HPNN_WIDE_TRACE=1 stamps: out[512][12] shader-clock ticks (wave 0 of each workgroup) */
+extern "C" int hpnn_wide2_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wide_trace), sizeof(g_wide_trace)) == hipSuccess ? 0 : -5;
 }

@@ -171,6 +171,11 @@ PYBIND11_MODULE(_native, m) {
     });
     m.def("wide2_ksplit", [](int Bp, int K0) { return hpnn_wide2_ksplit(Bp, K0); });
     m.def("wide2_pbuf_bytes", [](int Bp) { return hpnn_wide2_pbuf_bytes(Bp); });
+    m.def("wide2_trace", []() {
+        std::vector<unsigned long long> v(512 * 12);
+        check(hpnn_wide2_trace(v.data()), "wide2_trace");
+        return v;
+    });
     m.def("mlp3_tile_grid", [](int Bp, int grid) { return hpnn_mlp3_tile_grid(Bp, grid); });
     m.def("mlp3_tile_trace", []() {
         std::vector<unsigned long long> v(1024 * 12);

@@ -35,7 +35,7 @@ def _worker(rank, world, port, sizes, net, fused, B, steps, q):
     for _ in range(steps):
         dp.train_step(X, labels=L, lr=0.05, alpha=0.2)
     if rank == 0:
-        q.put([w.clone() for w in m.host_weights()])
+        q.put([w.numpy() for w in m.host_weights()])  # by value: no shared-memory fd
     dist.barrier()
     dist.destroy_process_group()
 
@@ -62,6 +62,7 @@ def test_dp_equals_single(sizes, net, fused):
     for _ in range(steps):
         m.train_step(X, labels=Lall, lr=0.05, alpha=0.2)
     for a, b in zip(got, m.host_weights()):
+        a = torch.as_tensor(a)
         assert (a - b).abs().max().item() < 1e-5, (a - b).abs().max().item()
 
 
@@ -87,3 +88,56 @@ def test_split_counts_for_8phase_tn():
         s = MLP._splits_8ph(N, K, B)
         assert s and (N // 256) * (K // 256) * s >= 256 and (B // 64) % s == 0 and (B // 64 // s) % 2 == 0
     assert MLP._splits_8ph(256, 256, 16384) == 0          # 256 splits would leave 1 unit each
+
+
+def _worker_rs(rank, world, port, sizes, B, steps, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    Xall = torch.rand(B * world, sizes[0])
+    Lall = torch.randint(0, sizes[-1], (B * world,), dtype=torch.int32)
+    m = MLP(sizes, "ANN", batch=B, device="cpu", momentum=True, seed=11, fused=False)
+    dp = DataParallel(m, grad_comm=mode)
+    dp.broadcast_parameters()
+    T = torch.full((B * world, sizes[-1]), -1.0)
+    T[torch.arange(B * world), Lall.long()] = 1.0
+    X = m.prepare_input(Xall[rank * B:(rank + 1) * B])
+    for _ in range(steps):
+        dp.train_step(X, T=T[rank * B:(rank + 1) * B], lr=0.05, alpha=0.2)
+    if mode == "bf16rs":
+        assert dp.sharded == {0, 1, 2}  # padded rows (64, 32, 32) split evenly over 2 ranks
+        dp.gather_masters()
+    q.put((rank, [w.numpy() for w in m.host_weights()], [b.float().numpy() for b in m.Wb]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_bf16_reduce_scatter_sharded_update():
+    """grad_comm='bf16rs': BF16 reduce-scatter, each rank steps its rows of the FP32
+    masters, BF16 weights all-gathered -> identical BF16 weights on every rank, and the
+    same training as the FP32 all-reduce up to the BF16 rounding of the gradient sum."""
+    world, B, steps, sizes = 2, 128, 3, [24, 64, 32, 5]
+    res = {}
+    for mode in ("fp32", "bf16rs"):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker_rs, args=(r, world, port, sizes, B, steps, mode, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = {r: ([torch.as_tensor(x) for x in w], [torch.as_tensor(x) for x in b])
+               for r, w, b in (q.get(timeout=120) for _ in procs)}
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+        res[mode] = got
+    rs = res["bf16rs"]
+    for a, b in zip(rs[0][0], rs[1][0]):
+        assert torch.equal(a, b)  # gathered masters identical
+    for a, b in zip(rs[0][1], rs[1][1]):
+        assert torch.equal(a, b)  # BF16 compute weights identical on every rank
+    W0 = MLP(sizes, "ANN", batch=B, device="cpu", seed=11).host_weights()
+    for w0, a, b in zip(W0, rs[0][0], res["fp32"][0][0]):
+        da, db = a - w0, b - w0
+        rel = (da - db).norm() / (db.norm() + 1e-30)
+        assert rel < 2e-2, rel.item()

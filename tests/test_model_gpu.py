@@ -16,8 +16,15 @@ pytestmark = pytest.mark.gpu
     ("ANN", [64, 96, 32], False),
     ("LNN", [40, 64, 8], True),
     ("SNN", [300, 230, 230], True),
+    ("SNN", [4096, 230, 230], True),     # RRUFF shape: the wide-input front ("w")
+    ("ANN", [4096, 4096, 4096], True),   # full-width 4096 x 4096 layer pair (8-phase GEMMs)
 ])
 def test_train_step_matches_oracle(gpu, net_type, sizes, momentum):
+    """3 steps vs FP64 math on the same BF16-rounded inputs and initial weights.  The
+    kernels round activations and deltas to BF16 (8 significant bits, 2^-9 relative per
+    rounding) and the weights to BF16 for every GEMM, with FP32 accumulation; measured
+    relative error of the weight change (Frobenius): 2e-3 .. 6e-3 over these nets, loss
+    sum within 3e-3 -- the bounds below leave ~2x headroom."""
     torch.manual_seed(0)
     B = 256
     m = MLP(sizes, net_type, batch=B, momentum=momentum, seed=7)
@@ -43,9 +50,11 @@ def test_train_step_matches_oracle(gpu, net_type, sizes, momentum):
         dg = got[l] - W0[l]
         dr = W64[l] - W0[l]
         rel = (dg - dr).norm() / (dr.norm() + 1e-30)
-        assert rel < 0.05, (l, rel.item())
+        print(f"{net_type} {sizes} layer {l}: relative error of the weight change {rel.item():.2e}")
+        assert rel < 0.012, (l, rel.item())
     lsum, corr = m.read_stats()
-    assert lsum == pytest.approx(loss_total * B, rel=0.05)
+    print(f"loss sum {lsum:.6g} vs oracle {loss_total * B:.6g}")
+    assert lsum == pytest.approx(loss_total * B, rel=6e-3)
 
 
 def test_predict_matches_forward(gpu):

@@ -32,7 +32,7 @@ def _worker(rank, world, port, sizes, net, B, steps, q):
         tp.train_step(Xp, labels=L, lr=0.05, alpha=0.2)
     w = tp.full_weights()
     if rank == 0:
-        q.put(w)
+        q.put([t.numpy() for t in w])  # by value: no shared-memory fd to outlive the child
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,4 +64,5 @@ def test_tp_equals_single(sizes, net):
     for _ in range(steps):
         m.train_step(Xd, labels=L, lr=0.05, alpha=0.2)
     for a, b in zip(got, m.host_weights()):
+        a = torch.as_tensor(a)
         assert (a - b).abs().max().item() < 1e-4, (a - b).abs().max().item()
