@@ -99,38 +99,51 @@ def test_train_step_fragment_major_matches_tn(gpu):
 
 @pytest.mark.gpu
 def test_gemm_fm_direct_u8_pixels(gpu):
+    """8-bit operand: the kernel multiplies the exact integers (BF16 holds 0..255 exactly)
+    and applies hscale to the FP32 accumulator, so it matches D^T (pixels * hscale) in FP32,
+    not the BF16-rounded pixels / 255"""
     torch.manual_seed(21)
     Bt, N, M, S = 16384, 128, 800, 16
     D = _bf(Bt, N, scale=0.25)
     Hu = torch.randint(0, 256, (Bt, M), device="cuda", dtype=torch.uint8)
     sc = float(torch.tensor(1.0 / 255.0, dtype=torch.float32).item())
-    Hb = (Hu.float() * sc).bfloat16()  # what the kernel converts each byte to
     slab = ops.gemm_fm_direct(ops.to_fragment_major(D), ops.to_fragment_major(Hu), N, M, splits=S, hscale=sc)
-    ref_slab = ops.gemm_fm_direct(ops.to_fragment_major(D), ops.to_fragment_major(Hb), N, M, splits=S)
+    ref_int = ops.gemm_fm_direct(ops.to_fragment_major(D), ops.to_fragment_major(Hu.bfloat16()), N, M, splits=S)
     torch.cuda.synchronize()
-    assert (slab.sum(0) - D.float().t() @ Hb.float()).abs().max().item() < 2e-3
-    assert (slab - ref_slab).abs().max().item() < 1e-4  # same values, 4 vs 8 waves
+    ref = (D.float().t() @ Hu.float()) * sc
+    assert (slab.sum(0) - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+    # the same integer products as the BF16 kernel on the integers, scaled once per slab
+    assert (slab - ref_int * sc).abs().max().item() < 1e-5 * ref_int.abs().max().item() * sc
 
 
 @pytest.mark.gpu
-def test_train_step_u8_pixels_matches_float(gpu):
-    """uint8 pixel input (fragment-major 8-bit G0 operand) == the same pixels given as
-    floats pixel/255 (LDS-staged TN G0): same math, other summation order"""
+@pytest.mark.parametrize("fused", ["x", "t"])
+def test_train_step_u8_pixels_matches_float(gpu, fused):
+    """uint8 pixel input (exact integers, the pixel scale on the FP32 accumulators) vs the
+    same pixels given as floats pixel/255 (rounded to BF16 once at input preparation).  The
+    operands differ by BF16 input rounding (|rel| <= 2^-9 per pixel, unbiased), so after 3
+    steps the weights agree to the accumulated rounding, not bitwise: measured up to 2.2e-3
+    of a layer's largest weight change (layer 1, tile path; the differing inputs flip BF16
+    roundings of H1 downstream), gated at 5e-3."""
     torch.manual_seed(23)
     B = 16384
-    ms = [MLP([784, 128, 64, 10], "SNN", batch=B, seed=3, momentum=True, fused="x") for _ in range(2)]
+    ms = [MLP([784, 128, 64, 10], "SNN", batch=B, seed=3, momentum=True, fused=fused) for _ in range(2)]
+    W0 = [w.clone() for w in ms[0].W32]
     from hpnn_amd.models.mlp import PIXEL_SCALE
     for step in range(3):
         xu = torch.randint(0, 256, (B, 784), dtype=torch.uint8)
         lab = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
         Xa = ms[0].prepare_input(xu)
-        assert ms[0]._fm_input(Xa) is not None and ms[0]._fm_input(Xa).dtype == torch.uint8
         Xb = ms[1].prepare_input(xu.float() * PIXEL_SCALE)
-        assert ms[1]._fm_input(Xb) is None
-        assert torch.equal(Xa, Xb)  # the network sees the same BF16 values
+        if fused == "x":
+            assert ms[0]._fm_input(Xa) is not None and ms[0]._fm_input(Xa).dtype == torch.uint8
+            assert ms[1]._fm_input(Xb) is None
+        else:
+            assert Xa.dtype == torch.uint8 and Xb.dtype == torch.bfloat16
         ms[0].train_step(Xa, labels=lab, lr=0.05, alpha=0.2)
         ms[1].train_step(Xb, labels=lab, lr=0.05, alpha=0.2)
     torch.cuda.synchronize()
     for l in range(3):
-        e = (ms[0].W32[l] - ms[1].W32[l]).abs().max().item()
-        assert e < 1e-5, (l, e)
+        da, db = ms[0].W32[l] - W0[l], ms[1].W32[l] - W0[l]
+        e = (da - db).abs().max().item()
+        assert e < 5e-3 * db.abs().max().item(), (l, e, db.abs().max().item())
