@@ -41,7 +41,9 @@
  *
  * LDS (160 KiB, exactly): H1 [256][128] 64 KiB | X^T stages 2 x 16 KiB, aliased by
  * H2 [256][64] in the chain | delta2 [256][64] 32 KiB | delta3 [256][32] 16 KiB |
- * W1 [64][128] 16 KiB.  All images use the T32 layout of mfma_common.h.
+ * W1 [64][128] 16 KiB.  All images use the T32 layout of mfma_common.h.  (W1 / W1^T operands
+ * straight from the L2 into registers instead of the W1 image measured slower: 62.5-62.8 vs
+ * 60.2-60.7 us per step -- under phase A's streaming an L2 hit costs ~2-3K shader clocks.)
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -86,23 +88,35 @@ __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
-                                                         const __bf16 *__restrict__ W0f,
-                                                         const __bf16 *__restrict__ W1,
-                                                         const __bf16 *__restrict__ W2,
-                                                         const __bf16 *__restrict__ W2t,
-                                                         const int *__restrict__ labels,
-                                                         const float *__restrict__ T, int ldt, float t_hi,
-                                                         float t_lo, __bf16 *__restrict__ D1,
-                                                         float *__restrict__ gslab, float *__restrict__ loss_acc,
-                                                         unsigned int *__restrict__ correct, int n_tiles,
-                                                         int n_valid, int n_out) {
-    constexpr int XN = XU8 ? 1 : 2;       /* 16-byte loads per lane per k-step */
+                                                            const __bf16 *__restrict__ W0f,
+                                                            const __bf16 *__restrict__ W1,
+                                                            const __bf16 *__restrict__ W2,
+                                                            const __bf16 *__restrict__ W2t,
+                                                            const int *__restrict__ labels,
+                                                            const float *__restrict__ T, int ldt, float t_hi,
+                                                            float t_lo, __bf16 *__restrict__ D1,
+                                                            float *__restrict__ gslab, float *__restrict__ loss_acc,
+                                                            unsigned int *__restrict__ correct, int n_tiles,
+                                                            int n_valid, int n_out) {
+    /* 8 waves (a 16-wave workgroup, 128 VGPRs a wave, measured slower: 65.2 vs 60.2-60.7 us
+     * per step, its chain no faster -- the chain is bound by LDS / MFMA throughput, not by
+     * per-wave latency) */
+    constexpr int NW = 8;
     constexpr int CHUNK = XU8 ? 512 : 1024; /* bytes of one 32 x 16 input chunk */
-    constexpr int NCB = 2 * KS;           /* 16-feature blocks per 32-sample row of chunks */
+    constexpr int NCB = 2 * KS;             /* 16-feature blocks per 32-sample row of chunks */
+    /* per k-step the workgroup loads 16 chunks (8 sample rows x 2 feature halves): wave w
+     * takes row w, lane half h = l >> 5 takes feature half h, XB bytes per lane (2 fm lanes) */
+    constexpr int XB = 16 * (XU8 ? 1 : 2); /* bytes per lane per k-step */
+    constexpr int XV = XB / 16;            /* 16-byte vectors per lane */
+    constexpr int SG = NW / 4;           /* phase A: sample groups (waves per neuron group) */
+    constexpr int SPA = TS / SG;         /* phase A: samples per wave */
+    constexpr int STA = SPA / 16;        /* phase A: 16-sample tiles per wave */
+    constexpr int SPC = TS / NW;         /* chain: samples per wave */
+    constexpr int STC = SPC / 16;        /* chain: 16-sample tiles per wave */
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ng = wave & 3, sh = wave >> 2; /* phase A: neurons 32 ng.., samples 128 sh.. */
+    const int ng = wave & 3, sh = wave >> 2; /* phase A: neurons 32 ng.., samples SPA sh.. */
     const int r16 = lane & 15, q = lane >> 4;
     const LaneOff lo = lane_offsets(lane);
     char *imgH1 = lds + OFF_H1, *imgH2 = lds + OFF_H2, *imgD2 = lds + OFF_D2, *imgD3 = lds + OFF_D3;
@@ -115,47 +129,48 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     };
     mark(0);
 
-    /* ---- once per launch: W1 -> LDS image, W2 / W2^T operand fragments -> registers ---- */
+    /* ---- once per launch: W1 -> LDS image ---- */
     {
         constexpr int PIECES = (H1 / 32) * (H2 / 16);
-        for (int p = wave; p < PIECES; p += 8) glds_t32_piece<H2>((const char *)W1, (size_t)H1 * 2, imgW1, p, lane);
+        for (int p = wave; p < PIECES; p += NW) glds_t32_piece<H2>((const char *)W1, (size_t)H1 * 2, imgW1, p, lane);
     }
     /* no wait here: the W1 pieces are this wave's oldest vector-memory ops, so phase A's
      * first counted wait (for X(0)) covers them, and its barriers publish them */
     mark(1);
 
-    f32x4 g1acc[4], g2acc; /* G1: h1 tile = wave, h2 tiles 0..3; G2: h2 tile w&3, o tile w>>2 */
-#pragma unroll
-    for (int i = 0; i < 4; i++) g1acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g2acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    /* the G1 / G2 partial sums of this block's tiles live in its slab between tiles (not in
+     * registers through phase A): stored by the first tile, read-added-stored by later ones;
+     * every element belongs to one lane of one wave */
+    float *const slab = gslab + (size_t)blockIdx.x * SLAB;
     float my_loss = 0.f;
     unsigned int my_hit = 0;
     const int n_ot = n_out > 16 ? 2 : 1;
     const float inv_nout = 1.0f / (float)n_out;
 
     /* X^T stage image: row = feature within the k-step, column = sample of the tile.
-     * This lane converts slots 2i, 2i+1 (i = lane & 31) of chunk (t = wave, cb = 2s + lane/32). */
-    const int xi = lane & 31, xcbh = lane >> 5;
-    const int xg = xi >> 3;
+     * This lane converts fm slots 2i, 2i+1 (i = lane & 31) of chunk (t = wave, cb = 2s + lane/32). */
     int xoff[2];
+    const int xi = lane & 31, xcbh = lane >> 5, xg = xi >> 3;
 #pragma unroll
     for (int e = 0; e < 2; e++) {
         const int row = 16 * xcbh + 2 * (xi & 7) + e;
         xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
     }
+    const char *xbase = (const char *)Xg + ((size_t)wave * NCB + xcbh) * CHUNK + (size_t)xi * XB;
 
-    /* transposed-read addresses of this wave's 8 sample tiles in an X^T stage: sample tile st
-     * sits in 32-column sub-tile 4 sh + st/2, with the T32 chunk swap (lo.tr ^ 32) on odd st;
-     * two bases + immediate offsets (st/2 * 2 KiB, + 256 for rows 4..7, + 16 KiB per stage) */
-    const char *xt_e = lds + OFF_XT + (4 * sh) * (XR * 64) + lo.tr;
-    const char *xt_o = lds + OFF_XT + (4 * sh) * (XR * 64) + (lo.tr ^ 32);
+    /* transposed-read addresses of this wave's STA sample tiles in an X^T stage: sample tile
+     * st sits in 32-column sub-tile (STA/2) sh + st/2, with the T32 chunk swap (lo.tr ^ 32)
+     * on odd st; two bases + immediate offsets */
+    const char *xt_e = lds + OFF_XT + (STA / 2 * sh) * (XR * 64) + lo.tr;
+    const char *xt_o = lds + OFF_XT + (STA / 2 * sh) * (XR * 64) + (lo.tr ^ 32);
 
     for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
-        const char *xbase = (const char *)Xg + ((size_t)(T0 + wave) * NCB + xcbh) * CHUNK + (size_t)xi * (16 * XN);
+        const char *xtile = xbase + (size_t)T0 * NCB * CHUNK;
         const __bf16 *wbase = W0f + ((size_t)(2 * ng) * KS * 64 + lane) * 8;
 
-        uint4 xr[KS][XN];
+        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+        u32x4 xr[KS][XV];
         bf16x8 wr[KS][2];
         auto issue = [&](int s) {
             /* an opaque zero pins the loads to this point of the k-loop: the operands are
@@ -164,7 +179,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             unsigned int z = 0;
             asm volatile("" : "+s"(z));
 #pragma unroll
-            for (int n = 0; n < XN; n++) xr[s][n] = *(const uint4 *)(xbase + z + (size_t)(2 * s) * CHUNK + 16 * n);
+            for (int n = 0; n < XV; n++) xr[s][n] = *(const u32x4 *)(xtile + z + (size_t)(2 * s) * CHUNK + 16 * n);
 #pragma unroll
             for (int i = 0; i < 2; i++) wr[s][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + s) * 512);
         };
@@ -172,8 +187,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             char *img = lds + OFF_XT + (s & 1) * IMG_XT;
             bf16x8 v[2];
             if constexpr (XU8) {
-                v[0] = u8x8_int_bf16(xr[s][0].x, xr[s][0].y);
-                v[1] = u8x8_int_bf16(xr[s][0].z, xr[s][0].w);
+                v[0] = u8x8_int_bf16(xr[s][0][0], xr[s][0][1]);
+                v[1] = u8x8_int_bf16(xr[s][0][2], xr[s][0][3]);
             } else {
                 v[0] = __builtin_bit_cast(bf16x8, xr[s][0]);
                 v[1] = __builtin_bit_cast(bf16x8, xr[s][1]);
@@ -182,11 +197,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             *(bf16x8 *)(img + xoff[1]) = v[1];
         };
 
-        f32x4 acc[2][8];
+        f32x4 acc[2][STA];
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int st = 0; st < 8; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int st = 0; st < STA; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         /* the previous tile's chain read H2 (= the X^T stages) and H1 */
         lds_barrier();
@@ -199,10 +214,10 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
         for (int s = 0; s < KS; s++) {
             if (s + D + 1 < KS) issue(s + D + 1);
-            /* all 8 B fragments first (16 transposed reads in flight), then the 16 MFMAs */
-            bf16x8 b[8];
+            /* all B fragments first (2 STA transposed reads in flight), then the MFMAs */
+            bf16x8 b[STA];
 #pragma unroll
-            for (int st = 0; st < 8; st++) {
+            for (int st = 0; st < STA; st++) {
                 const char *pb = ((st & 1) ? xt_o : xt_e) + (s & 1) * IMG_XT + (st >> 1) * (XR * 64);
                 const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)pb);
                 const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(pb + 256));
@@ -210,7 +225,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 b[st] = __builtin_bit_cast(bf16x8, v);
             }
 #pragma unroll
-            for (int st = 0; st < 8; st++) {
+            for (int st = 0; st < STA; st++) {
                 acc[0][st] = mfma(wr[s][0], b[st], acc[0][st]);
                 acc[1][st] = mfma(wr[s][1], b[st], acc[1][st]);
             }
@@ -222,17 +237,17 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int st = 0; st < 8; st++) {
+            for (int st = 0; st < STA; st++) {
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
-                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, 128 * sh + 16 * st, 32 * ng + 16 * i) = o;
+                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i) = o;
             }
         lds_barrier();
 
         mark(4);
-        /* ================= phase B: back chain on this wave's 32 samples ================= */
-        const int sw = 32 * wave;
+        /* ================= phase B: back chain on this wave's SPC samples ================= */
+        const int sw = SPC * wave;
         /* W2 / W2^T operand fragments (L2-resident), not held through phase A */
         bf16x8 w2f[2][2], w2tf[4]; /* P2: A = W2[o][h2] rows; P3: A = W2^T[h2][o] rows */
 #pragma unroll
@@ -242,10 +257,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 w2f[ot][kk] = *(const bf16x8 *)(W2 + (size_t)(16 * ot + r16) * H2 + 32 * kk + 8 * q);
 #pragma unroll
         for (int ht = 0; ht < 4; ht++) w2tf[ht] = *(const bf16x8 *)(W2t + (size_t)(16 * ht + r16) * NO + 8 * q);
-        int lab[2] = {-1, -1};
-        if constexpr (LABELS) {
+        int lab[STC];
 #pragma unroll
-            for (int st = 0; st < 2; st++) {
+        for (int st = 0; st < STC; st++) {
+            lab[st] = -1;
+            if constexpr (LABELS) {
                 int s = tile * TS + sw + 16 * st + r16;
                 s = s < n_valid ? s : (n_valid > 0 ? n_valid - 1 : 0);
                 lab[st] = labels[s];
@@ -253,7 +269,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         }
         /* P1: H2^T [h2][sample] = f(W1 H1^T) */
 #pragma unroll
-        for (int st = 0; st < 2; st++) {
+        for (int st = 0; st < STC; st++) {
             const int r0 = sw + 16 * st;
             f32x4 a[4];
 #pragma unroll
@@ -276,7 +292,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         wave_lds_fence();
         /* P2: logits, output activation, loss, delta3 -> D3 image */
 #pragma unroll
-        for (int st = 0; st < 2; st++) {
+        for (int st = 0; st < STC; st++) {
             const int r0 = sw + 16 * st;
             const int s = tile * TS + r0 + r16;
             f32x4 z[2];
@@ -298,7 +314,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         wave_lds_fence();
         /* P3: delta2^T [h2][sample] = (W2^T delta3^T) * f'(H2) */
 #pragma unroll
-        for (int st = 0; st < 2; st++) {
+        for (int st = 0; st < STC; st++) {
             const int r0 = sw + 16 * st;
             const bf16x8 b = rd_row<TS>(imgD3, lo, r0, 0);
 #pragma unroll
@@ -316,9 +332,10 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         /* P4: delta1 [sample][h1] = (delta2 W1) * f'(H1) -> HBM, fragment-major:
          * chunk (32-sample row, h1 block) = [g][r][j] = delta1[32 t + 8 g + j][16 hb + r] */
         {
-            __bf16 *chunk0 = D1 + (size_t)(T0 + wave) * (H1 / 16) * 512;
+            __bf16 *chunk0 = D1 + (size_t)(T0 + (sw >> 5)) * (H1 / 16) * 512;
+            const int gb = 2 * ((sw >> 4) & 1);
 #pragma unroll
-            for (int st = 0; st < 2; st++) {
+            for (int st = 0; st < STC; st++) {
                 const int r0 = sw + 16 * st;
                 const bf16x8 d0 = rd_row<TS>(imgD2, lo, r0, 0), d1 = rd_row<TS>(imgD2, lo, r0, 32);
 #pragma unroll
@@ -332,7 +349,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     bf16x4 o;
 #pragma unroll
                     for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)hv[r]));
-                    const int g = 2 * st + (q >> 1);
+                    const int g = gb + 2 * st + (q >> 1);
                     *(bf16x4 *)(chunk0 + (size_t)ht * 512 + (g * 16 + r16) * 8 + 4 * (q & 1)) = o;
                 }
             }
@@ -341,27 +358,60 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         lds_barrier();
 
         /* ================= phase C: G1, G2 over the tile's 256 samples ================= */
+        /* [G1 (H2 x H1) | G2 (NO x H2)] slab.  G1: wave w owns the 2 x 2 output tiles h1 tiles
+         * ha + i x h2 tiles hb + j, D[h1 = 16 (ha + i) + 4q + r][h2 = 16 (hb + j) + r16]; every
+         * operand of the 8 k-steps is read first (64 transposed reads in flight: the chain's
+         * registers are free here), then the 32 MFMAs.  G2: wave w < 8 owns h2 tile w&3 x o
+         * tile w>>2, D[h2 = 16 (w&3) + 4q + r][o = 16 (w>>2) + r16]. */
+        const bool first = tile == (int)blockIdx.x;
+        {
+            const int ha = 2 * (wave & 3), hb = 2 * (wave >> 2);
+            bf16x8 fa[TS / 32][2], fb[TS / 32][2];
 #pragma unroll
-        for (int k = 0; k < TS; k += 32) {
-            const bf16x8 a = rd_tr<TS>(imgH1, lo, k, 16 * wave); /* A[h1][sample] */
+            for (int k = 0; k < TS / 32; k++)
 #pragma unroll
-            for (int t2 = 0; t2 < 4; t2++) g1acc[t2] = mfma(a, rd_tr<TS>(imgD2, lo, k, 16 * t2), g1acc[t2]);
+                for (int i = 0; i < 2; i++) {
+                    fa[k][i] = rd_tr<TS>(imgH1, lo, 32 * k, 16 * (ha + i)); /* A[h1][sample] */
+                    fb[k][i] = rd_tr<TS>(imgD2, lo, 32 * k, 16 * (hb + i)); /* B[sample][h2] */
+                }
+            f32x4 g[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const float *p = slab + (size_t)((hb + j) * 16 + r16) * H1 + (ha + i) * 16 + 4 * q;
+                    g[i][j] = first ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4 *)p;
+                }
+#pragma unroll
+            for (int k = 0; k < TS / 32; k++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) g[i][j] = mfma(fa[k][i], fb[k][j], g[i][j]);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    *(f32x4 *)(slab + (size_t)((hb + j) * 16 + r16) * H1 + (ha + i) * 16 + 4 * q) = g[i][j];
         }
-        if ((wave >> 2) < n_ot) {
+        {
+            float *const g2p = slab + H2 * H1 + (size_t)((wave >> 2) * 16 + r16) * H2 + (wave & 3) * 16 + 4 * q;
+            f32x4 g2acc = first ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4 *)g2p;
+            if ((wave >> 2) < n_ot) {
+                bf16x8 fa[TS / 32], fb[TS / 32];
 #pragma unroll
-            for (int k = 0; k < TS; k += 32)
-                g2acc = mfma(rd_tr<TS>(imgH2, lo, k, 16 * (wave & 3)), rd_tr<TS>(imgD3, lo, k, 16 * (wave >> 2)), g2acc);
+                for (int k = 0; k < TS / 32; k++) {
+                    fa[k] = rd_tr<TS>(imgH2, lo, 32 * k, 16 * (wave & 3));
+                    fb[k] = rd_tr<TS>(imgD3, lo, 32 * k, 16 * (wave >> 2));
+                }
+#pragma unroll
+                for (int k = 0; k < TS / 32; k++) g2acc = mfma(fa[k], fb[k], g2acc);
+            }
+            *(f32x4 *)g2p = g2acc;
         }
     }
 
     mark(9);
-    /* ---- the block's [G1 (H2 x H1) | G2 (NO x H2)] slab ---- */
-    float *slab = gslab + (size_t)blockIdx.x * SLAB;
-#pragma unroll
-    for (int t2 = 0; t2 < 4; t2++) /* D[h1 = 16w + 4q + r][h2 = 16 t2 + r16] */
-        *(f32x4 *)(slab + (size_t)(t2 * 16 + r16) * H1 + wave * 16 + 4 * q) = g1acc[t2];
-    /* D[h2 = 16 (w&3) + 4q + r][o = 16 (w>>2) + r16] */
-    *(f32x4 *)(slab + H2 * H1 + (size_t)((wave >> 2) * 16 + r16) * H2 + (wave & 3) * 16 + 4 * q) = g2acc;
     lds_barrier();
     float *sl = (float *)(lds + OFF_D3);
     unsigned int *shh = (unsigned int *)(lds + OFF_D3 + 64);
@@ -376,7 +426,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     if (tid == 0) {
         float a = 0.f;
         unsigned int h = 0;
-        for (int w = 0; w < 8; w++) {
+        for (int w = 0; w < NW; w++) {
             a += sl[w];
             h += shh[w];
         }
@@ -396,23 +446,23 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
     /* k-steps of loads in flight (HPNN_TILE_D tunes the MNIST-shaped instance) */
     static const int dsel = [] { const char *e = getenv("HPNN_TILE_D"); return e ? atoi(e) : 0; }();
     static const bool trace = [] { const char *e = getenv("HPNN_TILE_TRACE"); return e && e[0] == '1'; }();
-    auto go = [&](auto kern) {
+    auto go = [&](auto kern, int threads) {
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
             attr = true;
         }
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), LDS_TOTAL, stream, Xg, xscale, (const __bf16 *)W0f,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), LDS_TOTAL, stream, Xg, xscale, (const __bf16 *)W0f,
                            (const __bf16 *)W1, (const __bf16 *)W2, (const __bf16 *)W2t, labels, T, ldt, t_hi, t_lo,
                            (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
         return hipGetLastError() == hipSuccess ? grid : -5;
     };
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
-        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5, true>);
-        if (dsel == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>);
-        if (dsel == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 7>);
+        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5, true>, 512);
+        if (dsel == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
+        if (dsel == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 7>, 512);
     }
-    return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5>);
+    return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5>, 512);
 }
 
 template <int KS>
