@@ -172,16 +172,24 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
         u32x4 xr[KS][XV];
         bf16x8 wr[KS][2];
-        auto issue = [&](int s) {
-            /* an opaque zero pins the loads to this point of the k-loop: the operands are
-             * read-only, so the compiler would otherwise hoist every W0 load out of the
-             * tile loop (50 live fragments: spills) */
+        /* X(sx) and W0(sw) in one batch: an opaque zero pins the loads to this point of the
+         * k-loop (the operands are read-only, so the compiler would otherwise hoist every W0
+         * load out of the tile loop: spills).  X(k) is consumed two k-steps before W0(k)
+         * (converted into the LDS stage the B reads of step k come from), so the batch at
+         * step s carries X(s + D + 1) and W0(s + D - 1): step s then waits for exactly one
+         * batch, X(s + 2) for its conversion and W0(s) for its MFMAs. */
+        auto issue = [&](int sx, int sw) {
             unsigned int z = 0;
             asm volatile("" : "+s"(z));
+            if (sx < KS) {
 #pragma unroll
-            for (int n = 0; n < XV; n++) xr[s][n] = *(const u32x4 *)(xtile + z + (size_t)(2 * s) * CHUNK + 16 * n);
+                for (int n = 0; n < XV; n++)
+                    xr[sx][n] = *(const u32x4 *)(xtile + z + (size_t)(2 * sx) * CHUNK + 16 * n);
+            }
+            if (sw >= 0 && sw < KS) {
 #pragma unroll
-            for (int i = 0; i < 2; i++) wr[s][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + s) * 512);
+                for (int i = 0; i < 2; i++) wr[sw][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
+            }
         };
         auto convert = [&](int s) {
             char *img = lds + OFF_XT + (s & 1) * IMG_XT;
@@ -203,19 +211,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
             for (int st = 0; st < STA; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-        /* the previous tile's chain read H2 (= the X^T stages) and H1 */
-        lds_barrier();
-#pragma unroll
-        for (int s = 0; s <= D && s < KS; s++) issue(s);
-        convert(0);
-        lds_barrier();
-        mark(2);
-        /* ================= phase A: H1 = f(X W0^T) ================= */
-#pragma unroll
-        for (int s = 0; s < KS; s++) {
-            if (s + D + 1 < KS) issue(s + D + 1);
-            /* all B fragments first (2 STA transposed reads in flight), then the MFMAs */
-            bf16x8 b[STA];
+        /* B operand fragments of this wave's STA sample tiles from X^T stage s & 1 */
+        auto read_b = [&](int s, bf16x8 (&b)[STA]) {
 #pragma unroll
             for (int st = 0; st < STA; st++) {
                 const char *pb = ((st & 1) ? xt_o : xt_e) + (s & 1) * IMG_XT + (st >> 1) * (XR * 64);
@@ -224,12 +221,35 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 const s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
                 b[st] = __builtin_bit_cast(bf16x8, v);
             }
+        };
+        /* the previous tile's chain read H2 (= the X^T stages) and H1 */
+        lds_barrier();
+#pragma unroll
+        for (int s = 0; s <= D && s < KS; s++) issue(s, s - 2);
+        convert(0);
+        if (KS > 1) convert(1);
+        lds_barrier();
+        bf16x8 bb[2][STA]; /* B fragments of k-step s in bb[s & 1], read one k-step ahead */
+        read_b(0, bb[0]);
+        lds_barrier(); /* every wave's stage-0 reads are done before convert(2) refills it */
+        mark(2);
+        /* ================= phase A: H1 = f(X W0^T) =================
+         * k-step s: the B reads of step s + 1 (stage (s+1) & 1, filled at step s - 1) go out
+         * before the MFMAs of step s, so their LDS latency hides behind them; then X(s + 2)
+         * is converted into stage s & 1 (its step-s reads finished before the last barrier)
+         * and one barrier publishes it and retires the step-(s+1) reads. */
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            issue(s + D + 1, s + D - 1);
+            if (s + 1 < KS) read_b(s + 1, bb[(s + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int st = 0; st < STA; st++) {
-                acc[0][st] = mfma(wr[s][0], b[st], acc[0][st]);
-                acc[1][st] = mfma(wr[s][1], b[st], acc[1][st]);
+                acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
+                acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
             }
-            if (s + 1 < KS) convert(s + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (s + 2 < KS) convert(s + 2);
             lds_barrier();
         }
         mark(3);
@@ -457,12 +477,14 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
                            (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
         return hipGetLastError() == hipSuccess ? grid : -5;
     };
+    /* D = 3 k-steps of loads in flight: 58.7 us per MNIST step vs 59.6-59.7 at D = 4 (B reads
+     * one k-step ahead; the deeper ring costs the registers the B prefetch needs) */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
-        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5, true>, 512);
-        if (dsel == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
-        if (dsel == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 7>, 512);
+        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+        if (dsel == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 4>, 512);
+        if (dsel == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2>, 512);
     }
-    return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 5>, 512);
+    return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }
 
 template <int KS>
