@@ -183,7 +183,9 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
                 : launch_fm<__VA_ARGS__, false>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)
     if (M % 160 == 0 && N % 128 == 0) {
         /* 8-bit H: 8 waves (two k-interleaved groups) hide the byte -> bf16 conversion
-         * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves */
+         * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves.
+         * Round 3, in the MNIST step (tile front): 59.8-59.9 us per step with this one vs
+         * 60.0 with 2 k-steps in flight, 62.3 / 61.4 with 4 waves and 2 / 3 in flight. */
         if (h_u8) { HPNN_FM(5, 4, 1, 2); }
         HPNN_FM(5, 4, 2, 1);
     }
