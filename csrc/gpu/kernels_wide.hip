@@ -15,21 +15,19 @@
  * its tile (the output layer needs it):
  *
  *  A  acc[256 x 128] = W0[:, slice] X[tile, slice]^T.  Wave w owns neurons 32w..32w+31
- *     for all 128 samples (16 MFMA 16x16x32 per 32 features, 64 accumulator registers):
- *     each W0 element is read once per workgroup, straight from the L2 into registers
- *     (the XCD's workgroups share a K slice: tile = block / 2, slice = block % 2, and
- *     blocks b, b + 8 share an XCD).  The X slice is register-staged, 4 stages of 64
- *     features ahead (32 B per thread per stage, whole 128-B rows per 4 threads), into a
- *     2 x 16 KiB LDS double buffer read back conflict-free with ds_read_b128; one barrier
- *     per stage.  (An LDS-DMA ring measured slower here: the compiler cannot count the
- *     DMA in its vmcnt waits for the W0 register loads, which then drained the ring.)
- *  X  KSPLIT = 2: the first of the two workgroups of a tile to finish (a self-resetting
- *     atomicInc per tile) hands its FP32 partial over through memory with write-through
- *     (sc1) stores and an sc1 flag, and exits; the second adds it (a + b == b + a: the
- *     result does not depend on which finished first) and runs the chain.  The second
- *     only waits for a workgroup that is already past its last dependency, so nothing
- *     relies on co-residency.  (MI355X_MICROARCH.md, "Valid forms", first sc1 row.)
- *  B  chain, 8 waves on the tile, images in LDS (T32 layout of mfma_common.h):
+ *     for all 128 samples (16 MFMA 16x16x32 per 32 features, 64 accumulator registers).
+ *     Both operands stream by LDS-DMA into a 3-deep ring of 64-feature stages (X 16 KiB +
+ *     W0 32 KiB a stage, 144 KiB, aliased by the chain's images); all vmcnt waits are the
+ *     kernel's own (no compiler-visible loads in the loop); fragments of stage s + 1 are
+ *     read while the MFMAs of stage s run; one barrier per stage (the XCD's workgroups
+ *     share a K slice: tile = block / 2, slice = block % 2, and blocks b, b + 8 share an
+ *     XCD).
+ *  X  KSPLIT = 2: the two workgroups of a tile exchange halves of their FP32 partials
+ *     (write-through sc1 stores, a monotonic per-tile ticket counter, sc1 polls; see the
+ *     code) and each runs the chain on 64 of the tile's samples, so every CU works through
+ *     the chain.  (MI355X_MICROARCH.md, "Valid forms", agent-scope atomic-add row.)
+ *  B  chain, 8 waves on the workgroup's 64 (KSPLIT = 2) or 128 samples, images in LDS
+ *     (T32 layout of mfma_common.h):
  *     H0 = f(acc) -> LDS (and HBM, for the layer-1 weight gradient);
  *     Z = H0 W1^T, wave w owning outputs 32w..; softmax / sigmoid / linear with the
  *     per-sample max and denominator combined across the 8 waves through LDS; loss,
@@ -42,7 +40,7 @@
  * gradients and updates that follow are unchanged): H0, delta2, delta1; loss / hits into
  * the HPNN_STAT_SLOT slots.
  *
- * LDS: phase A double buffer 2 x 16 KiB (aliased by the chain) | chain: H0 / delta1 image 64 KiB,
+ * LDS: phase A ring 3 x 48 KiB (aliased by the chain) | chain: H0 / delta1 image 64 KiB,
  * delta2 image 64 KiB, cross-wave reduction words 20 KiB.
  */
 #include <hip/hip_runtime.h>
@@ -62,12 +60,10 @@ namespace {
 
 constexpr int TS = 128;                /* samples per tile */
 constexpr int HW = 256;                /* hidden / output width (padded) */
-constexpr int STG = TS * 64 * 2;       /* one 64-feature stage of X: 16 KiB */
 constexpr int IMG = TS * HW * 2;       /* [128][256] bf16 image: 64 KiB */
 constexpr int OFF_H = 0, OFF_D2 = IMG, OFF_RED = 2 * IMG;
 constexpr int RED_W = 8 * TS;          /* floats per reduction array ([wave][sample]) */
 constexpr int LDS_TOTAL = OFF_RED + 5 * RED_W * 4 + 16;
-static_assert(2 * STG <= OFF_RED, "the X double buffer aliases the chain images");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
 constexpr unsigned long long XCH_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
@@ -100,7 +96,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
                                                     f32x4 *__restrict__ pbuf, unsigned int *cnt,
                                                     unsigned int *flag, unsigned int *err,
                                                     float *__restrict__ loss_acc, unsigned int *__restrict__ correct,
-                                                    int n_valid, int n_out) {
+                                                    int n_valid, int n_out, int abl) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -108,8 +104,11 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     const LaneOff lo = lane_offsets(lane);
     const int b = blockIdx.x;
     const int tile = KSPLIT == 2 ? (b >> 1) : b, half = KSPLIT == 2 ? (b & 1) : 0;
-    const int kbeg = half * NS * 64;
+    const int kbeg = half * NS * 64; /* NS 64-feature stages per workgroup */
     const size_t row0 = (size_t)tile * TS;
+    constexpr int SC = KSPLIT == 2 ? TS / 2 : TS; /* chain samples per workgroup */
+    constexpr int SFC = SC / 16;
+    const size_t crow0 = row0 + (size_t)half * SC;
     auto mark = [&](int i) {
         if constexpr (TRACE) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -125,91 +124,118 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 #pragma unroll
         for (int sf = 0; sf < 8; sf++) acc[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-        /* X: register-staged (every load is the compiler's, so its vmcnt waits are exact):
-         * thread t fetches 32 B of row t/4 per stage, 3 stages ahead, and writes them into
-         * the other half of a 2 x 16 KiB LDS double buffer one stage ahead of their use.
-         * W0: this wave's 4 fragments per stage straight into registers, 2 stages ahead.
-         * Per stage all 16 X fragments are read before the 32 MFMAs (a scheduling barrier
-         * keeps the compiler from interleaving them 2 by 2, which exposed the LDS latency
-         * on every pair). */
-        const int xr_row = tid >> 2, xc0 = (tid & 3) * 2;
-        const char *xrow = (const char *)(X + (row0 + xr_row) * ldx + kbeg) + xc0 * 16;
-        const __bf16 *wg = W0 + (size_t)(32 * wave + r16) * K0 + kbeg + 8 * q;
-        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-        u32x4 xr[3][2]; /* native vectors: promoted to registers (HIP's uint4 struct was not) */
-        bf16x8 wr[3][2][2];
-        auto load_x = [&](int s, int slot) {
-            xr[slot][0] = *(const u32x4 *)(xrow + (size_t)s * 128);
-            xr[slot][1] = *(const u32x4 *)(xrow + (size_t)s * 128 + 16);
+        /* Both operands by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a RING-deep
+         * ring of 64-feature stages: X [128 samples][64] (16 KiB) and W0 [256 neurons][64]
+         * (32 KiB) as 128-byte-row images (every DMA piece is 8 whole cache lines; x_frag
+         * row reads conflict-free).  Stage s: 48 one-KiB pieces, 6 per wave.  In the middle of
+         * stage s each wave waits (counted vmcnt) for its own pieces of stage s + 1 and passes
+         * one barrier (every wave's pieces landed; every wave's reads of stage s retired), then
+         * refills stage s's slot with stage s + RING; fragment reads run one 32-feature half
+         * ahead of their 16 MFMAs.  All vmcnt waits are the kernel's own: no compiler-visible
+         * loads in the loop. */
+        constexpr int SX = TS * 128, STG2 = SX + HW * 128, RING = 3, PW = (TS / 8 + HW / 8) / 8;
+        static_assert(RING * STG2 <= LDS_TOTAL, "phase-A ring fits the chain's LDS");
+        const char *xg = (const char *)(X + (row0 * ldx + kbeg));
+        const char *wg = (const char *)(W0 + kbeg);
+        auto issue = [&](int st) {
+            char *img = lds + (st % RING) * STG2;
+#pragma unroll
+            for (int j = 0; j < PW; j++) {
+                const int p = PW * wave + j; /* wave-uniform */
+                if (p < TS / 8) glds_x_piece<TS, 1>(xg + (size_t)st * 128, (size_t)ldx * 2, img, p, lane);
+                else glds_x_piece<HW, 1>(wg + (size_t)st * 128, (size_t)K0 * 2, img + SX, p - TS / 8, lane);
+            }
         };
-        auto load_w = [&](int s, int slot) {
+        /* fragments of one 32-feature half of a stage per register set: (stage, kk) goes to set
+         * kk, read one half-stage ahead of its MFMAs */
+        bf16x8 fa[2][2], fb[2][8];
+        auto read = [&](int st, int kk) {
+            const char *img = lds + (st % RING) * STG2;
 #pragma unroll
-            for (int i = 0; i < 2; i++)
+            for (int i = 0; i < 2; i++) fa[kk][i] = x_frag<HW, 1>(img + SX, 32 * wave + 16 * i, kk, lane);
 #pragma unroll
-                for (int kk = 0; kk < 2; kk++)
-                    wr[slot][i][kk] = *(const bf16x8 *)(wg + (size_t)i * 16 * K0 + (size_t)s * 64 + 32 * kk);
+            for (int sf = 0; sf < 8; sf++) fb[kk][sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
         };
-        auto store_x = [&](int slot, int lslot) {
-            char *img = lds + lslot * STG;
-            *(u32x4 *)(img + w128_off(xr_row, xc0)) = xr[slot][0];
-            *(u32x4 *)(img + w128_off(xr_row, xc0 + 1)) = xr[slot][1];
-        };
-        auto compute = [&](int wslot, int lslot) {
-            const char *img = lds + lslot * STG;
-            bf16x8 bb[2][8];
-#pragma unroll
-            for (int kk = 0; kk < 2; kk++)
-#pragma unroll
-                for (int sf = 0; sf < 8; sf++) bb[kk][sf] = x_frag<TS, 1>(img, 16 * sf, kk, lane);
+        auto mma = [&](int kk) {
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int kk = 0; kk < 2; kk++)
-#pragma unroll
-                for (int sf = 0; sf < 8; sf++) {
-                    acc[0][sf] = mfma(wr[wslot][0][kk], bb[kk][sf], acc[0][sf]);
-                    acc[1][sf] = mfma(wr[wslot][1][kk], bb[kk][sf], acc[1][sf]);
-                }
+            for (int sf = 0; sf < 8; sf++) {
+                acc[0][sf] = mfma(fa[kk][0], fb[kk][sf], acc[0][sf]);
+                acc[1][sf] = mfma(fa[kk][1], fb[kk][sf], acc[1][sf]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         };
+        auto wait_stages = [&](int n) { /* n = stages issued after the one waited for */
+            if (n <= 0) wait_vm<0>();
+            else if (n == 1) wait_vm<PW>();
+            else wait_vm<2 * PW>();
+        };
+        if (abl != 2 && abl < 3) {
 #pragma unroll
-        for (int s = 0; s < 3; s++) load_x(s, s);
-#pragma unroll
-        for (int s = 0; s < 2; s++) load_w(s, s);
-        store_x(0, 0);
+        for (int st = 0; st < RING && st < NS; st++) issue(st);
+        wait_stages((RING < NS ? RING : NS) - 1);
         lds_barrier();
+        read(0, 0);
         mark(1);
-        /* fully unrolled: every ring index static (register arrays stay in registers) */
 #pragma unroll
-        for (int s = 0; s < NS; s++) {
-            if (s + 3 < NS) load_x(s + 3, s % 3);             /* slot of stage s: already in LDS */
-            if (s + 2 < NS) load_w(s + 2, (s + 2) % 3);       /* slot of stage s - 1: consumed */
-            __builtin_amdgcn_sched_barrier(0);
-            compute(s % 3, s & 1);
-            __builtin_amdgcn_sched_barrier(0);
-            if (s + 1 < NS) store_x((s + 1) % 3, (s + 1) & 1); /* stage s + 1, other buffer */
-            lds_barrier();
+        for (int st = 0; st < NS; st++) {
+            read(st, 1);
+            mma(0);
+            if (st + 1 < NS) {
+                const int last = st + RING - 1 < NS - 1 ? st + RING - 1 : NS - 1; /* last stage issued */
+                wait_stages(last - (st + 1));
+                lds_barrier(); /* stage st + 1 landed everywhere; every read of stage st retired */
+                if (st + RING < NS) issue(st + RING);
+                read(st + 1, 0);
+            }
+            mma(1);
         }
+        }
+    }
+    if (abl == 1) { /* profiling ablation: phase A only */
+        if (acc[0][0][0] == 12345.f) loss_acc[0] = acc[1][7][3];
+        return;
     }
 
     mark(2);
-    int *role = (int *)(lds + OFF_RED + 5 * RED_W * 4);
-    /* ================= X: the two K slices of the tile meet ================= */
+    /* ================= X: the two K slices of the tile meet =================
+     * KSPLIT = 2: the chain is split too -- workgroup h of the tile keeps samples
+     * [64 h, 64 h + 64) and hands the partner its partial sums of the other 64 (64 KiB,
+     * write-through sc1 stores, drained, then one agent-scope ticket add per workgroup);
+     * it waits for the partner's ticket (sc1 polls of the monotonic per-tile counter: launch
+     * k's tickets are 2k and 2k + 1, both arrived once it reads >= 2k + 2) and adds the
+     * partner's half (a + b == b + a: the sums do not depend on arrival order).  Both
+     * workgroups of a tile are resident at once (one per CU, grid = tiles x 2 <= CUs; every
+     * wait bounded, a timeout sets *err).  (A one-way hand-over to a single finisher left
+     * half the CUs idle through the whole chain: 35 vs ~20 us.) */
+    f32x4 cacc[2][SFC];
     if constexpr (KSPLIT == 2) {
-        if (tid == 0) *role = (int)atomicInc(cnt + tile, 1u); /* 0: first, 1: second (and reset) */
-        __syncthreads();
-        f32x4 *pb = pbuf + ((size_t)tile * 8 + wave) * 16 * 64 + lane;
-        if (*role == 0) {
+        f32x4 *pout = pbuf + (((size_t)tile * 2 + half) * 8 + wave) * 8 * 64 + lane;
+        const f32x4 *pin = pbuf + (((size_t)tile * 2 + (half ^ 1)) * 8 + wave) * 8 * 64 + lane;
+        if (half == 0) {
 #pragma unroll
-            for (int e = 0; e < 16; e++) st_sc1(pb + e * 64, acc[e >> 3][e & 7]);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mark(3);
-            return;
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    st_sc1(pout + (i * 4 + j) * 64, acc[i][4 + j]);
+                    cacc[i][j] = acc[i][j];
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    st_sc1(pout + (i * 4 + j) * 64, acc[i][j]);
+                    cacc[i][j] = acc[i][4 + j];
+                }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (tid == 0) {
+            const unsigned int want = (atomicAdd(cnt + tile, 1u) | 1u) + 1u;
             const unsigned long long t0 = wall_clock64();
-            while (__hip_atomic_load((gu32 *)flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-                __builtin_amdgcn_s_sleep(2);
+            while ((int)(__hip_atomic_load((gu32 *)cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+                __builtin_amdgcn_s_sleep(1);
                 if (wall_clock64() - t0 > XCH_TIMEOUT) {
                     __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
@@ -217,28 +243,35 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
             }
         }
         __syncthreads();
-        f32x4 v[16];
+        f32x4 v[8];
 #pragma unroll
-        for (int e = 0; e < 16; e++) v[e] = ld_sc1(pb + e * 64);
+        for (int e = 0; e < 8; e++) v[e] = ld_sc1(pin + e * 64);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int e = 0; e < 16; e++) acc[e >> 3][e & 7] += v[e];
-        if (tid == 0) __hip_atomic_store((gu32 *)flag + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) cacc[i][j] += v[i * 4 + j];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < SFC; j++) cacc[i][j] = acc[i][j];
     }
 
     mark(3);
+    if (abl == 3) return; /* profiling ablation: stop after mark 3 */
     /* ================= B: the chain on the tile ================= */
     char *imgH = lds + OFF_H, *imgD2 = lds + OFF_D2;
     float *red_max = (float *)(lds + OFF_RED), *red_den = red_max + RED_W, *red_bt = red_den + RED_W;
     float *red_zt = red_bt + RED_W;
     int *red_it = (int *)(red_zt + RED_W);
     /* labels of the tile's samples (this lane's 8), issued early */
-    int lab[8];
+    int lab[SFC];
 #pragma unroll
-    for (int sf = 0; sf < 8; sf++) {
+    for (int sf = 0; sf < SFC; sf++) {
         lab[sf] = -1;
         if constexpr (LABELS) {
-            const long s = (long)row0 + 16 * sf + r16;
+            const long s = (long)crow0 + 16 * sf + r16;
             lab[sf] = labels[s < n_valid ? s : (n_valid > 0 ? n_valid - 1 : 0)];
         }
     }
@@ -252,42 +285,51 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int sf = 0; sf < 8; sf++) {
+        for (int sf = 0; sf < SFC; sf++) {
             bf16x4 o;
 #pragma unroll
-            for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][sf][r]);
-            *(bf16x4 *)wr_ptr<TS>(imgH, lo, 16 * sf, 32 * wave + 16 * i) = o;
+            for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(cacc[i][sf][r]);
+            *(bf16x4 *)wr_ptr<SC>(imgH, lo, 16 * sf, 32 * wave + 16 * i) = o;
         }
     lds_barrier();
     auto copy_out = [&](const char *img, __bf16 *out) {
 #pragma unroll
-        for (int it = 0; it < 8; it++) {
+        for (int it = 0; it < SC / 16; it++) {
             const int idx = tid + 512 * it, r = idx >> 5, c = (idx & 31) * 8;
-            *(uint4 *)(out + (row0 + r) * HW + c) = *(const uint4 *)(img + t32<TS>(r, c));
+            *(uint4 *)(out + (crow0 + r) * HW + c) = *(const uint4 *)(img + t32<SC>(r, c));
         }
     };
     copy_out(imgH, H0out);
     mark(4);
+    if (abl == 4) return; /* profiling ablation: stop after mark 4 */
 
     /* Z^T [o][s] = W1 H0^T: lane holds o = 32w + 16i + 4q + r, s = 16sf + r16 */
-    f32x4 z[2][8];
+    f32x4 z[2][SFC];
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int sf = 0; sf < 8; sf++) z[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sf = 0; sf < SFC; sf++) z[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 8; ks++) {
-        bf16x8 bb[8];
+        bf16x8 bb[SFC];
 #pragma unroll
-        for (int sf = 0; sf < 8; sf++) bb[sf] = rd_row<TS>(imgH, lo, 16 * sf, 32 * ks);
+        for (int sf = 0; sf < SFC; sf++) bb[sf] = rd_row<SC>(imgH, lo, 16 * sf, 32 * ks);
 #pragma unroll
-        for (int sf = 0; sf < 8; sf++) {
+        for (int sf = 0; sf < SFC; sf++) {
             z[0][sf] = mfma(wf[0][ks], bb[sf], z[0][sf]);
             z[1][sf] = mfma(wf[1][ks], bb[sf], z[1][sf]);
         }
     }
 
+    /* W1^T fragments for delta1 (L2-resident), issued as soon as the W1 fragments are dead:
+     * the output layer hides their L2 latency */
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) wf[i][ks] = *(const bf16x8 *)(W1t + (size_t)(32 * wave + 16 * i + r16) * HW + 32 * ks + 8 * q);
+
     mark(5);
+    if (abl == 5) return; /* profiling ablation: stop after mark 5 */
     /* ---- output layer: per-sample max (and softmax denominator) across the 8 waves ---- */
     float cm[2][4];
 #pragma unroll
@@ -295,7 +337,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 #pragma unroll
         for (int r = 0; r < 4; r++) cm[i][r] = (32 * wave + 16 * i + 4 * q + r < n_out) ? 1.f : 0.f;
 #pragma unroll
-    for (int sf = 0; sf < 8; sf++) {
+    for (int sf = 0; sf < SFC; sf++) {
         float m = -INFINITY;
 #pragma unroll
         for (int i = 0; i < 2; i++)
@@ -305,9 +347,9 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         if (q == 0) red_max[wave * TS + 16 * sf + r16] = m;
     }
     lds_barrier();
-    float gmax[8];
+    float gmax[SFC];
 #pragma unroll
-    for (int sf = 0; sf < 8; sf++) {
+    for (int sf = 0; sf < SFC; sf++) {
         float m = -INFINITY;
 #pragma unroll
         for (int w = 0; w < 8; w++) m = fmaxf(m, red_max[w * TS + 16 * sf + r16]);
@@ -317,8 +359,8 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     float my_loss = 0.f;
     unsigned int my_hit = 0;
 #pragma unroll
-    for (int sf = 0; sf < 8; sf++) {
-        const size_t s = row0 + 16 * sf + r16;
+    for (int sf = 0; sf < SFC; sf++) {
+        const size_t s = crow0 + 16 * sf + r16;
         const bool valid = (long)s < (long)n_valid;
         if constexpr (LABELS) {
 #pragma unroll
@@ -360,10 +402,10 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
             }
         }
     }
-    float inv[8];
+    float inv[SFC];
     if constexpr (TYPE == 2) {
 #pragma unroll
-        for (int sf = 0; sf < 8; sf++) {
+        for (int sf = 0; sf < SFC; sf++) {
             float d = 0.f;
 #pragma unroll
             for (int i = 0; i < 2; i++)
@@ -380,8 +422,8 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     lds_barrier();
     const float inv_nout = 1.0f / (float)n_out;
 #pragma unroll
-    for (int sf = 0; sf < 8; sf++) {
-        const size_t s = row0 + 16 * sf + r16;
+    for (int sf = 0; sf < SFC; sf++) {
+        const size_t s = crow0 + 16 * sf + r16;
         const bool valid = (long)s < (long)n_valid;
         if constexpr (TYPE == 2) {
             float d = 0.f;
@@ -417,7 +459,7 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
                 }
                 dv[r] = (__bf16)d;
             }
-            *(bf16x4 *)wr_ptr<TS>(imgD2, lo, 16 * sf, 32 * wave + 16 * i) = dv;
+            *(bf16x4 *)wr_ptr<SC>(imgD2, lo, 16 * sf, 32 * wave + 16 * i) = dv;
         }
         if (valid) my_loss += (TYPE == 2) ? -l * inv_nout : 0.5f * l;
         if constexpr (!LABELS) {
@@ -438,11 +480,6 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
             }
         }
     }
-    /* W1^T fragments for delta1 (L2-resident) */
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int ks = 0; ks < 8; ks++) wf[i][ks] = *(const bf16x8 *)(W1t + (size_t)(32 * wave + 16 * i + r16) * HW + 32 * ks + 8 * q);
     mark(6);
     lds_barrier();
     copy_out(imgD2, D2out);
@@ -450,18 +487,18 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 
     /* ---- delta1 [s][h] = (delta2 W1)[s][h] f'(H0): lane holds h = 32w + 16i + 4q + r ---- */
     {
-        f32x4 a[2][8];
+        f32x4 a[2][SFC];
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int sf = 0; sf < 8; sf++) a[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int sf = 0; sf < SFC; sf++) a[i][sf] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 8; ks++) {
-            bf16x8 bb[8];
+            bf16x8 bb[SFC];
 #pragma unroll
-            for (int sf = 0; sf < 8; sf++) bb[sf] = rd_row<TS>(imgD2, lo, 16 * sf, 32 * ks);
+            for (int sf = 0; sf < SFC; sf++) bb[sf] = rd_row<SC>(imgD2, lo, 16 * sf, 32 * ks);
 #pragma unroll
-            for (int sf = 0; sf < 8; sf++) {
+            for (int sf = 0; sf < SFC; sf++) {
                 a[0][sf] = mfma(wf[0][ks], bb[sf], a[0][sf]);
                 a[1][sf] = mfma(wf[1][ks], bb[sf], a[1][sf]);
             }
@@ -469,8 +506,8 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int sf = 0; sf < 8; sf++) {
-                bf16x4 *p = (bf16x4 *)wr_ptr<TS>(imgH, lo, 16 * sf, 32 * wave + 16 * i);
+            for (int sf = 0; sf < SFC; sf++) {
+                bf16x4 *p = (bf16x4 *)wr_ptr<SC>(imgH, lo, 16 * sf, 32 * wave + 16 * i);
                 const bf16x4 hv = *p;
                 bf16x4 o;
 #pragma unroll
@@ -507,6 +544,10 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     mark(10);
 }
 
+/* HPNN_WIDE_ABL (profiling only): 1 = phase A alone, 2 = everything but phase A,
+ * 3..9 = no phase A and stop at trace mark 3..9 */
+const int g_wide_abl = [] { const char *e = getenv("HPNN_WIDE_ABL"); return e ? atoi(e) : 0; }();
+
 template <int TYPE, bool LABELS, int NS, int KSPLIT>
 int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
     static const bool trace = [] { const char *e = getenv("HPNN_WIDE_TRACE"); return e && e[0] == '1'; }();
@@ -523,7 +564,7 @@ int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
     hipLaunchKernelGGL(kern, dim3(n_tiles * KSPLIT), dim3(512), LDS_TOTAL, stream, (const __bf16 *)a.X, a.ldx,
                        (const __bf16 *)a.W0, a.K0, (const __bf16 *)a.W1, (const __bf16 *)a.W1t, a.labels, a.T, a.ldt,
                        a.t_hi, a.t_lo, (__bf16 *)a.H0, (__bf16 *)a.D2, (__bf16 *)a.D1, (f32x4 *)a.pbuf, a.cnt,
-                       a.flag, a.err, a.loss_acc, a.correct, a.n_valid, a.n_out);
+                       a.flag, a.err, a.loss_acc, a.correct, a.n_valid, a.n_out, g_wide_abl);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -292,9 +292,9 @@ WIDE2_TILE = 128  # samples per tile (the batch must be a multiple)
 
 
 class Wide2Workspace:
-    """hand-over state of hpnn_wide2_front with two workgroups per tile: the FP32 partial
-    buffer and the per-tile counter / flag words (zeroed once, self-resetting) plus an
-    error word (set if a hand-over ever timed out)."""
+    """exchange state of hpnn_wide2_front with two workgroups per tile: the FP32 partial
+    buffer and the per-tile ticket counters (zeroed once, monotonic: two tickets per tile and
+    launch; the flag words are unused) plus an error word (set if an exchange ever timed out)."""
 
     def __init__(self, Bp, K0, device, ksplit=None):
         if torch.device(device).type != "cuda":

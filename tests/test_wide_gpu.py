@@ -71,8 +71,10 @@ def test_wide_front_bitwise_repeatable_with_handover(gpu):
     b, _, sb, _, _ = _front("SNN", 230, False, 8192, 8192, 2, seed=5)
     assert all(torch.equal(x, y) for x, y in zip(a, b))
     assert torch.equal(sa[:, 1], sb[:, 1])
-    # the per-tile counters and flags are back at zero after the launch
-    assert int(ws.words.abs().sum()) == 0
+    # one launch: two tickets per tile on the monotonic counters, no exchange timed out
+    n_tiles = 8192 // ops.WIDE2_TILE
+    assert torch.equal(ws.cnt.cpu(), torch.full((n_tiles,), 2, dtype=torch.int32))
+    assert int(ws.err.item()) == 0
 
 
 def _oracle_step(W, V, X, lab, n_out, lr, alpha):
