@@ -405,7 +405,8 @@ class MLP:
             self.update_all(lr, alpha, scale, [self.slab[0], g1, g2])
             return
         if self.fused_mode == "w":
-            # one launch up to the deltas, then the per-layer weight gradients and steps
+            # one launch up to the deltas, then the per-layer weight gradients and steps (one
+            # multi-layer update launch measured no faster: 22.1 us vs 2 x 10.7)
             self._fused_front(X, labels, T, n_valid)
             self._grads_and_steps(X, lr, alpha, scale)
             return
