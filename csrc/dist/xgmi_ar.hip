@@ -116,7 +116,7 @@ __device__ __forceinline__ void add4(float4 &a, const float4 &b) {
 /* local sum of element i of the input: slabs s = k (mod U) accumulate in acc[k], U = 8 loads
  * in flight per thread, combined in a fixed tree (2 in flight took 15.2 us per MNIST step,
  * 8 took 11.3).  More measured slower on the N > 1 step path timed on one GPU: 16 per batch
- * +0.7-1.1 us, a software-pipelined 16 + 16 variant +8 us (scripts/gpu_xar_pipe.sh,
+ * +0.7-1.1 us, a software-pipelined 16 + 16 variant +8 us (round-2 A/B script, since pruned;
  * profiles/r2/s5_xar_launch_shape.txt). */
 template <int U>
 __device__ __forceinline__ float4 xar_load_in_u(const float4 *p, long st, int S) {

@@ -17,8 +17,8 @@
  * (MLP.prepare_input): half the bytes of the BF16 batch, converted in registers to the
  * same bf16(pixel * scale) values the front computes with (8 waves hide the conversion).
  * In the step: 72.5-72.7 us with it vs 74.8-75.6 us for the LDS-DMA TN kernel on the
- * BF16 batch (scripts/gpu_ab_input.sh); cold 26.5 us vs 34 in scripts/g0_direct.py.
- * Measured (scripts/g0_direct.py, 48 splits): LDS-staged TN kernel 31.2 us (its LDS-DMA
+ * BF16 batch; cold 26.5 us vs 34 standalone (round-2 A/B scripts, since pruned).
+ * Measured (48 splits): LDS-staged TN kernel 31.2 us (its LDS-DMA
  * fill, ~27 GB/s per CU, is the bound); this kernel 23.8 us, ~5.1 TB/s of HBM reads --
  * it streams at the memory rate.  Rejected on the way: the same kernel on plain
  * batch-contiguous (transposed row-major) operands, 51 us -- each wave load then hits

@@ -463,8 +463,6 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
                 const int *labels, const float *T, int ldt, float t_hi, float t_lo, void *D1, float *gslab,
                 float *loss_acc, unsigned int *correct, int n_tiles, int n_valid, int n_out, int grid,
                 hipStream_t stream) {
-    /* k-steps of loads in flight (HPNN_TILE_D tunes the MNIST-shaped instance) */
-    static const int dsel = [] { const char *e = getenv("HPNN_TILE_D"); return e ? atoi(e) : 0; }();
     static const bool trace = [] { const char *e = getenv("HPNN_TILE_TRACE"); return e && e[0] == '1'; }();
     auto go = [&](auto kern, int threads) {
         static bool attr = false;
@@ -477,13 +475,11 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
                            (__bf16 *)D1, gslab, loss_acc, correct, n_tiles, n_valid, n_out);
         return hipGetLastError() == hipSuccess ? grid : -5;
     };
-    /* D = 3 k-steps of loads in flight: 58.7 us per MNIST step vs 59.6-59.7 at D = 4 (B reads
-     * one k-step ahead; the deeper ring costs the registers the B prefetch needs) */
-    if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
+    /* D = 3 k-steps of loads in flight: 58.7-59.4 us per MNIST step vs 59.6-60.4 at D = 4 and
+     * 59.8-60.3 at D = 2 (B reads one k-step ahead; a deeper ring costs the registers the B
+     * prefetch needs), profiles/r3/SUMMARY.md */
+    if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8)
         if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
-        if (dsel == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 4>, 512);
-        if (dsel == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2>, 512);
-    }
     return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }
 
