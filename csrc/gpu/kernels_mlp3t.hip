@@ -86,7 +86,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
-template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false>
+template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -108,7 +108,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
      * takes row w, lane half h = l >> 5 takes feature half h, XB bytes per lane (2 fm lanes) */
     constexpr int XB = 16 * (XU8 ? 1 : 2); /* bytes per lane per k-step */
     constexpr int XV = XB / 16;            /* 16-byte vectors per lane */
-    constexpr int SG = NW / 4;           /* phase A: sample groups (waves per neuron group) */
+    constexpr int NT = 4;                /* phase A: 16-neuron tiles per wave (64 neurons) */
+    constexpr int SG = NW / (H1 / (16 * NT)); /* phase A: sample groups (waves per neuron group) */
     constexpr int SPA = TS / SG;         /* phase A: samples per wave */
     constexpr int STA = SPA / 16;        /* phase A: 16-sample tiles per wave */
     constexpr int SPC = TS / NW;         /* chain: samples per wave */
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ng = wave & 3, sh = wave >> 2; /* phase A: neurons 32 ng.., samples SPA sh.. */
+    const int ng = wave & 1, sh = wave >> 1; /* phase A: neurons 64 ng.., samples SPA sh.. */
     const int r16 = lane & 15, q = lane >> 4;
     const LaneOff lo = lane_offsets(lane);
     char *imgH1 = lds + OFF_H1, *imgH2 = lds + OFF_H2, *imgD2 = lds + OFF_D2, *imgD3 = lds + OFF_D3;
@@ -167,11 +168,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
         const char *xtile = xbase + (size_t)T0 * NCB * CHUNK;
-        const __bf16 *wbase = W0f + ((size_t)(2 * ng) * KS * 64 + lane) * 8;
+        const __bf16 *wbase = W0f + ((size_t)(NT * ng) * KS * 64 + lane) * 8;
 
         typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
         u32x4 xr[KS][XV];
-        bf16x8 wr[KS][2];
+        bf16x8 wr[KS][NT];
         /* X(sx) and W0(sw) in one batch: an opaque zero pins the loads to this point of the
          * k-loop (the operands are read-only, so the compiler would otherwise hoist every W0
          * load out of the tile loop: spills).  X(k) is consumed two k-steps before W0(k)
@@ -181,14 +182,18 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         auto issue = [&](int sx, int sw) {
             unsigned int z = 0;
             asm volatile("" : "+s"(z));
+            /* ABL (profiling only): 1 = W0 loaded by the sh = 0 waves only, 2 = no X loads */
             if (sx < KS) {
 #pragma unroll
                 for (int n = 0; n < XV; n++)
-                    xr[sx][n] = *(const u32x4 *)(xtile + z + (size_t)(2 * sx) * CHUNK + 16 * n);
+                    xr[sx][n] = ABL == 2 ? u32x4{z, z, z, z}
+                                         : *(const u32x4 *)(xtile + z + (size_t)(2 * sx) * CHUNK + 16 * n);
             }
             if (sw >= 0 && sw < KS) {
 #pragma unroll
-                for (int i = 0; i < 2; i++) wr[sw][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
+                for (int i = 0; i < NT; i++)
+                    wr[sw][i] = (ABL == 1 && (sh & 1)) ? bf16x8{}
+                                                      : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
             }
         };
         auto convert = [&](int s) {
@@ -205,9 +210,9 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             *(bf16x8 *)(img + xoff[1]) = v[1];
         };
 
-        f32x4 acc[2][STA];
+        f32x4 acc[NT][STA];
 #pragma unroll
-        for (int i = 0; i < 2; i++)
+        for (int i = 0; i < NT; i++)
 #pragma unroll
             for (int st = 0; st < STA; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -244,10 +249,9 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             if (s + 1 < KS) read_b(s + 1, bb[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int st = 0; st < STA; st++) {
-                acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
-                acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
-            }
+            for (int st = 0; st < STA; st++)
+#pragma unroll
+                for (int i = 0; i < NT; i++) acc[i][st] = mfma(wr[s][i], bb[s & 1][st], acc[i][st]);
             __builtin_amdgcn_sched_barrier(0);
             if (s + 2 < KS) convert(s + 2);
             lds_barrier();
@@ -255,13 +259,13 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         mark(3);
         /* H1 tile -> LDS image [sample][neuron] */
 #pragma unroll
-        for (int i = 0; i < 2; i++)
+        for (int i = 0; i < NT; i++)
 #pragma unroll
             for (int st = 0; st < STA; st++) {
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
-                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i) = o;
+                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 16 * NT * ng + 16 * i) = o;
             }
         lds_barrier();
 
@@ -457,6 +461,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 }
 
 int g_tile_cus = 0;
+/* HPNN_TILE_ABL (profiling only, wrong results): 1 = half the W0 loads, 2 = no X loads */
+const int g_tile_abl = [] { const char *e = getenv("HPNN_TILE_ABL"); return e ? atoi(e) : 0; }();
 
 template <int TYPE, bool LABELS, int KS, bool XU8>
 int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, const void *W2, const void *W2t,
@@ -478,8 +484,11 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
     /* D = 3 k-steps of loads in flight: 58.7-59.4 us per MNIST step vs 59.6-60.4 at D = 4 and
      * 59.8-60.3 at D = 2 (B reads one k-step ahead; a deeper ring costs the registers the B
      * prefetch needs), profiles/r3/SUMMARY.md */
-    if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8)
+    if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
         if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+        if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
+        if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);
+    }
     return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }
 
