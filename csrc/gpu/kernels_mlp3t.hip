@@ -246,14 +246,16 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
         for (int s = 0; s < KS; s++) {
             issue(s + D + 1, s + D - 1);
-            if (s + 1 < KS) read_b(s + 1, bb[(s + 1) & 1]);
+            if (s + 1 < KS && ABL != 4) read_b(s + 1, bb[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int st = 0; st < STA; st++)
 #pragma unroll
-                for (int i = 0; i < NT; i++) acc[i][st] = mfma(wr[s][i], bb[s & 1][st], acc[i][st]);
+                for (int i = 0; i < NT; i++)
+                    if constexpr (ABL != 3) acc[i][st] = mfma(wr[s][i], bb[s & 1][st], acc[i][st]);
+                    else acc[i][st] += __builtin_bit_cast(f32x4, wr[s][i]) * 0.f;
             __builtin_amdgcn_sched_barrier(0);
-            if (s + 2 < KS) convert(s + 2);
+            if (s + 2 < KS && ABL != 5) convert(s + 2);
             lds_barrier();
         }
         mark(3);
@@ -461,7 +463,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 }
 
 int g_tile_cus = 0;
-/* HPNN_TILE_ABL (profiling only, wrong results): 1 = half the W0 loads, 2 = no X loads */
+/* HPNN_TILE_ABL (profiling only, wrong results): 1 = half the W0 loads, 2 = no X loads,
+ * 3 = no phase-A MFMAs, 4 = no phase-A B reads, 5 = no X^T conversion writes */
 const int g_tile_abl = [] { const char *e = getenv("HPNN_TILE_ABL"); return e ? atoi(e) : 0; }();
 
 template <int TYPE, bool LABELS, int KS, bool XU8>
@@ -488,6 +491,9 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
         if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);
+        if (g_tile_abl == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 3>, 512);
+        if (g_tile_abl == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 4>, 512);
+        if (g_tile_abl == 5) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 5>, 512);
     }
     return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }
