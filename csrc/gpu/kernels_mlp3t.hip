@@ -100,7 +100,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                                                             int n_valid, int n_out) {
     /* 8 waves (a 16-wave workgroup, 128 VGPRs a wave, measured slower: 65.2 vs 60.2-60.7 us
      * per step, its chain no faster -- the chain is bound by LDS / MFMA throughput, not by
-     * per-wave latency) */
+     * per-wave latency).  Phase A on 32 x 128 wave tiles: 64 x 64 (half the B reads, twice
+     * the W0 fragments) measured 59.1-59.9 vs 58.1-58.9 us same box. */
     constexpr int NW = 8;
     constexpr int CHUNK = XU8 ? 512 : 1024; /* bytes of one 32 x 16 input chunk */
     constexpr int NCB = 2 * KS;             /* 16-feature blocks per 32-sample row of chunks */
@@ -108,8 +109,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
      * takes row w, lane half h = l >> 5 takes feature half h, XB bytes per lane (2 fm lanes) */
     constexpr int XB = 16 * (XU8 ? 1 : 2); /* bytes per lane per k-step */
     constexpr int XV = XB / 16;            /* 16-byte vectors per lane */
-    constexpr int NT = 4;                /* phase A: 16-neuron tiles per wave (64 neurons) */
-    constexpr int SG = NW / (H1 / (16 * NT)); /* phase A: sample groups (waves per neuron group) */
+    constexpr int SG = NW / 4;           /* phase A: sample groups (waves per neuron group) */
     constexpr int SPA = TS / SG;         /* phase A: samples per wave */
     constexpr int STA = SPA / 16;        /* phase A: 16-sample tiles per wave */
     constexpr int SPC = TS / NW;         /* chain: samples per wave */
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ng = wave & 1, sh = wave >> 1; /* phase A: neurons 64 ng.., samples SPA sh.. */
+    const int ng = wave & 3, sh = wave >> 2; /* phase A: neurons 32 ng.., samples SPA sh.. */
     const int r16 = lane & 15, q = lane >> 4;
     const LaneOff lo = lane_offsets(lane);
     char *imgH1 = lds + OFF_H1, *imgH2 = lds + OFF_H2, *imgD2 = lds + OFF_D2, *imgD3 = lds + OFF_D3;
@@ -168,11 +168,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
         const char *xtile = xbase + (size_t)T0 * NCB * CHUNK;
-        const __bf16 *wbase = W0f + ((size_t)(NT * ng) * KS * 64 + lane) * 8;
+        const __bf16 *wbase = W0f + ((size_t)(2 * ng) * KS * 64 + lane) * 8;
 
         typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
         u32x4 xr[KS][XV];
-        bf16x8 wr[KS][NT];
+        bf16x8 wr[KS][2];
         /* X(sx) and W0(sw) in one batch: an opaque zero pins the loads to this point of the
          * k-loop (the operands are read-only, so the compiler would otherwise hoist every W0
          * load out of the tile loop: spills).  X(k) is consumed two k-steps before W0(k)
@@ -191,8 +191,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             }
             if (sw >= 0 && sw < KS) {
 #pragma unroll
-                for (int i = 0; i < NT; i++)
-                    wr[sw][i] = (ABL == 1 && (sh & 1)) ? bf16x8{}
+                for (int i = 0; i < 2; i++)
+                    wr[sw][i] = (ABL == 1 && sh == 1) ? bf16x8{}
                                                       : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
             }
         };
@@ -210,9 +210,9 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             *(bf16x8 *)(img + xoff[1]) = v[1];
         };
 
-        f32x4 acc[NT][STA];
+        f32x4 acc[2][STA];
 #pragma unroll
-        for (int i = 0; i < NT; i++)
+        for (int i = 0; i < 2; i++)
 #pragma unroll
             for (int st = 0; st < STA; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -249,11 +249,14 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             if (s + 1 < KS && ABL != 4) read_b(s + 1, bb[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int st = 0; st < STA; st++)
-#pragma unroll
-                for (int i = 0; i < NT; i++)
-                    if constexpr (ABL != 3) acc[i][st] = mfma(wr[s][i], bb[s & 1][st], acc[i][st]);
-                    else acc[i][st] += __builtin_bit_cast(f32x4, wr[s][i]) * 0.f;
+            for (int st = 0; st < STA; st++) {
+                if constexpr (ABL != 3) {
+                    acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
+                    acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
+                } else {
+                    acc[0][st] += __builtin_bit_cast(f32x4, wr[s][0]) * 0.f;
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
             if (s + 2 < KS && ABL != 5) convert(s + 2);
             lds_barrier();
@@ -261,13 +264,13 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         mark(3);
         /* H1 tile -> LDS image [sample][neuron] */
 #pragma unroll
-        for (int i = 0; i < NT; i++)
+        for (int i = 0; i < 2; i++)
 #pragma unroll
             for (int st = 0; st < STA; st++) {
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
-                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 16 * NT * ng + 16 * i) = o;
+                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i) = o;
             }
         lds_barrier();
 

@@ -11,3 +11,6 @@ for r in 1 2 3; do
   $T 200 python bench.py --steps 300 --warmup 30 "$@" > $O/b_$r.log 2>&1 || exit $?
   echo "A $(tail -n 1 $O/a_$r.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"]*1000)')  B $(tail -n 1 $O/b_$r.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"]*1000)')"
 done
+LD_LIBRARY_PATH=$PWD/build_ab:$LD_LIBRARY_PATH HPNN_TILE_TRACE=1 $T 120 python scripts/tile_trace.py > $O/trA.log 2>&1 || exit $?
+HPNN_TILE_TRACE=1 $T 120 python scripts/tile_trace.py > $O/trB.log 2>&1 || exit $?
+paste <(grep ticks $O/trA.log | cut -c1-60) <(grep ticks $O/trB.log | cut -c29-60)
