@@ -296,26 +296,35 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 lab[st] = labels[s];
             }
         }
-        /* P1: H2^T [h2][sample] = f(W1 H1^T) */
+        /* P1: H2^T [h2][sample] = f(W1 H1^T), this wave's STC sample tiles together: each W1
+         * fragment is read from LDS once and feeds STC independent MFMAs */
+        {
+            f32x4 a[STC][4];
 #pragma unroll
-        for (int st = 0; st < STC; st++) {
-            const int r0 = sw + 16 * st;
-            f32x4 a[4];
+            for (int st = 0; st < STC; st++)
 #pragma unroll
-            for (int ht = 0; ht < 4; ht++) a[ht] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int ht = 0; ht < 4; ht++) a[st][ht] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < H1; k += 32) {
-                const bf16x8 b = rd_row<TS>(imgH1, lo, r0, k);
+                bf16x8 b[STC];
 #pragma unroll
-                for (int ht = 0; ht < 4; ht++) a[ht] = mfma(rd_row<H2>(imgW1, lo, 16 * ht, k), b, a[ht]);
+                for (int st = 0; st < STC; st++) b[st] = rd_row<TS>(imgH1, lo, sw + 16 * st, k);
+#pragma unroll
+                for (int ht = 0; ht < 4; ht++) {
+                    const bf16x8 w = rd_row<H2>(imgW1, lo, 16 * ht, k);
+#pragma unroll
+                    for (int st = 0; st < STC; st++) a[st][ht] = mfma(w, b[st], a[st][ht]);
+                }
             }
 #pragma unroll
-            for (int ht = 0; ht < 4; ht++) {
-                bf16x4 o;
+            for (int st = 0; st < STC; st++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[ht][r]);
-                *(bf16x4 *)wr_ptr<TS>(imgH2, lo, r0, 16 * ht) = o;
-            }
+                for (int ht = 0; ht < 4; ht++) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[st][ht][r]);
+                    *(bf16x4 *)wr_ptr<TS>(imgH2, lo, sw + 16 * st, 16 * ht) = o;
+                }
         }
         mark(5);
         wave_lds_fence();
@@ -363,14 +372,21 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         {
             __bf16 *chunk0 = D1 + (size_t)(T0 + (sw >> 5)) * (H1 / 16) * 512;
             const int gb = 2 * ((sw >> 4) & 1);
+            bf16x8 d0[STC], d1[STC];
 #pragma unroll
             for (int st = 0; st < STC; st++) {
-                const int r0 = sw + 16 * st;
-                const bf16x8 d0 = rd_row<TS>(imgD2, lo, r0, 0), d1 = rd_row<TS>(imgD2, lo, r0, 32);
+                d0[st] = rd_row<TS>(imgD2, lo, sw + 16 * st, 0);
+                d1[st] = rd_row<TS>(imgD2, lo, sw + 16 * st, 32);
+            }
+            /* each W1^T fragment read once, for all STC sample tiles */
 #pragma unroll
-                for (int ht = 0; ht < 8; ht++) {
-                    f32x4 a = mfma(d0, rd_tr<H2>(imgW1, lo, 0, 16 * ht), f32x4{0.f, 0.f, 0.f, 0.f});
-                    a = mfma(d1, rd_tr<H2>(imgW1, lo, 32, 16 * ht), a);
+            for (int ht = 0; ht < 8; ht++) {
+                const bf16x8 w0 = rd_tr<H2>(imgW1, lo, 0, 16 * ht), w1 = rd_tr<H2>(imgW1, lo, 32, 16 * ht);
+#pragma unroll
+                for (int st = 0; st < STC; st++) {
+                    const int r0 = sw + 16 * st;
+                    f32x4 a = mfma(d0[st], w0, f32x4{0.f, 0.f, 0.f, 0.f});
+                    a = mfma(d1[st], w1, a);
                     /* D[row = sample r0 + 4q + r][col = h1 16 ht + r16]; f'(H1) of those 4 samples */
                     const s16x4 hr = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s16x4 *)(imgH1 + t32<TS>(r0 + 4 * q + (r16 >> 2), 16 * ht + 4 * (r16 & 3))));
