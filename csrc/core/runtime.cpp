@@ -172,7 +172,24 @@ void hpnn_rt_probe_memory_model(void) {
         }
         c->mem_model = CUDA_MEM_P2P;
     } else {
-        c->mem_model = CUDA_MEM_EXP;
+        /* the reference's fallback order (libhpnn.c:245-280): peer access, then managed
+         * memory with concurrent access on every device, then explicit copies.  The engines
+         * treat CMM like EXP (a replica per device, explicit collectives): on an xGMI node
+         * every pair has peer access, so CMM is only reached on a partial topology. */
+        BOOL cmm = TRUE;
+        for (UINT a = 0; a < c->n_gpu; a++) {
+            int mm = 0, conc = 0;
+            hipDeviceGetAttribute(&mm, hipDeviceAttributeManagedMemory, hpnn_rt_device(a));
+            hipDeviceGetAttribute(&conc, hipDeviceAttributeConcurrentManagedAccess, hpnn_rt_device(a));
+            cmm = cmm && mm && conc;
+        }
+        c->mem_model = cmm ? CUDA_MEM_CMM : CUDA_MEM_EXP;
+    }
+    switch (c->mem_model) {
+    case CUDA_MEM_P2P: NN_DBG(stdout, "multi-GPU will use peer access between all GPUs\n"); break;
+    case CUDA_MEM_CMM: NN_DBG(stdout, "multi-GPU will use managed memory (explicit collectives)\n"); break;
+    case CUDA_MEM_EXP: NN_DBG(stdout, "multi-GPU using explicit collectives\n"); break;
+    default: break;
     }
     hipSetDevice(hpnn_rt_device(0));
 }

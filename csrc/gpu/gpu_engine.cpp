@@ -64,7 +64,8 @@ struct GpuModel {
      * one fine-grained allocation on slot 0's device that every slot maps */
     std::vector<GpuModel *> slots;
     int n_slots = 1, sgrid = 0;
-    bool sloop = false;
+    int spd = 1; /* slots per device: S for virtual slots on device 0, else train_nn -S (capped) */
+    bool sstream_owned = true; /* false: sstream is one of the runtime's -S streams */
     double *sxch = nullptr;
     unsigned int *sctl = nullptr;
     long sxch_bytes = 0;
@@ -83,7 +84,7 @@ void free_model(GpuModel *g) {
     hipSetDevice(g->dev);
     if (g->sxch) hipFree(g->sxch);
     if (g->sctl) hipFree(g->sctl);
-    if (g->sstream) hipStreamDestroy(g->sstream);
+    if (g->sstream && g->sstream_owned) hipStreamDestroy(g->sstream);
     for (int l = 0; l < 16; l++) {
         if (g->W[l]) hpnn_dev_free(g->W[l]);
         if (g->dW[l]) hpnn_dev_free(g->dW[l]);
@@ -242,10 +243,25 @@ extern "C" void hpnn_gpu_mark_host_dirty(kernel_ann *k) {
 
 namespace {
 
-/* slot models for online training over S devices (or S virtual slots on device 0) */
-BOOL ensure_slots(kernel_ann *k, int S, bool loopback) {
+/* the stream slot s runs on: the runtime's stream (s mod spd) of its device when train_nn -S
+ * created that many (the reference's slice per stream, libhpnn.c:471-505), else its own */
+void slot_stream(GpuModel *m, int s, int spd) {
+    const nn_runtime *rt = hpnn_rt_get();
+    const bool shared = spd > 1 && rt && (int)rt->cudas.cuda_n_streams >= spd;
+    if (m->sstream && m->sstream_owned && !shared) return;
+    if (m->sstream && m->sstream_owned) hipStreamDestroy(m->sstream);
+    m->sstream = nullptr;
+    m->sstream_owned = !shared;
+    if (shared) m->sstream = hpnn_rt_stream((UINT)(s / spd), (UINT)(s % spd));
+    else if (hipStreamCreateWithFlags(&m->sstream, hipStreamNonBlocking) != hipSuccess) m->sstream = nullptr;
+}
+
+/* slot models for online training over S slots, spd of them per device (S devices with
+ * train_nn -G S; -G G -S 2: two slots per device; HPNN_ONLINE_SLOTS: S virtual slots on
+ * device 0) */
+BOOL ensure_slots(kernel_ann *k, int S, int spd) {
     GpuModel *g = (GpuModel *)k->gpu;
-    if (g->n_slots == S && g->sloop == loopback) return TRUE;
+    if (g->n_slots == S && g->spd == spd) return TRUE;
     for (GpuModel *m : g->slots) free_model(m);
     g->slots.clear();
     g->n_slots = 1;
@@ -253,7 +269,7 @@ BOOL ensure_slots(kernel_ann *k, int S, bool loopback) {
     if (S <= 1) return TRUE;
     for (int s = 1; s < S; s++) {
         GpuModel *m = new GpuModel();
-        m->dev = loopback ? g->dev : hpnn_rt_device((UINT)s);
+        m->dev = hpnn_rt_device((UINT)(s / spd));
         m->L = g->L;
         g->slots.push_back(m);
         HIPCHK(hipSetDevice(m->dev));
@@ -266,14 +282,18 @@ BOOL ensure_slots(kernel_ann *k, int S, bool loopback) {
         HIPCHK(hpnn_dev_malloc(&m->out, sizeof(double) * k->n_outputs));
         HIPCHK(hpnn_dev_malloc(&m->result, sizeof(double) * 8));
         HIPCHK(hpnn_dev_malloc(&m->scratch, sizeof(double) * 8));
-        HIPCHK(hipStreamCreateWithFlags(&m->sstream, hipStreamNonBlocking));
+        slot_stream(m, s, spd);
+        if (!m->sstream) return FALSE;
     }
     HIPCHK(hipSetDevice(g->dev));
-    if (!g->sstream) HIPCHK(hipStreamCreateWithFlags(&g->sstream, hipStreamNonBlocking));
+    slot_stream(g, 0, spd);
+    if (!g->sstream) return FALSE;
     g->n_slots = S;
     g->sgrid = 0;
-    g->sloop = loopback;
+    g->spd = spd;
     g->host_newer = true; /* every slot takes the host weights */
+    NN_OUT(stdout, "online GPU engine: rows over %d slots (%d per GPU, %s streams)\n", S, spd,
+           g->sstream_owned ? "own" : "runtime");
     return TRUE;
 }
 
@@ -303,7 +323,7 @@ BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBL
     const bool mom = train == NN_TRAIN_BPM;
     hpnn_online_args a0;
     fill_args(k, g, type, &a0);
-    const int grid = hpnn_online_coop_grid_slots(&a0, S, g->sloop ? 128 / S : 128);
+    const int grid = hpnn_online_coop_grid_slots(&a0, S, 128 / g->spd);
     if (grid <= 0) return FALSE;
     const int total = grid * S;
     g->sgrid = grid; /* fixed for a net and S: the row ownership gather_host relies on */
@@ -373,16 +393,33 @@ BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBL
 }
 
 /* online slots: HPNN_ONLINE_SLOTS=S runs S virtual slots on device 0 (tests of the
- * device-spanning protocol on one GPU; S = 2: every slot's persistent launch needs a
- * hardware queue of its own to run concurrently, and a process gets GPU_MAX_HW_QUEUES = 4
- * of them); else the runtime's GPU count (train_nn -G N) */
-int online_slots(bool *loopback) {
+ * device-spanning protocol on one GPU); else n_gpu x min(-S, 2) slots, the reference's
+ * rows over n_gpu x n_streams (cuda_ann.cu:533-1275).  At most two slots share a device:
+ * every slot's persistent launch needs a hardware queue of its own to run concurrently with
+ * the others (a process gets GPU_MAX_HW_QUEUES = 4, one of them the null stream's), and more
+ * slots on one device only split the same CUs finer. */
+int online_slots(int *spd) {
     const char *e = getenv("HPNN_ONLINE_SLOTS");
     const int v = e ? atoi(e) : 0;
-    *loopback = v > 1;
-    if (v > 1) return v;
+    if (v > 1) {
+        *spd = v;
+        return v;
+    }
     const nn_runtime *rt = hpnn_rt_get();
-    return rt && rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
+    if (!rt) {
+        *spd = 1;
+        return 1;
+    }
+    const int ng = rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
+    int ns = (int)rt->cudas.cuda_n_streams;
+    if (ns > 2) {
+        static bool warned = false;
+        if (!warned) NN_WARN(stderr, "online GPU engine: %d streams per GPU requested, 2 slots per GPU used\n", ns);
+        warned = true;
+        ns = 2;
+    }
+    *spd = ns > 1 ? ns : 1;
+    return ng * *spd;
 }
 
 }  // namespace
@@ -391,14 +428,14 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
                                         const DOUBLE *out, DOUBLE lr, DOUBLE alpha, DOUBLE delta, UINT *n_iter,
                                         BOOL *ok, DOUBLE *init_err, BOOL *first_ok) {
     {
-        bool loop = false;
-        const int S = online_slots(&loop);
+        int spd = 1;
+        const int S = online_slots(&spd);
         if (S > 1) {
             if (!k->gpu && !ensure_model(k, 0, true)) return 0.0;
             GpuModel *g = (GpuModel *)k->gpu;
             /* a different slot layout: the host takes the current rows first */
-            if (g->device_newer && (g->n_slots != S || g->sloop != loop)) gather_host(k);
-            if (!ensure_slots(k, S, loop)) return 0.0;
+            if (g->device_newer && (g->n_slots != S || g->spd != spd)) gather_host(k);
+            if (!ensure_slots(k, S, spd)) return 0.0;
             if (g->host_newer && !(ensure_model(k, 0, true) && upload_slots(k))) return 0.0;
             double res[5] = {0, 0, 0, 0, 0};
             bool to = false;
@@ -416,7 +453,7 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
                 return res[0];
             }
             /* the net does not suit the cooperative kernel: one device */
-            ensure_slots(k, 1, false);
+            ensure_slots(k, 1, 1);
         }
     }
     if (!ensure_model(k, 0)) return 0.0;

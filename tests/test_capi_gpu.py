@@ -171,20 +171,28 @@ def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots
     (Two slots: the slots' launches must run concurrently, and on one device more
     streams than hardware queues (GPU_MAX_HW_QUEUES = 4) would serialise them.)
     Every slot owns the rows j with (j mod total workgroups) in its range; the host gathers
-    each row from its owner when the kernel is dumped."""
+    each row from its owner when the kernel is dumped.
+    "streams": train_nn -S 2 without the variable -- the reference's rows over n_gpu x
+    n_streams (libhpnn.c:471-505): two slots on the device, each on one of the runtime's
+    two streams."""
     n_in, hid, n_out = dims
-    runs = {"cpu": (True, None), "one": (False, None), "slots": (False, {"HPNN_ONLINE_SLOTS": str(slots)})}
-    for tag, (cpu, env) in runs.items():
+    runs = {"cpu": (True, None, []), "one": (False, None, []),
+            "slots": (False, {"HPNN_ONLINE_SLOTS": str(slots)}, []), "streams": (False, None, ["-S", "2"])}
+    for tag, (cpu, env, flags) in runs.items():
         d = str(tmp_path / tag)
         _data(os.path.join(d, "samples"), 3, n_in, n_out, net == "SNN", seed=7)
         formats.write_conf(os.path.join(d, "nn.conf"), name="t", type=net, seed=9, inputs=n_in, hiddens=hid,
                            outputs=n_out, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
-        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, cpu=cpu, extra_env=env)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv"] + flags + ["nn.conf"], d, cpu=cpu, extra_env=env)
         assert out.count("TRAINING FILE") == 3
+        assert ("rows over 2 slots" in out) == (tag in ("slots", "streams")), out[-2000:]
+        if tag == "streams":
+            assert "runtime streams" in out, out[-2000:]
     ks = {t: formats.read_kernel(str(tmp_path / t / "kernel.opt"))["weights"] for t in runs}
-    for a, b, c in zip(ks["cpu"], ks["one"], ks["slots"]):
+    for a, b, c, e in zip(ks["cpu"], ks["one"], ks["slots"], ks["streams"]):
         assert np.abs(c - b).max() < 1e-9, np.abs(c - b).max()
         assert np.abs(c - a).max() < 1e-9, np.abs(c - a).max()
+        assert np.abs(e - b).max() < 1e-9, np.abs(e - b).max()
 
 
 @pytest.mark.parametrize("dtype,ranks,dims", [("f64", 2, (100, [48, 37], 7)), ("f64", 3, (64, [50], 9)),
