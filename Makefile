@@ -19,6 +19,9 @@ DEFS      := -D__HIP_PLATFORM_AMD__
 # -ffp-contract=off keeps the FP64 CPU oracle bit-stable across compilers
 CXXFLAGS  := -O2 -std=c++17 -fPIC -fopenmp -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result $(INC) $(DEFS)
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(INC)
+# make ABLATIONS=1: also build the front kernels' profiling ablations (HPNN_TILE_ABL /
+# HPNN_WIDE_ABL, wrong results by design); the default library has none of them
+HIPFLAGS  += $(if $(ABLATIONS),-DHPNN_ABLATIONS)
 LDFLAGS   := -L$(ROCM)/lib -lamdhip64 -fopenmp
 
 CORE_SRC  := $(wildcard csrc/core/*.cpp) $(wildcard csrc/cpu/*.cpp) $(wildcard csrc/dist/*.cpp) csrc/gpu/gpu_engine.cpp csrc/gpu/tp_engine.cpp

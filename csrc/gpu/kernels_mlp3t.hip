@@ -482,9 +482,12 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 }
 
 int g_tile_cus = 0;
-/* HPNN_TILE_ABL (profiling only, wrong results): 1 = half the W0 loads, 2 = no X loads,
- * 3 = no phase-A MFMAs, 4 = no phase-A B reads, 5 = no X^T conversion writes */
+#ifdef HPNN_ABLATIONS
+/* HPNN_TILE_ABL (make ABLATIONS=1 builds only; profiling, wrong results): 1 = half the W0
+ * loads, 2 = no X loads, 3 = no phase-A MFMAs, 4 = no phase-A B reads, 5 = no X^T
+ * conversion writes */
 const int g_tile_abl = [] { const char *e = getenv("HPNN_TILE_ABL"); return e ? atoi(e) : 0; }();
+#endif
 
 template <int TYPE, bool LABELS, int KS, bool XU8>
 int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, const void *W2, const void *W2t,
@@ -508,11 +511,13 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
      * prefetch needs), profiles/r3/SUMMARY.md */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
         if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+#ifdef HPNN_ABLATIONS
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);
         if (g_tile_abl == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 3>, 512);
         if (g_tile_abl == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 4>, 512);
         if (g_tile_abl == 5) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 5>, 512);
+#endif
     }
     return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }

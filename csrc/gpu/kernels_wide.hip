@@ -544,9 +544,13 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
     mark(10);
 }
 
-/* HPNN_WIDE_ABL (profiling only): 1 = phase A alone, 2 = everything but phase A,
- * 3..9 = no phase A and stop at trace mark 3..9 */
+#ifdef HPNN_ABLATIONS
+/* HPNN_WIDE_ABL (make ABLATIONS=1 builds only; profiling): 1 = phase A alone, 2 = everything
+ * but phase A, 3..9 = no phase A and stop at trace mark 3..9 */
 const int g_wide_abl = [] { const char *e = getenv("HPNN_WIDE_ABL"); return e ? atoi(e) : 0; }();
+#else
+constexpr int g_wide_abl = 0;
+#endif
 
 template <int TYPE, bool LABELS, int NS, int KSPLIT>
 int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {

@@ -1,5 +1,6 @@
 #!/bin/bash
 # tile front ablations (HPNN_TILE_ABL, profiling only): step time with half the W0 loads / no X loads
+# needs a library built with `make ABLATIONS=1` (the default build ignores the variable)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/ab; mkdir -p $O
 for v in 0 3 4 5 2 0; do

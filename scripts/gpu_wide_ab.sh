@@ -1,5 +1,6 @@
 #!/bin/bash
 # wide (RRUFF) front: numerics tests, ablations, bench step time, kernel table
+# needs a library built with `make ABLATIONS=1` (the default build ignores the variable)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/wide; mkdir -p $O; export TMPDIR=/tmp
 T="timeout -k 10"
