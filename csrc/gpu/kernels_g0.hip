@@ -136,20 +136,26 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
 
     float *out = slab + (size_t)split * N * ldg;
     const int q = lane >> 4;
-    if constexpr (KW == 2) { /* group 1 hands its partial tile to group 0 through LDS */
+    if constexpr (KW > 1) { /* groups 1.. hand their partial tiles to group 0 through LDS, in order */
         __shared__ f32x4 part[4][WF * WH][64];
-        if (kg == 1) {
 #pragma unroll
-            for (int i = 0; i < WF; i++)
+        for (int g = 1; g < KW; g++) {
+            if (kg == g) {
 #pragma unroll
-                for (int j = 0; j < WH; j++) part[wave & 3][i * WH + j][lane] = acc[i][j];
+                for (int i = 0; i < WF; i++)
+#pragma unroll
+                    for (int j = 0; j < WH; j++) part[wave & 3][i * WH + j][lane] = acc[i][j];
+            }
+            __syncthreads();
+            if (kg == 0) {
+#pragma unroll
+                for (int i = 0; i < WF; i++)
+#pragma unroll
+                    for (int j = 0; j < WH; j++) acc[i][j] += part[wave & 3][i * WH + j][lane];
+            }
+            if (g + 1 < KW) __syncthreads();
         }
-        __syncthreads();
-        if (kg == 1) return;
-#pragma unroll
-        for (int i = 0; i < WF; i++)
-#pragma unroll
-            for (int j = 0; j < WH; j++) acc[i][j] += part[wave & 3][i * WH + j][lane];
+        if (kg != 0) return;
     }
 #pragma unroll
     for (int i = 0; i < WF; i++)
@@ -186,6 +192,8 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
          * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves.
          * Round 3, in the MNIST step (tile front): 59.8-59.9 us per step with this one vs
          * 60.0 with 2 k-steps in flight, 62.3 / 61.4 with 4 waves and 2 / 3 in flight. */
+        /* session 7: three k-interleaved groups (12 waves, 3 a SIMD) 24.9 vs 23.4 us in the
+         * step, 58.9-59.3 vs 56.2-58.5 us per step (profiles/r3/s7_g0_kw_ab.txt) */
         if (h_u8) { HPNN_FM(5, 4, 1, 2); }
         HPNN_FM(5, 4, 2, 1);
     }
