@@ -4,9 +4,9 @@ convergence loop of fwd + bwd + update until the error stops improving) on a wid
 Writes N random samples, runs bin/train_nn with HPNN_METRICS, and takes the per-sample
 timestamps and N_ITER values from the metrics JSONL: it/s = sum(n_iter) / elapsed over
 samples 2..N (sample 1 pays the device setup).  Each configuration in --env runs in its own
-train_nn process.
+train_nn process; its comma-separated items are VAR=value pairs or train_nn flags ("-S2").
 
-    python scripts/online_bench.py --dims 4096,4096,230 --n 6 --env '' --env HPNN_ONLINE_SLOTS=2
+    python scripts/online_bench.py --dims 4096,4096,230 --n 6 --env '' --env HPNN_ONLINE_SLOTS=2 --env=-S2
 """
 import argparse
 import json
@@ -36,10 +36,14 @@ def run(dims, n, train, net, env_s, work):
                        outputs=n_out, train=train, sample_dir="./samples", test_dir="./samples", lr=0.001)
     env = dict(os.environ, HPNN_METRICS="m.jsonl")
     env.pop("HPNN_FORCE_CPU", None)
+    flags = []
     for kv in filter(None, env_s.split(",")):
+        if kv.startswith("-"):
+            flags.append(kv)
+            continue
         k, v = kv.split("=", 1)
         env[k] = v
-    r = subprocess.run([os.path.join(ROOT, "bin", "train_nn"), "-v", "nn.conf"], cwd=d, env=env,
+    r = subprocess.run([os.path.join(ROOT, "bin", "train_nn"), "-v"] + flags + ["nn.conf"], cwd=d, env=env,
                        capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
