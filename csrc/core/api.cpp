@@ -591,6 +591,10 @@ extern "C" BOOL _NN(train, kernel)(nn_def *conf) {
         conf->samples_seen++;
         free(in);
         free(out);
+        if (gpu && hpnn_gpu_failed(k)) {
+            NN_ERROR(stderr, "GPU device state lost after %u samples: training aborted\n", n_done);
+            return FALSE;
+        }
     }
     if (gpu) hpnn_gpu_sync_host(k);
     if (hpnn_metrics_active()) {

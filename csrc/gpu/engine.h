@@ -29,6 +29,11 @@ DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train train, const 
 BOOL hpnn_gpu_forward(kernel_ann *k, nn_type type, const DOUBLE *in);
 /* device weights -> host master copy (no-op if host is current) */
 void hpnn_gpu_sync_host(kernel_ann *k);
+/* TRUE once a device state was lost (a grid barrier timed out mid-sample): the caller
+ * stops training; the host weights are the last consistent ones */
+BOOL hpnn_gpu_failed(const kernel_ann *k);
+/* online slot layout (pure): n_gpu, -S streams, runtime memory model, HPNN_ONLINE_SLOTS */
+int hpnn_online_slot_plan(int n_gpu, int n_streams, int mem_model, int env_slots, int *spd);
 /* host master copy changed: mark device copy stale */
 void hpnn_gpu_mark_host_dirty(kernel_ann *k);
 

@@ -70,6 +70,11 @@ struct GpuModel {
     unsigned int *sctl = nullptr;
     long sxch_bytes = 0;
     hipStream_t sstream = nullptr;
+    /* a slot layout (S, spd) the cooperative kernel refused for this net: not retried */
+    int coop_bad_S = 0, coop_bad_spd = 0;
+    /* a grid barrier timed out mid-sample: the device rows are part-updated and
+     * unrecoverable, so training stops (hpnn_gpu_failed) instead of going on from them */
+    bool failed = false;
 };
 
 std::mutex g_mu;
@@ -152,13 +157,14 @@ BOOL ensure_model(kernel_ann *k, UINT gpu, bool keep_slots = false) {
     return TRUE;
 }
 
-BOOL ensure_momentum(kernel_ann *k) {
-    GpuModel *g = (GpuModel *)k->gpu;
+/* momentum buffers of model g, zeroed on stream st (the stream its kernel runs on, so the
+ * memset is ordered before the kernel's momentum writes) */
+BOOL ensure_momentum(kernel_ann *k, GpuModel *g, hipStream_t st) {
     for (int l = 0; l < g->L; l++) {
         layer_ann *ly = layer_of(k, l);
         size_t n = (size_t)ly->n_neurons * ly->n_inputs;
         if (!g->dW[l]) HIPCHK(hpnn_dev_malloc(&g->dW[l], sizeof(double) * n));
-        HIPCHK(hipMemsetAsync(g->dW[l], 0, sizeof(double) * n, hpnn_rt_stream(0, 0)));
+        HIPCHK(hipMemsetAsync(g->dW[l], 0, sizeof(double) * n, st));
     }
     return TRUE;
 }
@@ -236,9 +242,35 @@ extern "C" void hpnn_gpu_sync_host(kernel_ann *k) {
     gather_host(k);
 }
 
+extern "C" BOOL hpnn_gpu_failed(const kernel_ann *k) { return k && k->gpu && ((GpuModel *)k->gpu)->failed; }
+
 extern "C" void hpnn_gpu_mark_host_dirty(kernel_ann *k) {
     if (!k || !k->gpu) return;
     ((GpuModel *)k->gpu)->host_newer = true;
+}
+
+/* the slot layout of the online engine (pure: unit-tested on the CPU through ctypes,
+ * tests/test_capi_cpu.py): returns the slot count S and sets *spd (slots per device) */
+extern "C" int hpnn_online_slot_plan(int n_gpu, int n_streams, int mem_model, int env_slots, int *spd) {
+    if (env_slots > 1) { /* virtual slots on device 0: at most 2 run concurrently (hardware queues) */
+        static bool warned = false;
+        if (env_slots > 2 && !warned) {
+            NN_WARN(stderr, "HPNN_ONLINE_SLOTS=%d: capped to 2 slots on one device\n", env_slots);
+            warned = true;
+        }
+        *spd = env_slots > 2 ? 2 : env_slots;
+        return *spd;
+    }
+    int ns = n_streams;
+    if (ns > 2) {
+        static bool warned = false;
+        if (!warned) NN_WARN(stderr, "online GPU engine: %d streams per GPU requested, 2 slots per GPU used\n", ns);
+        warned = true;
+        ns = 2;
+    }
+    *spd = ns > 1 ? ns : 1;
+    const int ng = (n_gpu > 1 && mem_model == (int)CUDA_MEM_P2P) ? n_gpu : 1;
+    return ng * *spd;
 }
 
 namespace {
@@ -337,17 +369,11 @@ BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBL
     }
     if (!g->sctl) HIPCHK(hipExtMallocWithFlags((void **)&g->sctl, HPNN_ONLINE_CTL_BYTES, hipDeviceMallocUncached));
     HIPCHK(hipMemset(g->sctl, 0, HPNN_ONLINE_CTL_BYTES));
-    if (mom && !ensure_momentum(k)) return FALSE;
     for (int s = 0; s < S; s++) {
         GpuModel *m = s ? g->slots[s - 1] : g;
         HIPCHK(hipSetDevice(m->dev));
-        if (mom)
-            for (int l = 0; l < g->L; l++) {
-                layer_ann *ly = layer_of(k, l);
-                const size_t nw = (size_t)ly->n_neurons * ly->n_inputs;
-                if (!m->dW[l]) HIPCHK(hpnn_dev_malloc(&m->dW[l], sizeof(double) * nw));
-                HIPCHK(hipMemsetAsync(m->dW[l], 0, sizeof(double) * nw, m->sstream));
-            }
+        /* every slot (slot 0 included) zeroes its momentum on its own stream */
+        if (mom && !ensure_momentum(k, m, m->sstream)) return FALSE;
         HIPCHK(hipMemcpyAsync(m->x, in, sizeof(double) * k->n_inputs, hipMemcpyHostToDevice, m->sstream));
         HIPCHK(hipMemcpyAsync(m->t, out, sizeof(double) * k->n_outputs, hipMemcpyHostToDevice, m->sstream));
     }
@@ -397,29 +423,15 @@ BOOL train_sample_slots(kernel_ann *k, nn_type type, nn_train train, const DOUBL
  * rows over n_gpu x n_streams (cuda_ann.cu:533-1275).  At most two slots share a device:
  * every slot's persistent launch needs a hardware queue of its own to run concurrently with
  * the others (a process gets GPU_MAX_HW_QUEUES = 4, one of them the null stream's), and more
- * slots on one device only split the same CUs finer. */
+ * slots on one device only split the same CUs finer.  Slots go on several devices only
+ * with the P2P memory model: the exchange buffer and barrier words live on device 0 and the
+ * other devices' kernels access them directly, which needs peer mappings (runtime.cpp's
+ * probe can pick CMM / EXP on a partial topology). */
 int online_slots(int *spd) {
-    const char *e = getenv("HPNN_ONLINE_SLOTS");
-    const int v = e ? atoi(e) : 0;
-    if (v > 1) {
-        *spd = v;
-        return v;
-    }
     const nn_runtime *rt = hpnn_rt_get();
-    if (!rt) {
-        *spd = 1;
-        return 1;
-    }
-    const int ng = rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
-    int ns = (int)rt->cudas.cuda_n_streams;
-    if (ns > 2) {
-        static bool warned = false;
-        if (!warned) NN_WARN(stderr, "online GPU engine: %d streams per GPU requested, 2 slots per GPU used\n", ns);
-        warned = true;
-        ns = 2;
-    }
-    *spd = ns > 1 ? ns : 1;
-    return ng * *spd;
+    const char *e = getenv("HPNN_ONLINE_SLOTS");
+    return hpnn_online_slot_plan(rt ? (int)rt->cudas.n_gpu : 1, rt ? (int)rt->cudas.cuda_n_streams : 1,
+                                 rt ? (int)rt->cudas.mem_model : (int)CUDA_MEM_NONE, e ? atoi(e) : 0, spd);
 }
 
 }  // namespace
@@ -427,10 +439,15 @@ int online_slots(int *spd) {
 extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train train, const DOUBLE *in,
                                         const DOUBLE *out, DOUBLE lr, DOUBLE alpha, DOUBLE delta, UINT *n_iter,
                                         BOOL *ok, DOUBLE *init_err, BOOL *first_ok) {
+    if (k->gpu && ((GpuModel *)k->gpu)->failed) {
+        if (ok) *ok = FALSE;
+        return 0.0;
+    }
     {
         int spd = 1;
         const int S = online_slots(&spd);
-        if (S > 1) {
+        GpuModel *g0 = (GpuModel *)k->gpu;
+        if (S > 1 && !(g0 && g0->coop_bad_S == S && g0->coop_bad_spd == spd)) {
             if (!k->gpu && !ensure_model(k, 0, true)) return 0.0;
             GpuModel *g = (GpuModel *)k->gpu;
             /* a different slot layout: the host takes the current rows first */
@@ -442,7 +459,9 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
             if (train_sample_slots(k, type, train, in, out, lr, alpha, delta, res, &to)) {
                 g->device_newer = true;
                 if (to) {
-                    NN_ERROR(stderr, "device-spanning online kernel: a grid barrier timed out\n");
+                    NN_ERROR(stderr, "device-spanning online kernel: a grid barrier timed out; training stops\n");
+                    g->failed = true;
+                    g->device_newer = false; /* part-updated rows: never gathered into the host */
                     if (ok) *ok = FALSE;
                     return 0.0;
                 }
@@ -452,15 +471,19 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
                 if (first_ok) *first_ok = res[4] != 0.0;
                 return res[0];
             }
-            /* the net does not suit the cooperative kernel: one device */
+            /* the net does not suit the cooperative kernel: one device, and this layout is
+             * not tried again for this model (no per-sample gather / slot re-allocation) */
+            if (g->device_newer) gather_host(k);
             ensure_slots(k, 1, 1);
+            g->coop_bad_S = S;
+            g->coop_bad_spd = spd;
         }
     }
     if (!ensure_model(k, 0)) return 0.0;
     GpuModel *g = (GpuModel *)k->gpu;
     hipStream_t s = hpnn_rt_stream(0, 0);
     const bool mom = train == NN_TRAIN_BPM;
-    if (mom && !ensure_momentum(k)) return 0.0; /* momentum reset per sample */
+    if (mom && !ensure_momentum(k, g, s)) return 0.0; /* momentum reset per sample */
     hpnn_online_args a;
     fill_args(k, g, type, &a);
     a.momentum = mom;
@@ -497,8 +520,9 @@ extern "C" DOUBLE hpnn_gpu_train_sample(kernel_ann *k, nn_type type, nn_train tr
     hipMemcpyAsync(k->output.vec, g->out, sizeof(double) * k->n_outputs, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     if (grid > 0 && hpnn_online_coop_status(&a) != 0) {
-        NN_ERROR(stderr, "cooperative online kernel: a grid barrier timed out\n");
-        g->device_newer = true;
+        NN_ERROR(stderr, "cooperative online kernel: a grid barrier timed out; training stops\n");
+        g->failed = true;
+        g->device_newer = false; /* part-updated rows: never gathered into the host */
         if (ok) *ok = FALSE;
         return 0.0;
     }

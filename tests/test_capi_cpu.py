@@ -164,3 +164,30 @@ def test_capi_python_binding(tmp_path):
     c = formats.read_conf(os.path.join(d, "dump.conf"))
     assert c["hidden"] == [6] and c["type"] == "SNN"
     net.close()
+
+
+def test_online_slot_plan():
+    """online slot layout (gpu_engine.cpp hpnn_online_slot_plan): slots span several GPUs only
+    under the P2P memory model (the exchange buffer lives on GPU 0 and the other GPUs' kernels
+    access it directly); -S and HPNN_ONLINE_SLOTS are capped at 2 slots per device."""
+    import ctypes
+    from hpnn_amd._lib import lib_path
+    lib = ctypes.CDLL(lib_path())
+    f = lib.hpnn_online_slot_plan
+    f.restype = ctypes.c_int
+    NONE, EXP, P2P, CMM = 0, 1, 2, 3
+
+    def plan(n_gpu, n_streams, mem, env=0):
+        spd = ctypes.c_int(0)
+        S = f(n_gpu, n_streams, mem, env, ctypes.byref(spd))
+        return S, spd.value
+
+    assert plan(1, 1, NONE) == (1, 1)
+    assert plan(4, 1, P2P) == (4, 1)
+    assert plan(4, 2, P2P) == (8, 2)
+    assert plan(4, 5, P2P) == (8, 2)
+    for mem in (NONE, EXP, CMM):  # no peer mappings: one device only
+        assert plan(4, 1, mem) == (1, 1)
+        assert plan(4, 2, mem) == (2, 2)
+    assert plan(1, 1, NONE, env=2) == (2, 2)
+    assert plan(8, 1, P2P, env=6) == (2, 2)  # virtual slots on device 0, capped
