@@ -261,7 +261,11 @@ extern "C" int hpnn_online_slot_plan(int n_gpu, int n_streams, int mem_model, in
         *spd = env_slots > 2 ? 2 : env_slots;
         return *spd;
     }
-    int ns = n_streams;
+    const int ng = (n_gpu > 1 && mem_model == (int)CUDA_MEM_P2P) ? n_gpu : 1;
+    /* -S on ONE device is a no-op: two stream slots only split the same CUs finer and pay the
+     * system-scope exchange (4096-4096-230 BPM: 2745 it/s on one slot vs 2618 with -S 2,
+     * profiles/r4/a_online_engine.jsonl); HPNN_ONLINE_SLOTS still forces virtual slots (tests) */
+    int ns = ng > 1 ? n_streams : 1;
     if (ns > 2) {
         static bool warned = false;
         if (!warned) NN_WARN(stderr, "online GPU engine: %d streams per GPU requested, 2 slots per GPU used\n", ns);
@@ -269,7 +273,6 @@ extern "C" int hpnn_online_slot_plan(int n_gpu, int n_streams, int mem_model, in
         ns = 2;
     }
     *spd = ns > 1 ? ns : 1;
-    const int ng = (n_gpu > 1 && mem_model == (int)CUDA_MEM_P2P) ? n_gpu : 1;
     return ng * *spd;
 }
 

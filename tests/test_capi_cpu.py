@@ -169,7 +169,8 @@ def test_capi_python_binding(tmp_path):
 def test_online_slot_plan():
     """online slot layout (gpu_engine.cpp hpnn_online_slot_plan): slots span several GPUs only
     under the P2P memory model (the exchange buffer lives on GPU 0 and the other GPUs' kernels
-    access it directly); -S and HPNN_ONLINE_SLOTS are capped at 2 slots per device."""
+    access it directly); -S and HPNN_ONLINE_SLOTS are capped at 2 slots per device, and -S is a no-op on one
+    device (two slots there measured slower, profiles/r4/a_online_engine.jsonl)."""
     import ctypes
     from hpnn_amd._lib import lib_path
     lib = ctypes.CDLL(lib_path())
@@ -183,11 +184,13 @@ def test_online_slot_plan():
         return S, spd.value
 
     assert plan(1, 1, NONE) == (1, 1)
+    assert plan(1, 2, P2P) == (1, 1)
     assert plan(4, 1, P2P) == (4, 1)
     assert plan(4, 2, P2P) == (8, 2)
     assert plan(4, 5, P2P) == (8, 2)
-    for mem in (NONE, EXP, CMM):  # no peer mappings: one device only
+    for mem in (NONE, EXP, CMM):  # no peer mappings: one device only, where -S is a no-op
         assert plan(4, 1, mem) == (1, 1)
-        assert plan(4, 2, mem) == (2, 2)
+        assert plan(4, 2, mem) == (1, 1)
+    assert plan(1, 2, NONE) == (1, 1)
     assert plan(1, 1, NONE, env=2) == (2, 2)
     assert plan(8, 1, P2P, env=6) == (2, 2)  # virtual slots on device 0, capped

@@ -173,8 +173,8 @@ def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots
     Every slot owns the rows j with (j mod total workgroups) in its range; the host gathers
     each row from its owner when the kernel is dumped.
     "streams": train_nn -S 2 without the variable -- the reference's rows over n_gpu x
-    n_streams (libhpnn.c:471-505): two slots on the device, each on one of the runtime's
-    two streams."""
+    n_streams (libhpnn.c:471-505); on ONE device it is a no-op (two slots there measured
+    slower, profiles/r4/a_online_engine.jsonl), so it must match the one-slot run."""
     n_in, hid, n_out = dims
     runs = {"cpu": (True, None, []), "one": (False, None, []),
             "slots": (False, {"HPNN_ONLINE_SLOTS": str(slots)}, []), "streams": (False, None, ["-S", "2"])}
@@ -185,9 +185,8 @@ def test_online_device_spanning_matches_single(tmp_path, net, train, dims, slots
                            outputs=n_out, train=train, sample_dir="./samples", test_dir="./samples", lr=0.01)
         out = _run([os.path.join(BIN, "train_nn"), "-vv"] + flags + ["nn.conf"], d, cpu=cpu, extra_env=env)
         assert out.count("TRAINING FILE") == 3
-        assert ("rows over 2 slots" in out) == (tag in ("slots", "streams")), out[-2000:]
-        if tag == "streams":
-            assert "runtime streams" in out, out[-2000:]
+        # -S 2 on one device is a documented no-op (one slot); HPNN_ONLINE_SLOTS forces two
+        assert ("rows over 2 slots" in out) == (tag == "slots"), out[-2000:]
     ks = {t: formats.read_kernel(str(tmp_path / t / "kernel.opt"))["weights"] for t in runs}
     for a, b, c, e in zip(ks["cpu"], ks["one"], ks["slots"], ks["streams"]):
         assert np.abs(c - b).max() < 1e-9, np.abs(c - b).max()
