@@ -24,7 +24,7 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics $(I
 HIPFLAGS  += $(if $(ABLATIONS),-DHPNN_ABLATIONS)
 LDFLAGS   := -L$(ROCM)/lib -lamdhip64 -fopenmp
 
-CORE_SRC  := $(wildcard csrc/core/*.cpp) $(wildcard csrc/cpu/*.cpp) $(wildcard csrc/dist/*.cpp) csrc/gpu/gpu_engine.cpp csrc/gpu/tp_engine.cpp
+CORE_SRC  := $(wildcard csrc/core/*.cpp) $(wildcard csrc/cpu/*.cpp) $(wildcard csrc/dist/*.cpp) csrc/gpu/gpu_engine.cpp csrc/gpu/tp_engine.cpp csrc/gpu/bplan.cpp
 HIP_SRC   := $(wildcard csrc/gpu/*.hip) $(wildcard csrc/dist/*.hip)
 CORE_OBJ  := $(patsubst %.cpp,$(BUILD)/%.o,$(CORE_SRC))
 HIP_OBJ   := $(patsubst %.hip,$(BUILD)/%.o,$(HIP_SRC))

@@ -208,6 +208,45 @@ size_t HpnnSamples::load(const std::vector<UINT> &order, UINT ni, UINT no, int t
     return order.size();
 }
 
+/* write n records from memory: the same pack file (names "s%08u"), for data generated in a
+ * program (synthetic benchmark sets) rather than read from sample files */
+static BOOL write_pack(const CHAR *filename, const std::vector<std::string> &names, const DOUBLE *X, const DOUBLE *T,
+                       UINT n, UINT ni, UINT no) {
+    std::string nm;
+    for (const auto &s : names) {
+        nm += s;
+        nm.push_back('\0');
+    }
+    FILE *fp = fopen(filename, "wb");
+    if (!fp) {
+        NN_ERROR(stderr, "can't write pack file %s\n", filename);
+        return FALSE;
+    }
+    const UINT hdr[4] = {n, ni, no, 0};
+    const UINT64 nb = nm.size();
+    const size_t nx = (size_t)n * ni, nt = (size_t)n * no;
+    UINT64 h = hpnn_fnv1a(X, nx * 8, HPNN_FNV_SEED);
+    h = hpnn_fnv1a(T, nt * 8, h);
+    bool ok = fwrite(HPNN_PACK_MAGIC, 1, 8, fp) == 8 && fwrite(hdr, 4, 4, fp) == 4 && fwrite(&nb, 8, 1, fp) == 1 &&
+              (nb == 0 || fwrite(nm.data(), 1, nb, fp) == nb) && fwrite(X, 8, nx, fp) == nx &&
+              fwrite(T, 8, nt, fp) == nt && fwrite(&h, 8, 1, fp) == 1;
+    ok = (fclose(fp) == 0) && ok;
+    if (ok) NN_OUT(stdout, "packed %u samples (%u -> %u) into %s\n", n, ni, no, filename);
+    return ok ? TRUE : FALSE;
+}
+
+extern "C" BOOL _NN(pack, arrays)(const CHAR *filename, const DOUBLE *X, const DOUBLE *T, UINT n, UINT n_in,
+                                  UINT n_out) {
+    if (!filename || !X || !T || n == 0 || n_in == 0 || n_out == 0) return FALSE;
+    std::vector<std::string> names(n);
+    char b[32];
+    for (UINT i = 0; i < n; i++) {
+        snprintf(b, sizeof b, "s%08u", i);
+        names[i] = b;
+    }
+    return write_pack(filename, names, X, T, n, n_in, n_out);
+}
+
 extern "C" BOOL _NN(pack, samples)(const CHAR *dir, const CHAR *filename) {
     HpnnSamples s;
     if (!dir || !filename || !s.open(dir) || s.packed) {
@@ -220,24 +259,5 @@ extern "C" BOOL _NN(pack, samples)(const CHAR *dir, const CHAR *filename) {
     std::vector<std::string> kept;
     UINT ni = 0, no = 0;
     if (load_dir(s.dir, s.names, order, ni, no, omp_get_max_threads(), X, T, &kept) == 0) return FALSE;
-    std::string nm;
-    for (const auto &n : kept) {
-        nm += n;
-        nm.push_back('\0');
-    }
-    FILE *fp = fopen(filename, "wb");
-    if (!fp) {
-        NN_ERROR(stderr, "can't write pack file %s\n", filename);
-        return FALSE;
-    }
-    const UINT hdr[4] = {(UINT)kept.size(), ni, no, 0};
-    const UINT64 nb = nm.size();
-    UINT64 h = hpnn_fnv1a(X.data(), X.size() * 8, HPNN_FNV_SEED);
-    h = hpnn_fnv1a(T.data(), T.size() * 8, h);
-    bool ok = fwrite(HPNN_PACK_MAGIC, 1, 8, fp) == 8 && fwrite(hdr, 4, 4, fp) == 4 && fwrite(&nb, 8, 1, fp) == 1 &&
-              (nb == 0 || fwrite(nm.data(), 1, nb, fp) == nb) && fwrite(X.data(), 8, X.size(), fp) == X.size() &&
-              fwrite(T.data(), 8, T.size(), fp) == T.size() && fwrite(&h, 8, 1, fp) == 1;
-    ok = (fclose(fp) == 0) && ok;
-    if (ok) NN_OUT(stdout, "packed %zu samples (%u -> %u) into %s\n", kept.size(), ni, no, filename);
-    return ok ? TRUE : FALSE;
+    return write_pack(filename, kept, X.data(), T.data(), (UINT)kept.size(), ni, no);
 }

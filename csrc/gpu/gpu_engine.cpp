@@ -23,7 +23,9 @@
 #include <libhpnn/xar.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -33,6 +35,7 @@
 #include "../core/runtime_internal.h"
 #include "engine.h"
 #include "kernels.h"
+#include "bplan.h"
 
 #define HIPCHK(x)                                                                           \
     do {                                                                                    \
@@ -558,371 +561,202 @@ extern "C" BOOL hpnn_gpu_forward(kernel_ann *k, nn_type type, const DOUBLE *in) 
 /* ====================================================================== */
 namespace {
 
-inline int pad32(int v) { return (v + 31) / 32 * 32; }
-inline int pad128(int v) { return (v + 127) / 128 * 128; }
+inline int pad_rows(int v, int m) { return (v + m - 1) / m * m; }
 
-/* split-K factor of the weight-gradient GEMM: about one workgroup per CU (256 on
- * MI355X; 48 splits measured fastest for MNIST's G0) so every CU streams the same share (gemm_tn takes uneven 64-row units per
- * split), >= 512 batch rows per split, a multiple of 8 for the XCD-aware block order.
- * Mirrors hpnn_amd/models/mlp.py:MLP._pick_splits (HPNN_TN_SPLITS forces a value). */
-int tn_tile_m(int K) {
-    return K % 128 == 0 ? 128 : (K % 160 == 0 ? 160 : (K % 96 == 0 ? 96 : (K % 64 == 0 ? 64 : 32)));
-}
-int pick_splits(int Np, int Kp, int Bp) {
-    const int tn = (Np % 128 == 0) ? 128 : (Np % 64 == 0 ? 64 : 32);
-    const int tm = tn_tile_m(Kp);
-    const int tiles = (Np / tn) * (Kp / tm);
-    static const int forced = [] { const char *e = getenv("HPNN_TN_SPLITS"); return e ? atoi(e) : 0; }();
-    if (forced > 0) {
-        const int m = Bp / 64;
-        return forced < m ? forced : (m > 0 ? m : 1);
+/* the resident training set on one device, in the layout the engine's kernels read: x =
+ * the main input (row-major, or fragment-major for the tile front), xg = an optional
+ * fragment-major 8-bit copy (first-layer gradient of mode 'x'); row r of a minibatch starts
+ * r * row_bytes in (fragment-major layouts keep that for r % 32 == 0) */
+struct XSet {
+    void *x = nullptr, *xg = nullptr;
+    size_t row_bytes = 0, row_bytes_g = 0;
+    int u8 = 0;
+    float scale = 1.f;
+    void release() {
+        hpnn_dev_free(x);
+        hpnn_dev_free(xg);
+        x = xg = nullptr;
     }
-    /* 256x256 tiles: enough splits for the 8-phase TN kernel (>= 256 workgroups, an even
-     * number of 64-row units per split), as MLP._splits_8ph */
-    static const int tn8 = [] { const char *e = getenv("HPNN_TN_8PH"); return !(e && e[0] == '0'); }();
-    if (tn8 && Np % 256 == 0 && Kp % 256 == 0 && Bp % 128 == 0) {
-        const int t8 = (Np / 256) * (Kp / 256), units = Bp / 64, s0 = (256 + t8 - 1) / t8;
-        for (int s8 = s0; s8 <= 2 * s0; s8++)
-            if (units % s8 == 0 && (units / s8) % 2 == 0) return s8;
-    }
-    int s = (256 + tiles / 2) / (tiles > 0 ? tiles : 1);
-    const int maxs = Bp / 512;
-    if (s > maxs) s = maxs;
-    if (s >= 8) s -= s % 8;
-    return s < 1 ? 1 : s;
-}
+};
 
 BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t s);
 
+/* round-to-nearest-even FP32 -> BF16 bits (the kernels' rounding) */
+inline uint16_t bf16_bits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+}
+
+/* host [rows][cols] -> fragment-major [rows_p/32][cols_p/16][64][8] (hpnn_amd.ops.to_fragment_major:
+ * lane 16 g + r of fragment (t, cb) holds A[32 t + 8 g + j][16 cb + r], j < 8), zero padded */
+template <typename E, typename Cvt>
+std::vector<E> to_fragment_major(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, Cvt cvt) {
+    std::vector<E> out((size_t)rows_p * cols_p, (E)0);
+    const int nbc = cols_p / 16;
+    for (int r = 0; r < rows; r++) {
+        const int t = r / 32, g = (r % 32) / 8, j = r % 8;
+        for (int c = 0; c < cols; c++) {
+            const size_t idx = ((((size_t)t * nbc + c / 16) * 64) + 16 * g + c % 16) * 8 + j;
+            out[idx] = cvt(src[(size_t)r * cols + c]);
+        }
+    }
+    return out;
+}
+
+/* BF16 batched engine: an adapter of the library's batched plan (bplan.h, the same object
+ * hpnn_amd.models.MLP binds) to the precision-generic drivers below */
 struct Batched {
-    /* what the precision-generic drivers (train_batched, train_dp, train_dp_mp) need */
     typedef float target_t; /* dense targets, uploaded once */
     typedef float grad_t;   /* flat gradient buffer (the all-reduce payload) */
-    static constexpr size_t xelem = 2;
     static constexpr hpnn_comm_dtype comm_dt = HPNN_DT_F32;
     static const char *name() { return "bf16"; }
-    static BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t st) {
-        return upload_bf16(src, rows, cols, rows_p, cols_p, dst, st);
-    }
+    static constexpr size_t ACC_BYTES = HPNN_STAT_SLOTS * HPNN_STAT_STRIDE * 4;
     static int reduce_sum(grad_t *buf, int G, size_t count, hipStream_t st) {
         return hpnn_reduce_slabs(buf, G, (long)count, (long)count, buf, st);
     }
-    int L = 0, Bp = 0, n_out = 0, type = 2;
-    int M[16], N[16], Kp[16], Np[16], S[16];
-    float *W32[16] = {0}, *V32[16] = {0}, *slab[16] = {0};
-    void *Wb[16] = {0}, *Wt[16] = {0}, *H[16] = {0}, *D[16] = {0};
-    float *Z = nullptr;
-    /* loss / accuracy slots: HPNN_STAT_SLOTS x HPNN_STAT_STRIDE floats ([0] loss, [1] hits) */
-    float *acc = nullptr;
-    static constexpr size_t ACC_BYTES = HPNN_STAT_SLOTS * HPNN_STAT_STRIDE * 4;
-    /* fused n_in-128-64-(<=32) paths: fused_x = hpnn_mlp3_fused (X -> delta1 in one
-     * kernel, kernels_mlp3x.hip), else gemm_nt + hpnn_mlp3_mid (kernels_mlp3.hip) */
-    bool fused = false, fused_x = false;
-    int mid_grid = 0, mid_groups = 1;
-    float *midslab = nullptr, *midtmp = nullptr, *G12 = nullptr;
-    void *W0f = nullptr; /* fragment-major BF16 W0 (fused_x) */
+    hpnn::BPlan p;
+    int L = 0, Bp = 0;
+    float *acc = nullptr, *gflat = nullptr;
+    size_t goff[17] = {0};
+    bool fm_ok = true; /* minibatch starts are multiples of 32 rows: fragment-major inputs */
+    bool own_flat = false; /* the plan owns its flat buffer (loopback re-points it) */
     hipStream_t s = nullptr;
 
     ~Batched() {
         if (s) hipStreamSynchronize(s);
-        for (int l = 0; l < 16; l++) {
-            hpnn_dev_free(W32[l]);
-            hpnn_dev_free(V32[l]);
-            hpnn_dev_free(slab[l]);
-            hpnn_dev_free(Wb[l]);
-            hpnn_dev_free(Wt[l]);
-            hpnn_dev_free(H[l]);
-            hpnn_dev_free(D[l]);
-        }
-        hpnn_dev_free(Z);
-        hpnn_dev_free(acc);
-        hpnn_dev_free(midslab);
-        hpnn_dev_free(midtmp);
-        hpnn_dev_free(G12);
-        hpnn_dev_free(W0f);
-        if (own_flat) hpnn_dev_free(gflat);
     }
 
-    /* sum the stat slots: returns (loss sum, hits) */
-    BOOL read_stats(double *loss, unsigned int *hits) {
-        std::vector<float> h(HPNN_STAT_SLOTS * HPNN_STAT_STRIDE);
-        HIPCHK(hipMemcpyAsync(h.data(), acc, ACC_BYTES, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        double l = 0.0;
-        unsigned int c = 0;
-        for (int i = 0; i < HPNN_STAT_SLOTS; i++) {
-            l += h[(size_t)i * HPNN_STAT_STRIDE];
-            unsigned int u;
-            memcpy(&u, &h[(size_t)i * HPNN_STAT_STRIDE + 1], 4);
-            c += u;
-        }
-        *loss = l;
-        *hits = c;
-        return TRUE;
-    }
+    BOOL read_stats(double *loss, unsigned int *hits) { return p.read_stats(loss, hits, s) == 0; }
 
-    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st) {
+    /* allow_fm: every minibatch (shard) this net trains starts at a row multiple of 32;
+     * fused: the plan's structure request (-1 auto, 0 per-layer only) */
+    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st, bool allow_fm = true, int fused = -1) {
         s = st;
         L = (int)k->n_hiddens + 1;
-        Bp = pad128(B);
-        n_out = (int)k->n_outputs;
-        type = t == NN_TYPE_ANN ? 0 : (t == NN_TYPE_LNN ? 1 : 2);
+        std::vector<int> sizes(L + 1);
+        sizes[0] = (int)k->n_inputs;
+        for (int l = 0; l < L; l++) sizes[l + 1] = (int)layer_of(k, l)->n_neurons;
+        const int type = t == NN_TYPE_ANN ? 0 : (t == NN_TYPE_LNN ? 1 : 2);
+        std::string err;
+        int rc = p.configure(sizes.data(), L, type, B, momentum, fused, nullptr, 512, true, &err);
+        if (!rc && !allow_fm && p.mode == 't') /* the tile front reads fragment-major rows only */
+            rc = p.configure(sizes.data(), L, type, B, momentum, 'x', nullptr, 512, true, &err);
+        if (rc) {
+            NN_ERROR(stderr, "batched plan: %s (%d)\n", err.c_str(), rc);
+            return FALSE;
+        }
+        fm_ok = allow_fm;
+        if (p.allocate(s)) return FALSE;
+        Bp = p.Bp;
         for (int l = 0; l < L; l++) {
             layer_ann *ly = layer_of(k, l);
-            M[l] = (int)ly->n_inputs;
-            N[l] = (int)ly->n_neurons;
-            Kp[l] = pad32(M[l]);
-            Np[l] = pad32(N[l]);
-            S[l] = pick_splits(Np[l], Kp[l], Bp);
-            const size_t nw = (size_t)Np[l] * Kp[l];
-            HIPCHK(hpnn_dev_malloc(&W32[l], nw * 4));
-            HIPCHK(hpnn_dev_malloc(&Wb[l], nw * 2));
-            HIPCHK(hpnn_dev_malloc(&Wt[l], nw * 2));
-            HIPCHK(hpnn_dev_malloc(&slab[l], nw * 4 * S[l]));
-            if (momentum) {
-                HIPCHK(hpnn_dev_malloc(&V32[l], nw * 4));
-                HIPCHK(hipMemsetAsync(V32[l], 0, nw * 4, s));
-            }
-            HIPCHK(hpnn_dev_malloc(&D[l], (size_t)Bp * Np[l] * 2));
-            if (l < L - 1) HIPCHK(hpnn_dev_malloc(&H[l], (size_t)Bp * Np[l] * 2));
-            /* FP64 host -> padded FP32 master */
-            std::vector<float> tmp(nw, 0.f);
-            for (int n = 0; n < N[l]; n++)
-                for (int m = 0; m < M[l]; m++) tmp[(size_t)n * Kp[l] + m] = (float)ly->weights[(size_t)n * M[l] + m];
-            HIPCHK(hipMemcpyAsync(W32[l], tmp.data(), nw * 4, hipMemcpyHostToDevice, s));
+            const int M = (int)ly->n_inputs, N = (int)ly->n_neurons, Kp = p.Kp[l];
+            std::vector<float> tmp((size_t)p.Np[l] * Kp, 0.f); /* FP64 host -> padded FP32 master */
+            for (int n = 0; n < N; n++)
+                for (int m = 0; m < M; m++) tmp[(size_t)n * Kp + m] = (float)ly->weights[(size_t)n * M + m];
+            HIPCHK(hipMemcpyAsync(p.W32[l], tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
-            if (hpnn_cast_weights(W32[l], Wb[l], Wt[l], Np[l], Kp[l], s)) return FALSE;
         }
-        HIPCHK(hpnn_dev_malloc(&Z, (size_t)Bp * Np[L - 1] * 4));
-        HIPCHK(hpnn_dev_malloc(&acc, ACC_BYTES));
-        HIPCHK(hipMemsetAsync(acc, 0, ACC_BYTES, s));
-        fused = (L == 3 && Np[0] == 128 && Np[1] == 64 && Np[2] == 32);
-        fused_x = fused && (Kp[0] == 256 || Kp[0] == 512 || Kp[0] == 800 || Kp[0] == 832 || Kp[0] == 896);
-        if (fused) {
-            const int slab_f = hpnn_mlp3_slab_floats();
-            mid_grid = fused_x ? hpnn_mlp3_fused_grid(Bp, 0) : (Bp / 64 < 512 ? Bp / 64 : 512);
-            if (mid_grid <= 0) return FALSE;
-            mid_groups = mid_grid < 16 ? mid_grid : 16;
-            HIPCHK(hpnn_dev_malloc(&midslab, (size_t)mid_grid * slab_f * 4));
-            HIPCHK(hpnn_dev_malloc(&midtmp, (size_t)16 * slab_f * 4));
-            HIPCHK(hpnn_dev_malloc(&G12, (size_t)slab_f * 4));
-            if (fused_x) {
-                HIPCHK(hpnn_dev_malloc(&W0f, (size_t)Np[0] * Kp[0] * 2));
-                hpnn_upd_layer c0 = {W32[0], nullptr, W32[0], 0, Wb[0], Wt[0], W0f, 1, Np[0], Kp[0]};
-                if (hpnn_sgd_update_multi(&c0, 1, 0.f, 0.f, 0.f, 0, s)) return FALSE; /* lr 0: a cast */
-            }
-        }
+        if (p.cast_weights(s)) return FALSE;
+        acc = p.stats;
+        gflat = p.gflat;
+        memcpy(goff, p.goff, sizeof goff);
+        NN_DBG(stdout, "batched plan: mode %c, Bp %d, G0 splits %d\n", p.mode ? p.mode : '-', p.Bp, p.S[0]);
         return TRUE;
     }
 
-    BOOL forward(const void *X) {
-        for (int l = 0; l < L; l++) {
-            const void *A = l ? H[l - 1] : X;
-            const bool last = l == L - 1;
-            int r = hpnn_gemm_nt_bf16(A, Kp[l], Wb[l], Kp[l], last ? (void *)Z : H[l], Np[l], nullptr, 0, Bp, Np[l],
-                                      Kp[l], last ? HPNN_EPI_NONE : HPNN_EPI_ACT, last ? 1 : 0, s);
-            if (r) {
-                NN_ERROR(stderr, "gemm_nt (fwd layer %d) failed: %d\n", l, r);
-                return FALSE;
-            }
+    /* the training set in the plan's input layout: fragment-major for the tile front, plus a
+     * fragment-major byte copy for mode 'x'; data that are all integers 0..255 (the reference's
+     * pmnist pixels) go as bytes -- the same values, half the bytes of BF16 */
+    BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, XSet *xs) {
+        const int lay = fm_ok ? p.input_layout() : 0, Kp0 = p.Kp[0];
+        rows_p = pad_rows(rows_p, 32);
+        bool u8 = lay != 0;
+        for (size_t i = 0; u8 && i < (size_t)rows * cols; i++) {
+            const DOUBLE v = src[i];
+            u8 = v >= 0.0 && v <= 255.0 && v == (DOUBLE)(int)v;
         }
-        return TRUE;
-    }
-
-    BOOL step_fused(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
-        const float scale = 1.0f / (float)n_valid;
-        const float t_lo = type == 2 ? 0.f : -1.f;
-        const int slab_f = hpnn_mlp3_slab_floats();
-        int r;
-        if (fused_x) {
-            r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab, acc,
-                                (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, 0, s);
-            r = r > 0 ? 0 : (r ? r : -1);
-        } else {
-            r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0], HPNN_EPI_ACT, 0,
-                                  s);
-            if (!r)
-                r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab, acc,
-                                  (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2], mid_grid,
-                                  s);
-        }
-        /* first reduction pass of the [G1 | G2] block slabs (the optimizer sums the groups) on
-         * tail workgroups appended to the G0 GEMM grid: one launch */
-        if (!r)
-            r = hpnn_gemm_tn_bf16_reduce(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], midslab,
-                                         mid_grid, slab_f, slab_f, mid_groups, midtmp, s);
-        if (!r) {
-            const long n1 = (long)Np[1] * Kp[1];
-            hpnn_upd_layer u[3] = {
-                {W32[0], V32[0], slab[0], (long)Np[0] * Kp[0], Wb[0], Wt[0], W0f, S[0], Np[0], Kp[0]},
-                {W32[1], V32[1], midtmp, slab_f, Wb[1], Wt[1], nullptr, mid_groups, Np[1], Kp[1]},
-                {W32[2], V32[2], midtmp + n1, slab_f, Wb[2], Wt[2], nullptr, mid_groups, Np[2], Kp[2]}};
-            r = hpnn_sgd_update_multi(u, 3, lr, alpha, scale, mom ? 1 : 0, s);
-        }
-        if (r) NN_ERROR(stderr, "fused step failed: %d\n", r);
-        return r == 0;
-    }
-
-    BOOL step(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
-        const BOOL ok = step_launch(X, T, ldt, n_valid, lr, alpha, mom);
-        return ok && hpnn_debug_check("batched training step") == 0;
-    }
-
-    BOOL step_launch(const void *X, const float *T, int ldt, int n_valid, float lr, float alpha, bool mom) {
-        if (fused) return step_fused(X, T, ldt, n_valid, lr, alpha, mom);
-        if (!forward(X)) return FALSE;
-        if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
-                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
-            return FALSE;
-        for (int l = L - 1; l >= 1; l--) {
-            /* D[l-1] = (D[l] . W_l) * f'(H[l-1]);  W_l^T is [Kp[l] x Np[l]] */
-            int r = hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp,
-                                      Np[l - 1], Np[l], HPNN_EPI_DACT, 0, s);
-            if (r) {
-                NN_ERROR(stderr, "gemm_nt (bwd layer %d) failed: %d\n", l, r);
-                return FALSE;
-            }
-        }
-        /* every delta above used the pre-update weights: all gradients, then ONE update launch
-         * for the layers whose step did not already run in the gradient GEMM's epilogue
-         * (one-split layers of 256x256 tiles: hpnn_gemm_tn8_update, as MLP._tn_update_ok) */
-        static const int tn_upd = [] { const char *e = getenv("HPNN_TN_UPD"); return !(e && e[0] == '0'); }();
-        hpnn_upd_layer u[HPNN_UPD_MAX];
-        int nu = 0;
-        const float scale = 1.0f / (float)n_valid;
-        for (int l = 0; l < L; l++) {
-            const void *Hin = l ? H[l - 1] : X;
-            if (tn_upd && S[l] == 1 && Np[l] % 256 == 0 && Kp[l] % 256 == 0 && Bp % 128 == 0 &&
-                hpnn_gemm_tn8_update(D[l], Np[l], Hin, Kp[l], Np[l], Kp[l], Bp, W32[l], V32[l], Wb[l], Wt[l], lr,
-                                     alpha, scale, mom ? 1 : 0, s) == 0)
-                continue;
-            int r = hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s);
-            if (r) {
-                NN_ERROR(stderr, "gemm_tn (layer %d) failed: %d\n", l, r);
-                return FALSE;
-            }
-            if (L <= HPNN_UPD_MAX)
-                u[nu++] = {W32[l], V32[l], slab[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], nullptr, S[l], Np[l], Kp[l]};
-            else if (hpnn_sgd_update(W32[l], V32[l], slab[l], S[l], (long)Np[l] * Kp[l], Wb[l], Wt[l], Np[l], Kp[l],
-                                     lr, alpha, scale, mom ? 1 : 0, s))
-                return FALSE;
-        }
-        if (nu && hpnn_sgd_update_multi(u, nu, lr, alpha, scale, mom ? 1 : 0, s)) return FALSE;
-        return TRUE;
-    }
-
-    /* ---- data-parallel split of a step: gradients into one flat FP32 buffer (the
-     * all-reduce payload), then the update from it ---- */
-    float *gflat = nullptr; /* sum over this replica's samples, [layer 0 | layer 1 | ...] */
-    size_t goff[17] = {0};
-    BOOL alloc_flat(float *external = nullptr) {
-        goff[0] = 0;
-        for (int l = 0; l < L; l++) goff[l + 1] = goff[l] + (size_t)Np[l] * Kp[l];
-        if (external) {
-            gflat = external;
-            own_flat = false;
+        xs->u8 = u8 ? 1 : 0;
+        xs->scale = 1.f;
+        auto put = [&](const void *h, size_t bytes, void **dst) -> BOOL {
+            HIPCHK(hpnn_dev_malloc(dst, bytes));
+            HIPCHK(hipMemcpyAsync(*dst, h, bytes, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
             return TRUE;
-        }
-        HIPCHK(hpnn_dev_malloc(&gflat, goff[L] * 4));
-        own_flat = true;
-        return TRUE;
-    }
-    bool own_flat = false;
-    size_t flat_count() const { return goff[L]; }
-
-    /* forward + backward into the flat buffer; ready(lo, hi) is called as soon as the
-     * gradients of layers lo..hi (contiguous in gflat) are final -- last layers first --
-     * so the caller can start their all-reduce while the lower layers are computed */
-    template <class Ready>
-    BOOL grads(const void *X, const float *T, int ldt, int n_valid, Ready &&ready) {
-        const float t_lo = type == 2 ? 0.f : -1.f;
-        int r = 0;
-        if (fused) {
-            const int slab_f = hpnn_mlp3_slab_floats();
-            if (fused_x) {
-                r = hpnn_mlp3_fused(X, Kp[0], Kp[0], W0f, Wb[1], Wb[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab,
-                                    acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, mid_grid, 0, s);
-                r = r > 0 ? 0 : (r ? r : -1);
-            } else {
-                r = hpnn_gemm_nt_bf16(X, Kp[0], Wb[0], Kp[0], H[0], Np[0], nullptr, 0, Bp, Np[0], Kp[0],
-                                      HPNN_EPI_ACT, 0, s);
-                if (!r)
-                    r = hpnn_mlp3_mid(H[0], Wb[1], Wt[1], Wb[2], Wt[2], nullptr, T, ldt, 1.f, t_lo, D[0], midslab,
-                                      acc, (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, Np[0], Np[1], Np[2],
-                                      mid_grid, s);
+        };
+        if (lay == 1) {
+            if (u8) {
+                auto h = to_fragment_major<uint8_t>(src, rows, cols, rows_p, Kp0, [](DOUBLE v) { return (uint8_t)v; });
+                xs->row_bytes = Kp0;
+                return put(h.data(), h.size(), &xs->x);
             }
-            /* [G1 | G2] slab rows are exactly layers 1, 2 of the flat buffer: final first */
-            if (!r) r = hpnn_reduce_slabs2(midslab, mid_grid, slab_f, slab_f, midtmp, gflat + goff[1], s);
-            if (!r && !ready(1, 2)) r = -8;
-            if (!r) r = hpnn_gemm_tn_bf16(D[0], Np[0], X, Kp[0], slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], s);
-            if (!r) r = hpnn_reduce_slabs(slab[0], S[0], (long)Np[0] * Kp[0], (long)Np[0] * Kp[0], gflat, s);
-            if (!r && !ready(0, 0)) r = -8;
-            if (r) NN_ERROR(stderr, "fused gradients failed: %d\n", r);
-            return r == 0;
+            auto h = to_fragment_major<uint16_t>(src, rows, cols, rows_p, Kp0,
+                                                 [](DOUBLE v) { return bf16_bits((float)v); });
+            xs->row_bytes = (size_t)Kp0 * 2;
+            return put(h.data(), h.size() * 2, &xs->x);
         }
-        if (!forward(X)) return FALSE;
-        if (hpnn_output_delta(Z, Np[L - 1], T, ldt, nullptr, 0.f, 0.f, D[L - 1], Np[L - 1], nullptr, 0, acc,
-                              (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
-            return FALSE;
-        /* layer by layer from the top: the delta for layer l-1 (pre-update W_l), then
-         * layer l's gradient into its bucket -- its all-reduce overlaps the layers below */
-        for (int l = L - 1; l >= 0; l--) {
-            if (l >= 1 && hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp,
-                                            Np[l - 1], Np[l], HPNN_EPI_DACT, 0, s))
-                return FALSE;
-            const void *Hin = l ? H[l - 1] : X;
-            if (S[l] == 1) { /* one split: straight into the bucket */
-                if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], gflat + goff[l], Kp[l], Np[l], Kp[l], Bp, 1, s))
-                    return FALSE;
-            } else if (hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s) ||
-                       hpnn_reduce_slabs(slab[l], S[l], (long)Np[l] * Kp[l], (long)Np[l] * Kp[l], gflat + goff[l], s))
-                return FALSE;
-            if (!ready(l, l)) return FALSE;
+        if (!upload_bf16(src, rows, cols, rows_p, Kp0, &xs->x, s)) return FALSE;
+        xs->row_bytes = (size_t)Kp0 * 2;
+        if (lay == 2 && u8) {
+            auto h = to_fragment_major<uint8_t>(src, rows, cols, rows_p, Kp0, [](DOUBLE v) { return (uint8_t)v; });
+            xs->row_bytes_g = Kp0;
+            return put(h.data(), h.size(), &xs->xg);
         }
+        xs->u8 = 0;
         return TRUE;
     }
-    BOOL grads(const void *X, const float *T, int ldt, int n_valid) {
-        return grads(X, T, ldt, n_valid, [](int, int) { return true; });
-    }
-    /* the (lo, hi) layer buckets grads() reports, in order */
-    std::vector<std::pair<int, int>> buckets() const {
-        std::vector<std::pair<int, int>> v;
-        if (fused) return {{1, 2}, {0, 0}};
-        for (int l = L - 1; l >= 0; l--) v.push_back({l, l});
+    hpnn::XIn at(const XSet &xs, long row) const {
+        hpnn::XIn v;
+        v.x = (const char *)xs.x + row * xs.row_bytes;
+        v.xg = xs.xg ? (const char *)xs.xg + row * xs.row_bytes_g : nullptr;
+        v.u8 = xs.u8;
+        v.scale = xs.scale;
         return v;
     }
 
-    /* update every layer from a flat gradient buffer G (this replica's gflat after the
-     * all-reduce, or the loopback sum) with scale = 1 / (samples of all replicas) */
-    BOOL update_flat(const float *G, float lr, float alpha, float scale, bool mom) {
-        hpnn_upd_layer u[HPNN_UPD_MAX];
-        if (L > HPNN_UPD_MAX) {
-            for (int l = 0; l < L; l++)
-                if (hpnn_sgd_update(W32[l], V32[l], G + goff[l], 1, 0, Wb[l], Wt[l], Np[l], Kp[l], lr, alpha, scale,
-                                    mom ? 1 : 0, s))
-                    return FALSE;
-            return TRUE;
-        }
-        for (int l = 0; l < L; l++)
-            u[l] = {W32[l], V32[l], G + goff[l], 0, Wb[l], Wt[l], (l == 0 && fused_x) ? W0f : nullptr, 1, Np[l],
-                    Kp[l]};
-        return hpnn_sgd_update_multi(u, L, lr, alpha, scale, mom ? 1 : 0, s) == 0;
+    BOOL step(const XSet &xs, long row, const float *T, int ldt, int n_valid, float lr, float alpha, bool) {
+        const int r = p.step(at(xs, row), nullptr, T, ldt, n_valid, lr, alpha, s);
+        if (r) NN_ERROR(stderr, "batched step failed: %d\n", r);
+        return r == 0 && hpnn_debug_check("batched training step") == 0;
+    }
+
+    /* data parallel: gradients into the flat FP32 buffer (the all-reduce payload) */
+    BOOL alloc_flat(float *external = nullptr) {
+        if (external) p.gflat = external; /* loopback: replicas' buffers in one allocation */
+        gflat = p.gflat;
+        return TRUE;
+    }
+    size_t flat_count() const { return p.goff[L]; }
+    template <class Ready>
+    BOOL grads(const XSet &xs, long row, const float *T, int ldt, int n_valid, Ready &&ready) {
+        const int r = p.grads(at(xs, row), nullptr, T, ldt, n_valid, hpnn::ReadyFn(ready), s);
+        if (r) NN_ERROR(stderr, "batched gradients failed: %d\n", r);
+        return r == 0;
+    }
+    BOOL grads(const XSet &xs, long row, const float *T, int ldt, int n_valid) {
+        return grads(xs, row, T, ldt, n_valid, [](int, int) { return true; });
+    }
+    std::vector<std::pair<int, int>> buckets() const { return p.buckets(); }
+    BOOL update_flat(const float *G, float lr, float alpha, float scale, bool) {
+        return p.update_flat(G, lr, alpha, scale, s) == 0;
     }
 
     /* FP32 master weights (and BPM momentum, into k->dw) -> host FP64 */
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
-        if (V32[0]) ann_momentum_init(k);
+        if (p.V32[0]) ann_momentum_init(k);
         for (int l = 0; l < L; l++) {
             layer_ann *ly = layer_of(k, l);
-            std::vector<float> tmp((size_t)Np[l] * Kp[l]);
-            HIPCHK(hipMemcpy(tmp.data(), W32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
-            for (int n = 0; n < N[l]; n++)
-                for (int m = 0; m < M[l]; m++) ly->weights[(size_t)n * M[l] + m] = tmp[(size_t)n * Kp[l] + m];
-            if (!V32[l]) continue;
-            HIPCHK(hipMemcpy(tmp.data(), V32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
-            for (int n = 0; n < N[l]; n++)
-                for (int m = 0; m < M[l]; m++) k->dw[l][(size_t)n * M[l] + m] = tmp[(size_t)n * Kp[l] + m];
+            const int M = (int)ly->n_inputs, N = (int)ly->n_neurons, Kp = p.Kp[l];
+            std::vector<float> tmp((size_t)p.Np[l] * Kp);
+            HIPCHK(hipMemcpy(tmp.data(), p.W32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N; n++)
+                for (int m = 0; m < M; m++) ly->weights[(size_t)n * M + m] = tmp[(size_t)n * Kp + m];
+            if (!p.V32[l]) continue;
+            HIPCHK(hipMemcpy(tmp.data(), p.V32[l], tmp.size() * 4, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N; n++)
+                for (int m = 0; m < M; m++) k->dw[l][(size_t)n * M + m] = tmp[(size_t)n * Kp + m];
         }
         return TRUE;
     }
@@ -931,11 +765,13 @@ struct Batched {
     BOOL upload_momentum(const kernel_ann *k) {
         if (!k->dw) return TRUE;
         for (int l = 0; l < L; l++) {
-            if (!V32[l]) continue;
-            std::vector<float> tmp((size_t)Np[l] * Kp[l], 0.f);
-            for (int n = 0; n < N[l]; n++)
-                for (int m = 0; m < M[l]; m++) tmp[(size_t)n * Kp[l] + m] = (float)k->dw[l][(size_t)n * M[l] + m];
-            HIPCHK(hipMemcpyAsync(V32[l], tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, s));
+            if (!p.V32[l]) continue;
+            const int M = (int)layer_of((kernel_ann *)k, l)->n_inputs, N = (int)layer_of((kernel_ann *)k, l)->n_neurons;
+            const int Kp = p.Kp[l];
+            std::vector<float> tmp((size_t)p.Np[l] * Kp, 0.f);
+            for (int n = 0; n < N; n++)
+                for (int m = 0; m < M; m++) tmp[(size_t)n * Kp + m] = (float)k->dw[l][(size_t)n * M + m];
+            HIPCHK(hipMemcpyAsync(p.V32[l], tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
         }
         return TRUE;
@@ -966,7 +802,6 @@ struct BatchedFP {
     typedef T target_t;
     typedef T grad_t;
     static constexpr int F64 = sizeof(T) == 8 ? 1 : 0;
-    static constexpr size_t xelem = sizeof(T);
     static constexpr hpnn_comm_dtype comm_dt = sizeof(T) == 8 ? HPNN_DT_F64 : HPNN_DT_F32;
     static const char *name() { return sizeof(T) == 8 ? "f64" : "f32"; }
     static constexpr size_t ACC_BYTES = Batched::ACC_BYTES;
@@ -980,15 +815,16 @@ struct BatchedFP {
     size_t goff[17] = {0};
     hipStream_t s = nullptr;
 
-    static BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t st) {
-        std::vector<T> h((size_t)rows_p * cols_p, (T)0);
-        for (int r = 0; r < rows; r++)
-            for (int c = 0; c < cols; c++) h[(size_t)r * cols_p + c] = (T)src[(size_t)r * cols + c];
-        HIPCHK(hpnn_dev_malloc(dst, h.size() * sizeof(T)));
-        HIPCHK(hipMemcpyAsync(*dst, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
-        HIPCHK(hipStreamSynchronize(st));
+    BOOL upload_x(const DOUBLE *src, int rows, int cols, int rows_p, XSet *xs) {
+        std::vector<T> h((size_t)rows_p * cols, (T)0);
+        for (size_t i = 0; i < (size_t)rows * cols; i++) h[i] = (T)src[i];
+        HIPCHK(hpnn_dev_malloc(&xs->x, h.size() * sizeof(T)));
+        HIPCHK(hipMemcpyAsync(xs->x, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        xs->row_bytes = (size_t)cols * sizeof(T);
         return TRUE;
     }
+    static const void *at(const XSet &xs, long row) { return (const char *)xs.x + row * xs.row_bytes; }
     static int reduce_sum(grad_t *buf, int G, size_t count, hipStream_t st) {
         return hpnn_reduce_fp(F64, buf, buf, G, (long)count, (long)count, st);
     }
@@ -1033,7 +869,7 @@ struct BatchedFP {
         return hpnn_gemm_fp_splits(B, sp < 1 ? 1 : sp);
     }
 
-    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st) {
+    BOOL init(kernel_ann *k, int B, nn_type t, bool momentum, hipStream_t st, bool = true, int = -1) {
         s = st;
         L = (int)k->n_hiddens + 1;
         Bp = B;
@@ -1101,8 +937,8 @@ struct BatchedFP {
         return TRUE;
     }
 
-    BOOL step(const void *X, const T *Tt, int ldt, int n_valid, double lr, double alpha, bool mom) {
-        if (!backprop(X, Tt, ldt, n_valid)) return FALSE;
+    BOOL step(const XSet &xs, long row, const T *Tt, int ldt, int n_valid, double lr, double alpha, bool mom) {
+        if (!backprop(at(xs, row), Tt, ldt, n_valid)) return FALSE;
         const double scale = 1.0 / (double)n_valid;
         for (int l = 0; l < L; l++)
             if (hpnn_update_fp(F64, W[l], V[l], slab[l], S[l], (long)N[l] * M[l], (long)N[l] * M[l], lr, alpha, scale,
@@ -1126,7 +962,8 @@ struct BatchedFP {
     size_t flat_count() const { return goff[L]; }
 
     template <class Ready>
-    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid, Ready &&ready) {
+    BOOL grads(const XSet &xs, long row, const T *Tt, int ldt, int n_valid, Ready &&ready) {
+        const void *X = at(xs, row);
         if (!forward(X, Bp)) return FALSE;
         if (hpnn_output_fp(F64, Z, N[L - 1], Tt, ldt, D[L - 1], N[L - 1], nullptr, 0, nullptr, acc,
                            (unsigned int *)(acc + 1), Bp, n_valid, n_out, type, s))
@@ -1144,8 +981,8 @@ struct BatchedFP {
         }
         return TRUE;
     }
-    BOOL grads(const void *X, const T *Tt, int ldt, int n_valid) {
-        return grads(X, Tt, ldt, n_valid, [](int, int) { return true; });
+    BOOL grads(const XSet &xs, long row, const T *Tt, int ldt, int n_valid) {
+        return grads(xs, row, Tt, ldt, n_valid, [](int, int) { return true; });
     }
     std::vector<std::pair<int, int>> buckets() const {
         std::vector<std::pair<int, int>> v;
@@ -1251,6 +1088,37 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
 
 namespace {
 
+/* HIP graph of one epoch's steps (HPNN_GRAPH=0: eager launches): the epoch's minibatches
+ * are the same every epoch (the sample order is drawn once, libhpnn.c:1218-1229), so one
+ * capture is replayed per epoch and the host launches nothing per step.  Returns FALSE when
+ * the launches cannot be captured (the caller then runs them eagerly: nothing of a failed
+ * capture was executed). */
+template <class Launch>
+bool capture_epoch(hipStream_t s, Launch &&launch, hipGraphExec_t *exec) {
+    *exec = nullptr;
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) return false;
+    const bool ok = launch();
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    if (!ok || e != hipSuccess || !g) {
+        if (g) hipGraphDestroy(g);
+        hipGetLastError();
+        return false;
+    }
+    const bool inst = hipGraphInstantiate(exec, g, nullptr, nullptr, 0) == hipSuccess;
+    hipGraphDestroy(g);
+    if (!inst) {
+        *exec = nullptr;
+        hipGetLastError();
+    }
+    return inst;
+}
+
+bool graphs_enabled() {
+    const char *e = getenv("HPNN_GRAPH");
+    return !(e && e[0] == '0') && !hpnn_debug_enabled();
+}
+
 template <class Net>
 BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpnn_batched_opts *o,
                   hpnn_batched_stats *st) {
@@ -1262,55 +1130,80 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
     const int B = (int)(o->batch ? o->batch : 256);
     const bool mom = o->train == NN_TRAIN_BPM;
     Net net;
-    if (!net.init(k, B, o->type, mom, s)) return FALSE;
+    if (!net.init(k, B, o->type, mom, s, B % 32 == 0)) return FALSE;
     NN_OUT(stdout, "batched GPU training: %s, %d samples per step\n", Net::name(), B);
     if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = (n_batches - 1) * B + net.Bp; /* last batch reads Bp rows */
-    void *Xd = nullptr;
+    XSet xs;
     TT *Td = nullptr;
-    if (!Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
+    if (!net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &xs)) return FALSE;
     {
         std::vector<TT> tf((size_t)rows_p * k->n_outputs, (TT)0);
         for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (TT)T[i];
         HIPCHK(hpnn_dev_malloc(&Td, tf.size() * sizeof(TT)));
         HIPCHK(hipMemcpy(Td, tf.data(), tf.size() * sizeof(TT), hipMemcpyHostToDevice));
     }
+    auto epoch = [&]() -> bool {
+        for (int b = 0; b < n_batches; b++) {
+            const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
+            if (!net.step(xs, (long)b * B, Td + (size_t)b * B * k->n_outputs, (int)k->n_outputs, nv, o->lr, o->alpha,
+                          mom))
+                return false;
+        }
+        return true;
+    };
+    /* ne epochs back to back, each from zeroed statistics (so the last one's remain) */
+    auto epochs = [&](int ne) -> bool {
+        for (int i = 0; i < ne; i++)
+            if (hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess || !epoch()) return false;
+        return true;
+    };
+    /* one graph replays epg epochs (about 32 steps: the host launches once per replay); with
+     * per-epoch metrics every epoch is its own replay followed by a statistics read */
+    const bool metrics = hpnn_metrics_active() != 0;
+    const int E = (int)o->epochs;
+    const int epg = metrics ? 1 : std::max(1, std::min(E, 32 / std::max(1, n_batches)));
+    std::map<int, hipGraphExec_t> graphs;
+    if (graphs_enabled() && n_batches <= 4096)
+        for (int ne : {epg, E % epg}) {
+            if (ne <= 0 || graphs.count(ne)) continue;
+            hipGraphExec_t x = nullptr;
+            if (!capture_epoch(s, [&]() { return epochs(ne); }, &x))
+                NN_DBG(stdout, "batched GPU training: epochs not capturable, eager launches\n");
+            graphs[ne] = x;
+        }
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
-    for (UINT e = 0; e < o->epochs; e++) {
-        HIPCHK(hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s));
-        for (int b = 0; b < n_batches; b++) {
-            const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-            const char *xb = (const char *)Xd + (size_t)b * B * net.Kp[0] * Net::xelem;
-            const TT *tb = Td + (size_t)b * B * k->n_outputs;
-            if (!net.step(xb, tb, (int)k->n_outputs, nv, o->lr, o->alpha, mom)) {
-                hpnn_dev_free(Xd);
-                hpnn_dev_free(Td);
-                return FALSE;
-            }
-        }
-        if (!net.read_stats(&ep_loss, &ep_hits)) return FALSE;
-        if (hpnn_metrics_active())
-            hpnn_metrics_epoch("gpu", o->epoch0 + e + 1, ep_loss / (double)n, ep_hits, n,
+    BOOL ok = TRUE;
+    for (int e = 0; e < E && ok;) {
+        const int ne = std::min(epg, E - e);
+        auto g = graphs.find(ne);
+        ok = (g != graphs.end() && g->second) ? hipGraphLaunch(g->second, s) == hipSuccess : epochs(ne);
+        e += ne;
+        if (ok && (metrics || e == E)) ok = net.read_stats(&ep_loss, &ep_hits);
+        if (ok && metrics)
+            hpnn_metrics_epoch("gpu", o->epoch0 + e, ep_loss / (double)n, ep_hits, n,
                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
-                               (UINT64)n * (e + 1));
+                               (UINT64)n * e);
     }
     auto t1 = std::chrono::steady_clock::now();
-    net.download(k);
-    if (st) {
+    for (auto &g : graphs)
+        if (g.second) hipGraphExecDestroy(g.second);
+    if (ok) ok = net.download(k);
+    if (ok && st) {
         st->seconds = std::chrono::duration<double>(t1 - t0).count();
         st->samples = (UINT64)n * o->epochs;
         st->epoch_loss = ep_loss / (double)n;
         st->correct = ep_hits;
         st->last_loss = st->epoch_loss;
     }
-    hpnn_dev_free(Xd);
+    xs.release();
     hpnn_dev_free(Td);
     /* device FP64 copy of the online engine (if any) is now stale */
     if (k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
-    return TRUE;
+    return ok;
 }
 
 }  // namespace
@@ -1333,7 +1226,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     std::vector<hipStream_t> str(G);
     std::vector<std::unique_ptr<Net>> nets(G);
     GT *lb_flat = nullptr; /* loopback: [G][count] in one allocation */
-    std::vector<void *> Xd(G, nullptr);
+    std::vector<XSet> Xd(G);
     std::vector<TT *> Td(G, nullptr);
     std::vector<hpnn_comm *> comms(G, nullptr);
     BOOL ok = TRUE;
@@ -1342,7 +1235,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         for (int g = 0; g < G; g++) {
             hipSetDevice(dev[g]);
             if (!loopback || g == 0) {
-                hpnn_dev_free(Xd[g]);
+                Xd[g].release();
                 hpnn_dev_free(Td[g]);
             }
             nets[g].reset();
@@ -1361,7 +1254,8 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     for (int g = 0; g < G && ok; g++) {
         if (hipSetDevice(dev[g]) != hipSuccess) return FALSE;
         nets[g].reset(new Net());
-        ok = nets[g]->init(k, Bg, o->type, mom, str[g]);
+        /* fragment-major inputs need every shard to start at a multiple of 32 rows */
+        ok = nets[g]->init(k, Bg, o->type, mom, str[g], B % 32 == 0 && Bg % 32 == 0);
         if (ok && mom && o->resume) ok = nets[g]->upload_momentum(k);
         if (!ok) break;
         if (loopback) {
@@ -1384,7 +1278,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         }
         if (!ok) break;
         if (!loopback || g == 0) {
-            ok = Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, nets[g]->Kp[0], &Xd[g], str[g]);
+            ok = nets[g]->upload_x(X, (int)n, (int)k->n_inputs, rows_p, &Xd[g]);
             if (ok) {
                 std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
                 for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];
@@ -1423,9 +1317,8 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                     int nv = end - start;
                     nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
                     total += nv;
-                    const char *xb = (const char *)Xd[g] + (size_t)start * nets[g]->Kp[0] * Net::xelem;
                     const TT *tb = Td[g] + (size_t)start * n_out;
-                    ok = nets[g]->grads(xb, tb, n_out, nv);
+                    ok = nets[g]->grads(Xd[g], start, tb, n_out, nv);
                 }
                 if (!ok) break;
                 /* virtual replicas share one stream: sum the G buffers into replica 0's */
@@ -1453,7 +1346,6 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                         int nv = end - start;
                         nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
                         const int total = end - b * B;
-                        const char *xb = (const char *)Xd[g] + (size_t)start * net.Kp[0] * Net::xelem;
                         const TT *tb = Td[g] + (size_t)start * n_out;
                         const std::vector<std::pair<int, int>> seq = net.buckets();
                         size_t issued = 0;
@@ -1465,7 +1357,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                         };
                         /* after a local failure every remaining bucket is still all-reduced (same
                          * sizes, same order on every replica), so no peer is left waiting */
-                        int okb = tok[g] && net.grads(xb, tb, n_out, nv, ready) ? 1 : 0;
+                        int okb = tok[g] && net.grads(Xd[g], start, tb, n_out, nv, ready) ? 1 : 0;
                         for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
                         okb = (hpnn_comm_join(comms[g], str[g]) == 0) && okb;
                         const double scale = 1.0 / (double)(total > 0 ? total : 1);
@@ -1540,7 +1432,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const bool mom = o->train == NN_TRAIN_BPM;
     const int n_out = (int)k->n_outputs;
     Net net;
-    if (!net.init(k, Bg, o->type, mom, s) || !net.alloc_flat()) return FALSE;
+    if (!net.init(k, Bg, o->type, mom, s, B % 32 == 0 && Bg % 32 == 0) || !net.alloc_flat()) return FALSE;
     if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const size_t count = net.flat_count();
     /* gradient exchange: one-shot xGMI all-reduce when every rank is on this node and the
@@ -1585,9 +1477,9 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
            use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Net::name(), Bg);
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = n_batches * B + Bg + 128;
-    void *Xd = nullptr;
+    XSet Xd;
     TT *Td = nullptr;
-    BOOL ok = Net::upload_x(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s);
+    BOOL ok = net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &Xd);
     if (ok) {
         std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
         for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];
@@ -1604,11 +1496,10 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             const int start = b * B + R * Bg;
             int nv = end - start;
             nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
-            const char *xb = (const char *)Xd + (size_t)start * net.Kp[0] * Net::xelem;
             const TT *tb = Td + (size_t)start * n_out;
             if (use_xar) {
                 /* small gradients: ONE latency-bound xGMI all-reduce of the whole buffer */
-                ok = net.grads(xb, tb, n_out, nv);
+                ok = net.grads(Xd, start, tb, n_out, nv);
                 if (!ok) break;
                 ok = hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s) == 0;
             } else {
@@ -1621,7 +1512,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                     return hpnn_comm_all_reduce_async(comm, net.gflat + net.goff[lo],
                                                       (long)(net.goff[hi + 1] - net.goff[lo]), Net::comm_dt, s) == 0;
                 };
-                ok = net.grads(xb, tb, n_out, nv, ready);
+                ok = net.grads(Xd, start, tb, n_out, nv, ready);
                 for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
                 ok = (hpnn_comm_join(comm, s) == 0) && ok;
             }
@@ -1663,7 +1554,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     }
     hipStreamSynchronize(s);
     hpnn_boot_finish(); /* every rank is past its last all-reduce before any buffer goes */
-    if (Xd) hpnn_dev_free(Xd);
+    Xd.release();
     if (Td) hpnn_dev_free(Td);
     if (xar) hpnn_xar_destroy(xar);
     if (comm) hpnn_comm_destroy(comm);
@@ -1678,33 +1569,26 @@ namespace {
 BOOL infer_bf16(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, hipStream_t s) {
     const int B = 4096;
     Batched net;
-    if (!net.init(k, B, type, false, s)) return FALSE;
+    if (!net.init(k, B, type, false, s, false, 0)) return FALSE; /* forward only: per-layer plan */
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = (n_batches - 1) * B + net.Bp;
-    void *Xd = nullptr;
-    float *O = nullptr, *Tz = nullptr;
-    if (!upload_bf16(X, (int)n, (int)k->n_inputs, rows_p, net.Kp[0], &Xd, s)) return FALSE;
-    HIPCHK(hpnn_dev_malloc(&O, (size_t)net.Bp * net.Np[net.L - 1] * 4));
-    HIPCHK(hpnn_dev_malloc(&Tz, (size_t)net.Bp * k->n_outputs * 4));
-    HIPCHK(hipMemset(Tz, 0, (size_t)net.Bp * k->n_outputs * 4));
-    std::vector<float> h((size_t)net.Bp * net.Np[net.L - 1]);
+    const int no = net.p.Np[net.L - 1];
+    XSet xs;
+    float *O = nullptr;
+    if (!net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &xs)) return FALSE;
+    HIPCHK(hpnn_dev_malloc(&O, (size_t)net.Bp * no * 4));
+    std::vector<float> h((size_t)net.Bp * no);
     BOOL ok = TRUE;
     for (int b = 0; b < n_batches && ok; b++) {
         const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-        ok = net.forward((const char *)Xd + (size_t)b * B * net.Kp[0] * 2);
-        if (ok)
-            ok = hpnn_output_delta(net.Z, net.Np[net.L - 1], Tz, (int)k->n_outputs, nullptr, 0.f, 0.f,
-                                   net.D[net.L - 1], net.Np[net.L - 1], O, net.Np[net.L - 1], nullptr, nullptr, net.Bp,
-                                   nv, net.n_out, net.type, s) == 0;
+        ok = net.p.predict(net.at(xs, (long)b * B).x, nv, O, no, s) == 0;
         ok = ok && hipMemcpyAsync(h.data(), O, h.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
         for (int r = 0; ok && r < nv; r++)
-            for (UINT c = 0; c < k->n_outputs; c++)
-                Y[((size_t)b * B + r) * k->n_outputs + c] = h[(size_t)r * net.Np[net.L - 1] + c];
+            for (UINT c = 0; c < k->n_outputs; c++) Y[((size_t)b * B + r) * k->n_outputs + c] = h[(size_t)r * no + c];
     }
-    hpnn_dev_free(Xd);
+    xs.release();
     hpnn_dev_free(O);
-    hpnn_dev_free(Tz);
     return ok;
 }
 
@@ -1718,15 +1602,15 @@ BOOL infer_fp(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, h
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = n_batches * B;
     const int no = (int)k->n_outputs;
-    void *Xd = nullptr;
+    XSet xs;
     T *O = nullptr;
-    if (!BatchedFP<T>::upload_x(X, (int)n, (int)k->n_inputs, rows_p, (int)k->n_inputs, &Xd, s)) return FALSE;
+    if (!net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &xs)) return FALSE;
     HIPCHK(hpnn_dev_malloc(&O, (size_t)B * no * sizeof(T)));
     std::vector<T> h((size_t)B * no);
     BOOL ok = TRUE;
     for (int b = 0; b < n_batches && ok; b++) {
         const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-        ok = net.forward((const char *)Xd + (size_t)b * B * k->n_inputs * sizeof(T), B);
+        ok = net.forward(BatchedFP<T>::at(xs, (long)b * B), B);
         if (ok)
             ok = hpnn_output_fp(BatchedFP<T>::F64, net.Z, no, nullptr, 0, nullptr, 0, O, no, nullptr, nullptr, nullptr,
                                 B, 0, no, net.type, s) == 0;
@@ -1734,7 +1618,7 @@ BOOL infer_fp(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, h
              hipStreamSynchronize(s) == hipSuccess;
         for (size_t i = 0; ok && i < (size_t)nv * no; i++) Y[(size_t)b * B * no + i] = (DOUBLE)h[i];
     }
-    hpnn_dev_free(Xd);
+    xs.release();
     hpnn_dev_free(O);
     return ok;
 }

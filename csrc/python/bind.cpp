@@ -17,6 +17,7 @@
 #include <pybind11/stl.h>
 
 #include "../gpu/kernels.h"
+#include "../gpu/bplan.h"
 #include <libhpnn/comm.h>
 #include <libhpnn/xar.h>
 #include <libhpnn/devmem.h>
@@ -30,7 +31,138 @@ static void check(int rc, const char *what) {
     if (rc != 0) throw std::runtime_error(std::string(what) + " failed (rc=" + std::to_string(rc) + ")");
 }
 
+namespace {
+using hpnn::BPlan;
+using hpnn::XIn;
+
+XIn xin(uptr x, uptr xg, int u8, float scale) {
+    XIn v;
+    v.x = P(x);
+    v.xg = P(xg);
+    v.u8 = u8;
+    v.scale = scale;
+    return v;
+}
+
+/* the batched training plan (csrc/gpu/bplan.h): configuration + buffer table on the host,
+ * launches on the given stream; memory is bound from tensors the caller allocated */
+void bind_plan(py::module_ &m) {
+    py::class_<BPlan>(m, "BPlan")
+        .def(py::init([](std::vector<int> sizes, int type, int batch, bool momentum, int fused,
+                         std::vector<int> splits, int mid_grid, bool device) {
+                 auto *p = new BPlan();
+                 std::string err;
+                 if (sizes.size() < 2) throw std::runtime_error("BPlan: at least two layer sizes");
+                 std::vector<int> sp(sizes.size(), 0);
+                 for (size_t i = 0; i < splits.size() && i < sp.size(); i++) sp[i] = splits[i];
+                 const int rc = p->configure(sizes.data(), (int)sizes.size() - 1, type, batch, momentum, fused,
+                                             sp.data(), mid_grid, device, &err);
+                 if (rc) {
+                     delete p;
+                     throw std::invalid_argument("BPlan: " + err + " (rc=" + std::to_string(rc) + ")");
+                 }
+                 return p;
+             }),
+             py::arg("sizes"), py::arg("type"), py::arg("batch"), py::arg("momentum"), py::arg("fused") = -1,
+             py::arg("splits") = std::vector<int>(), py::arg("mid_grid") = 512, py::arg("device") = true)
+        .def("config",
+             [](const BPlan &p) {
+                 py::dict d;
+                 d["L"] = p.L;
+                 d["Bp"] = p.Bp;
+                 d["mode"] = p.mode ? std::string(1, p.mode) : std::string();
+                 d["Kp"] = std::vector<int>(p.Kp, p.Kp + p.L);
+                 d["Np"] = std::vector<int>(p.Np, p.Np + p.L);
+                 d["S"] = std::vector<int>(p.S, p.S + p.L);
+                 d["mid_grid"] = p.mid_grid;
+                 d["mid_groups"] = p.mid_groups;
+                 d["wide_ksplit"] = p.wide_ksplit;
+                 d["slab_floats"] = p.slab_f;
+                 d["input_layout"] = p.input_layout();
+                 d["buckets"] = p.buckets();
+                 return d;
+             })
+        .def("buffers",
+             [](const BPlan &p) {
+                 py::list out;
+                 for (const auto &b : p.specs)
+                     out.append(py::make_tuple(b.name, b.layer, b.dtype,
+                                               std::vector<long>(b.shape, b.shape + b.ndim), b.zero));
+                 return out;
+             })
+        .def("bind",
+             [](BPlan &p, std::vector<uptr> ptrs) {
+                 if (ptrs.size() != p.specs.size()) throw std::runtime_error("BPlan.bind: one pointer per buffer");
+                 std::vector<void *> v;
+                 for (uptr a : ptrs) v.push_back(P(a));
+                 p.bind(v.data());
+             })
+        .def_static("pick_splits", &BPlan::pick_splits)
+        .def("cast_weights", [](BPlan &p, uptr s) { check(p.cast_weights(S(s)), "BPlan.cast_weights"); })
+        .def("zero_stats", [](BPlan &p, uptr s) { check(p.zero_stats(S(s)), "BPlan.zero_stats"); })
+        .def("forward", [](BPlan &p, uptr X, uptr s) { check(p.forward(P(X), S(s)), "BPlan.forward"); })
+        .def("output",
+             [](BPlan &p, uptr labels, uptr T, int ldt, int n_valid, uptr O, int ldo, bool stats, uptr s) {
+                 check(p.output((const int *)P(labels), (const float *)P(T), ldt, n_valid, (float *)P(O), ldo, stats,
+                                S(s)),
+                       "BPlan.output");
+             })
+        .def("backward_layer", [](BPlan &p, int l, uptr s) { check(p.backward_layer(l, S(s)), "BPlan.backward_layer"); })
+        .def("grad_layer",
+             [](BPlan &p, int l, uptr x, uptr xg, int u8, float sc, bool reduce, uptr s) {
+                 check(p.grad_layer(l, xin(x, xg, u8, sc), reduce, S(s)), "BPlan.grad_layer");
+             })
+        .def("update_layer",
+             [](BPlan &p, int l, float lr, float alpha, float scale, bool from_g, uptr s) {
+                 check(p.update_layer(l, lr, alpha, scale, from_g, S(s)), "BPlan.update_layer");
+             })
+        .def("front",
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, uptr s) {
+                 check(p.front(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid, S(s)),
+                       "BPlan.front");
+             })
+        .def("step",
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, float lr,
+                float alpha, uptr s) {
+                 check(p.step(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid, lr, alpha,
+                              S(s)),
+                       "BPlan.step");
+             })
+        .def("grads",
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid,
+                py::object ready, uptr s) {
+                 hpnn::ReadyFn fn = [&](int lo, int hi) {
+                     if (ready.is_none()) return true;
+                     py::object r = ready(lo, hi);
+                     return r.is_none() || r.cast<bool>();
+                 };
+                 check(p.grads(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid, fn,
+                               S(s)),
+                       "BPlan.grads");
+             })
+        .def("grads_slabs",
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, uptr s) {
+                 hpnn::SlabSegs g;
+                 check(p.grads_slabs(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid,
+                                     &g, S(s)),
+                       "BPlan.grads_slabs");
+                 py::list out; /* (address, slab stride, slabs, floats) per segment */
+                 for (int i = 0; i < g.count; i++)
+                     out.append(py::make_tuple((uptr)g.base[i], g.stride[i], g.cnt[i], g.n[i]));
+                 return out;
+             })
+        .def("update_flat",
+             [](BPlan &p, uptr G, float lr, float alpha, float scale, uptr s) {
+                 check(p.update_flat((const float *)P(G), lr, alpha, scale, S(s)), "BPlan.update_flat");
+             })
+        .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {
+            check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
+        });
+}
+}  // namespace
+
 PYBIND11_MODULE(_native, m) {
+    bind_plan(m);
     m.doc() = "libhpnn gfx950 kernels (MFMA GEMMs, fused output/optimizer kernels)";
     m.attr("EPI_NONE") = (int)HPNN_EPI_NONE;
     m.attr("EPI_ACT") = (int)HPNN_EPI_ACT;

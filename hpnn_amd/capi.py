@@ -50,6 +50,7 @@ def lib():
             "nn_return_version": (cp, []), "nn_return_type": (i, [vp]), "nn_return_train": (i, [vp]),
             "nn_dump_state": (i, [vp, cp]), "nn_load_state": (i, [vp, cp]), "nn_return_epochs_done": (u, [vp]),
             "nn_pack_samples": (i, [cp, cp]),
+            "nn_pack_arrays": (i, [cp, vp, vp, u, u, u]),
             "hpnn_trace_enable": (None, [i]), "hpnn_trace_enabled": (i, []), "hpnn_trace_push": (None, [cp]),
             "hpnn_trace_pop": (None, []), "hpnn_trace_add": (None, [cp, d]), "hpnn_trace_reset": (None, []),
             "hpnn_trace_calls": (ctypes.c_uint64, [cp]), "hpnn_trace_seconds": (d, [cp]),
@@ -164,6 +165,19 @@ def pack_samples(sample_dir, out_path):
     """pack a directory of sample files into one binary file (csrc/core/dataset.cpp)"""
     if not lib().nn_pack_samples(sample_dir.encode(), out_path.encode()):
         raise OSError(f"nn_pack_samples({sample_dir}) failed")
+
+
+def pack_arrays(out_path, X, T):
+    """write n records (X [n, n_in], T [n, n_out], anything numpy turns into float64) as a pack
+    file train_nn / run_nn accept in place of a sample directory"""
+    import numpy as np
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    T = np.ascontiguousarray(T, dtype=np.float64)
+    n, n_in = X.shape
+    if T.shape[0] != n:
+        raise ValueError("X and T need the same number of rows")
+    if not lib().nn_pack_arrays(out_path.encode(), X.ctypes.data, T.ctypes.data, n, n_in, T.shape[1]):
+        raise OSError(f"nn_pack_arrays({out_path}) failed")
 
 
 def smoke_online():

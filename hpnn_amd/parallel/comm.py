@@ -158,12 +158,17 @@ class NativeComm:
         if self.h:
             native().comm_join(self.h, _stream())
 
+    @staticmethod
+    def _segs(segs):
+        """segments as (address, slab stride, S, n) -- the form BPlan.grads_slabs returns --
+        or (tensor [S, >= n], S, n)"""
+        return [s if len(s) == 4 else (s[0].data_ptr(), s[0].stride(0), s[1], s[2]) for s in segs]
+
     def all_reduce_slabs(self, out, segs):
-        """out = sum over ranks of [seg_0 | seg_1 | ...] where segment j = (slabs, S, n) is
-        the local sum of the S slabs slabs[s, :n]: split-K reduction and exchange in ONE
-        launch (xGMI all-reduce, include/libhpnn/xar.h), on the current stream"""
-        native().xar_all_reduce_slabs_f32(self.xar, [(t.data_ptr(), t.stride(0), S, n) for t, S, n in segs],
-                                          out.data_ptr(), _stream())
+        """out = sum over ranks of [seg_0 | seg_1 | ...] where segment j is the local sum of
+        its S slabs of n floats: split-K reduction and exchange in ONE launch (xGMI
+        all-reduce, include/libhpnn/xar.h), on the current stream"""
+        native().xar_all_reduce_slabs_f32(self.xar, self._segs(segs), out.data_ptr(), _stream())
         return out
 
     def all_reduce_slabs_update(self, out, segs, layers, lr, alpha, scale, momentum):
@@ -173,7 +178,7 @@ class NativeComm:
         def p(t):
             return 0 if t is None else t.data_ptr()
         native().xar_all_reduce_slabs_update_f32(
-            self.xar, [(t.data_ptr(), t.stride(0), S, n) for t, S, n in segs], out.data_ptr(),
+            self.xar, self._segs(segs), out.data_ptr(),
             [(p(w), p(v), p(wb), p(wt), p(wf), w.shape[0], w.shape[1]) for w, v, wb, wt, wf in layers],
             float(lr), float(alpha), float(scale), int(bool(momentum)), _stream())
         return out

@@ -124,11 +124,7 @@ class DataParallel:
         copy-in phase also sums the local split-K slabs of G0 and the [G1|G2] groups and
         which then applies every layer's update to the reduced gradients"""
         m = self.m
-        m._fused_front(X, labels, T, n_valid)
-        groups = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
-        m._g0_reduce(X, groups)
-        n0 = m.G[0].numel()
-        segs = [(m.slab[0].view(m.S[0], n0), m.S[0], n0), (groups, m.mid_groups, m.grad_flat.numel() - n0)]
+        segs = m.grads_slabs(X, labels, T, n_valid)
         scale = 1.0 / (n_valid * self.world)
         if _XAR_UPD:
             # exchange + every layer's optimizer step in ONE launch (the update kernel and
@@ -138,7 +134,7 @@ class DataParallel:
                                     for l in range(m.L)], lr, alpha, scale, m.momentum)
         else:
             self.native.all_reduce_slabs(m.grad_flat, segs)
-            m.update_all(lr, alpha, scale, m.G)
+            m.update_all(lr, alpha, scale)
 
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         m = self.m
@@ -146,8 +142,7 @@ class DataParallel:
         if not self.active:
             return m.train_step(X, labels=labels, T=T, n_valid=n_valid, lr=lr, alpha=alpha)
         if (self.native is not None and self.native.xar and getattr(m, "fused_mode", None) in ("x", "t")
-                and m.grad_flat.numel() * 4 <= self.native.xar_max
-                and m.grad_flat.numel() - m.G[0].numel() == ops.MLP3_SLAB):
+                and m.grad_flat.numel() * 4 <= self.native.xar_max):
             return self._fused_xgmi_step(X, labels, T, n_valid, lr, alpha)
         works = []
         done = set()
@@ -169,11 +164,7 @@ class DataParallel:
             self.native.join()
         for w in works:
             w.wait()
-        if m.L <= ops.UPD_MAX:
-            m.update_all(lr, alpha, scale, m.G)  # one launch for every layer
-        else:
-            for l in range(m.L):
-                m.update_layer(l, lr, alpha, scale, from_G=True)
+        m.update_all(lr, alpha, scale)  # every layer from the reduced buckets
 
 
     # ------------------------------------------------------------ bf16rs (sharded) step

@@ -268,6 +268,8 @@ UINT _NN(return, epochs_done)(nn_def *conf);
 /* pack a directory of sample files into one binary file; train / run accept a pack
  * file wherever a sample or test directory is expected */
 BOOL _NN(pack, samples)(const CHAR *dir, const CHAR *filename);
+/* the same file from n records in memory (X: n x n_in, T: n x n_out, row-major) */
+BOOL _NN(pack, arrays)(const CHAR *filename, const DOUBLE *X, const DOUBLE *T, UINT n, UINT n_in, UINT n_out);
 
 #ifdef __cplusplus
 }

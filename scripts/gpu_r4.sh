@@ -1,0 +1,33 @@
+#!/bin/bash
+# round-4 GPU call: steps by name, each under its own time limit; a crash / fault / timeout
+# (rc not 0 or 1) ends the call.   usage: scripts/gpu_r4.sh <tag> <step> [<step> ...]
+#   steps: tests | tests:<pytest -k expr> | smoke | bench | rruff | libbench | prof | prof_rruff
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+tag=$1; shift
+O=gpurun_out/$tag; mkdir -p $O
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $O/steps.log
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $O/steps.log
+  tail -n 15 "$O/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+export TMPDIR=/tmp
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    tests:*) step pytest_sel 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${s#tests:}" ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 300 python bench.py --steps 200 --warmup 20 ;;
+    rruff) step bench_rruff 300 python bench.py --model rruff --steps 100 --warmup 10 ;;
+    synth) step bench_synth 300 python bench.py --model synth --steps 20 --warmup 5 ;;
+    libbench) step libbench 900 python scripts/lib_vs_bench.py --out $O/lib_vs_bench.jsonl ;;
+    prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
+    prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo DONE

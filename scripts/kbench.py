@@ -45,15 +45,12 @@ def main():
         lab = torch.randint(0, 10, (m.Bp,), device=dev, dtype=torch.int32)
         bytes_x = X.numel() * 2
         kw = dict(labels=lab, T=None, n_valid=m.Bp)
-        phases = {"fused front (" + mode + ")": lambda: m._fused_front(X, **kw)}
+        phases = {"fused front (" + mode + ")": lambda: m.front(X, **kw)}
         if mode == "mid":
             phases["  fwd_l0 (gemm_nt X.W0^T)"] = lambda: ops.gemm_nt(X, m.Wb[0], ops.EPI_ACT, out=m.H[0])
         phases["grad_l0 (gemm_tn D1^T.X)"] = lambda: ops.gemm_tn(m.D[0], X, splits=m.S[0], out=m.slab[0])
         if mode == "x":
-            gv = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
-            g1, g2 = m._mid_group_views()
-            phases["reduce_groups (mid slabs)"] = lambda: ops.reduce_groups(m.midslab, m.mid_groups, gv)
-            phases["update_all (3 layers)"] = lambda: m.update_all(0.01, 0.2, 1.0 / m.Bp, [m.slab[0], g1, g2])
+            phases["front + G0 (grads_slabs)"] = lambda: m.grads_slabs(X, **kw)
         phases["full train_step"] = lambda: m.train_step(X, labels=lab)
         for f in phases.values():
             f()

@@ -1,0 +1,87 @@
+"""Per-step time of the library's batched engine (train_nn -m batched, the reference's entry
+point: tests/train_nn.c:232 -> nn_train_kernel) against bench.py for the same configs.
+
+Both drive the same plan (csrc/gpu/bplan.h).  train_nn trains `--batches` minibatches per
+epoch for `--epochs` epochs from a generated pack file (8-bit pixel values for the MNIST
+shape, uniform floats for RRUFF) and prints its training wall time; per step = seconds /
+(epochs x batches).  bench.py runs its usual timed loop.  Writes one JSON line per config.
+
+    python scripts/lib_vs_bench.py --out gpurun_out/lib_vs_bench.jsonl
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hpnn_amd import capi  # noqa: E402
+from hpnn_amd.utils import formats  # noqa: E402
+
+CONFIGS = {"mnist": ((784, [128, 64], 10), 65536, True), "rruff": ((4096, [230], 230), 16384, False)}
+
+
+def run_train_nn(name, batches, epochs, work):
+    (n_in, hid, n_out), B, pixels = CONFIGS[name]
+    n = B * batches
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 256, (n, n_in), dtype=np.uint8).astype(np.float64) if pixels else \
+        rng.uniform(0, 1, (n, n_in)).astype(np.float64)
+    T = np.zeros((n, n_out))
+    T[np.arange(n), rng.integers(0, n_out, n)] = 1.0
+    d = os.path.join(work, name)
+    os.makedirs(d, exist_ok=True)
+    capi.pack_arrays(os.path.join(d, "train.hpnb"), X, T)
+    del X, T
+    formats.write_conf(os.path.join(d, "nn.conf"), name=name, type="SNN", seed=10958, inputs=n_in, hiddens=hid,
+                       outputs=n_out, train="BPM", sample_dir="./train.hpnb", test_dir="./train.hpnb",
+                       mode="batched", batch=B, epochs=epochs, dtype="bf16", lr=0.01)
+    env = dict(os.environ)
+    env.pop("HPNN_FORCE_CPU", None)
+    r = subprocess.run([os.path.join(ROOT, "bin", "train_nn"), "-vvv", "nn.conf"], cwd=d, env=env,
+                       capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit(r.stdout[-3000:] + r.stderr[-3000:])
+    m = re.search(r"BATCHED TRAINING: (\d+) samples in ([0-9.]+) s", r.stdout)
+    mode = re.search(r"batched plan: mode (\S)", r.stdout)
+    samples, secs = int(m.group(1)), float(m.group(2))
+    steps = epochs * batches
+    return {"us_per_step": secs / steps * 1e6, "steps": steps, "samples": samples, "seconds": secs,
+            "plan_mode": mode.group(1) if mode else None}
+
+
+def run_bench(name, steps):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", name, "--steps", str(steps),
+                        "--warmup", "10"], capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit(r.stdout[-3000:] + r.stderr[-3000:])
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"us_per_step": j["ms_per_step"] * 1e3, "steps": steps}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="mnist,rruff")
+    ap.add_argument("--batches", type=int, default=4)
+    ap.add_argument("--epochs", type=int, default=50)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    with tempfile.TemporaryDirectory() as work:
+        for name in a.configs.split(","):
+            lib = run_train_nn(name, a.batches, a.epochs, work)
+            b = run_bench(name, 200)
+            rec = {"config": name, "batch": CONFIGS[name][1], "train_nn": lib, "bench": b,
+                   "ratio": round(lib["us_per_step"] / b["us_per_step"], 4)}
+            print(json.dumps(rec), flush=True)
+            if a.out:
+                with open(a.out, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -9,7 +9,6 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from hpnn_amd import ops  # noqa: E402
 from hpnn_amd.models import MLP  # noqa: E402
 from scripts.kbench import timeit  # noqa: E402
 
@@ -28,17 +27,14 @@ def main():
               for _ in range(args.sets)]
         lab = torch.randint(0, 10, (m.Bp,), device=dev, dtype=torch.int32)
         kw = dict(labels=lab, T=None, n_valid=m.Bp)
-        gv = m.midtmp[:m.mid_groups * ops.MLP3_SLAB].view(m.mid_groups, ops.MLP3_SLAB)
-        g1, g2 = m._mid_group_views()
         it = [0]
 
         def nxt():
             it[0] += 1
             return Xs[it[0] % len(Xs)]
         phases = {
-            f"front ({mode})": lambda: m._fused_front(nxt(), **kw),
-            "front+G0 (same batch)": lambda: (lambda X: (m._fused_front(X, **kw), m._g0_reduce(X, gv)))(nxt()),
-            "update_all": lambda: m.update_all(0.01, 0.2, 1.0 / m.Bp, [m.slab[0], g1, g2]),
+            f"front ({mode})": lambda: m.front(nxt(), **kw),
+            "front + G0 (grads_slabs)": lambda: m.grads_slabs(nxt(), **kw),
             "full train_step": lambda: m.train_step(nxt(), labels=lab),
         }
         for f in phases.values():

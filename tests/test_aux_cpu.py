@@ -170,3 +170,20 @@ def test_python_state_pack_trace(tmp_path, monkeypatch):
     trace.enable(False)
     net.close()
     net2.close()
+
+
+def test_pack_arrays_matches_directory(tmp_path):
+    """nn_pack_arrays (records from memory, e.g. a generated benchmark set) writes the same
+    pack as the directory path: training from it gives the same kernel"""
+    from hpnn_amd import capi
+    a, b = tmp_path / "a", tmp_path / "b"
+    _dataset(str(a / "samples"))
+    files = sorted(os.listdir(a / "samples"))
+    recs = [formats.read_sample(str(a / "samples" / f)) for f in files]
+    os.makedirs(b, exist_ok=True)
+    capi.pack_arrays(str(b / "gen.hpnb"), np.array([x for x, _ in recs]), np.array([t for _, t in recs]))
+    _conf(str(a))
+    _conf(str(b), samples="./gen.hpnb")
+    for d in (a, b):
+        _run([os.path.join(BIN, "train_nn"), "-vv", "-b", "4", "-e", "2", "nn.conf"], str(d))
+    assert _read(a / "kernel.opt") == _read(b / "kernel.opt")

@@ -79,15 +79,15 @@ def test_bucket_plan():
 def test_split_counts_for_8phase_tn():
     """weight gradients with 256x256 tiles get a split count the 8-phase TN kernel accepts
     (>= 256 workgroups, an even number of 64-row units per split); others keep the
-    one-workgroup-per-CU rule (MNIST's G0: 48)"""
+    one-workgroup-per-CU rule (MNIST's G0: 48).  One rule, in the library (bplan.cpp)."""
     from hpnn_amd.models.mlp import MLP
     assert MLP._pick_splits(256, 4096, 16384) == 16       # RRUFF-shaped first layer
     assert MLP._pick_splits(4096, 4096, 8192) == 1        # synthetic 8x4096 ANN
     assert MLP._pick_splits(128, 800, 65536) == 48        # MNIST G0 (not 256-divisible)
     for N, K, B in [(256, 4096, 16384), (512, 2048, 8192), (4096, 4096, 1024)]:
-        s = MLP._splits_8ph(N, K, B)
-        assert s and (N // 256) * (K // 256) * s >= 256 and (B // 64) % s == 0 and (B // 64 // s) % 2 == 0
-    assert MLP._splits_8ph(256, 256, 16384) == 0          # 256 splits would leave 1 unit each
+        s = MLP._pick_splits(N, K, B)
+        assert (N // 256) * (K // 256) * s >= 256 and (B // 64) % s == 0 and (B // 64 // s) % 2 == 0
+    assert MLP._pick_splits(256, 256, 16384) == 32        # no 8-phase split: 32 splits of 512 rows
 
 
 def _worker_rs(rank, world, port, sizes, B, steps, mode, q):
