@@ -147,6 +147,159 @@ __global__ __launch_bounds__(256) void gemm_fp_kernel(const T *__restrict__ A, i
             }
 }
 
+/* ---- 128 x 128 tiles: the large-GEMM path -------------------------------------------
+ * 256 threads = 4 waves in 2 x 2, wave tile 64 x 64 = 4 x 4 MFMA tiles (16 accumulators);
+ * K in stages of 16 (4 MFMA k-steps), two LDS stages: the next stage's operands are loaded
+ * with 16-byte global loads into registers while the current stage is multiplied, then
+ * written to the other LDS buffer; one barrier per stage.  Both operands are staged k-major
+ * ([16][BM + 16]): an MFMA fragment (16 consecutive rows x 4 k) is one ds_read_b64 / b32 per
+ * lane, and the 16-element padding puts the two k-rows a half-wave reads into disjoint banks.
+ * Column c of k-row k holds row c ^ swz(k) (swz permutes within 16-row groups, so fragment
+ * reads stay conflict-free): with it the stores of row-major ([row][k]) operands, where the
+ * lanes of a group write 8 (f64) / 4 (f32) different k-rows, hit distinct banks too.
+ * Per stage and CU: f64 64 MFMAs x 64 cycles per SIMD against 32 KiB staged -- the
+ * matrix-core rate of FP64 needs ~8 B/clock/CU from the L2. */
+constexpr int BB = 128, LDB = BB + 16;
+
+template <typename T>
+struct FpBig {
+    static constexpr int VW = 16 / sizeof(T); /* elements per 16-byte load */
+    /* column swizzle of k-row k (see above) */
+    __device__ static int swz(int k) { return sizeof(T) == 8 ? ((k >> 1) & 7) * 2 : ((k >> 2) & 3) * 8; }
+};
+
+/* one operand stage: rows [r0, r0 + 128) x k [k0, k0 + 16) of P (row-major [row][k] when
+ * !TRANS, [k][row] when TRANS) into registers: NL chunks of VW elements per thread */
+template <typename T, bool TRANS>
+struct StageLoad {
+    static constexpr int VW = FpBig<T>::VW;
+    static constexpr int NL = BB * BK / VW / 256;
+    T v[NL][VW];
+    __device__ void load(const T *__restrict__ P, int ld, int r0, int k0, int R, int K, bool vec) {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            int r, k;
+            if (!TRANS) { /* lanes along k first: BK / VW lanes cover a row's 16 k */
+                constexpr int LPR = BK / VW;
+                r = r0 + (t + 256 * i) / LPR;
+                k = k0 + ((t + 256 * i) % LPR) * VW;
+            } else { /* lanes along the rows: BB / VW lanes cover one k-row */
+                constexpr int LPK = BB / VW;
+                k = k0 + (t + 256 * i) / LPK;
+                r = r0 + ((t + 256 * i) % LPK) * VW;
+            }
+            const T *src = !TRANS ? P + (size_t)r * ld + k : P + (size_t)k * ld + r;
+            const bool whole = !TRANS ? (r < R && k + VW <= K) : (k < K && r + VW <= R);
+            if (vec && whole) {
+                typedef __attribute__((ext_vector_type(VW))) T vT;
+                const vT x = *(const vT *)src;
+#pragma unroll
+                for (int e = 0; e < VW; e++) v[i][e] = x[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < VW; e++) {
+                    const bool in = !TRANS ? (r < R && k + e < K) : (k < K && r + e < R);
+                    v[i][e] = in ? src[e] : (T)0;
+                }
+            }
+        }
+    }
+    __device__ void store(T *s) const {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            if (!TRANS) {
+                constexpr int LPR = BK / VW;
+                const int r = (t + 256 * i) / LPR, k = ((t + 256 * i) % LPR) * VW;
+#pragma unroll
+                for (int e = 0; e < VW; e++) s[(k + e) * LDB + (r ^ FpBig<T>::swz(k + e))] = v[i][e];
+            } else {
+                constexpr int LPK = BB / VW;
+                const int k = (t + 256 * i) / LPK, r = ((t + 256 * i) % LPK) * VW;
+                typedef __attribute__((ext_vector_type(VW))) T vT;
+                vT x;
+#pragma unroll
+                for (int e = 0; e < VW; e++) x[e] = v[i][e];
+                *(vT *)(s + k * LDB + (r ^ FpBig<T>::swz(k))) = x; /* swz keeps VW-aligned runs contiguous */
+            }
+        }
+    }
+};
+
+template <typename T, int EPI, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_fp_big_kernel(const T *__restrict__ A, int lda, const T *__restrict__ B,
+                                                          int ldb, T *__restrict__ C, int ldc, const T *__restrict__ aux,
+                                                          int ldaux, int M, int N, int K, int kchunk, long slab_stride,
+                                                          int vec, int tiles_n) {
+    typedef typename Acc<T>::type accT;
+    __shared__ T As[2][BK * LDB], Bs[2][BK * LDB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    /* XCD-aware order: consecutive tiles of a row of C (sharing the A rows) on one XCD */
+    const int nt = gridDim.x, b = blockIdx.x;
+    const int per = nt / 8, rem = nt % 8, x = b & 7, j = b >> 3;
+    const int tile = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + j;
+    const int m0 = (tile / tiles_n) * BB, n0 = (tile % tiles_n) * BB;
+    const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+    C += (size_t)blockIdx.z * slab_stride;
+    const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+    accT acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) acc[i][jj] = accT{0, 0, 0, 0};
+    StageLoad<T, TA> la;
+    StageLoad<T, TB> lb;
+    const int nst = (ke - kb + BK - 1) / BK;
+    if (nst > 0) {
+        la.load(A, lda, m0, kb, M, ke, vec);
+        lb.load(B, ldb, n0, kb, N, ke, vec);
+        la.store(As[0]);
+        lb.store(Bs[0]);
+    }
+    __syncthreads();
+    const int fr = lane & 15, fk = lane >> 4;
+    for (int st = 0; st < nst; st++) {
+        const int cur = st & 1;
+        if (st + 1 < nst) {
+            la.load(A, lda, m0, kb + (st + 1) * BK, M, ke, vec);
+            lb.load(B, ldb, n0, kb + (st + 1) * BK, N, ke, vec);
+        }
+        const T *as = As[cur], *bs = Bs[cur];
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 4) {
+            const int k = kk + fk, sw = FpBig<T>::swz(k);
+            T a[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) a[i] = as[k * LDB + ((wm + 16 * i + fr) ^ sw)];
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) bv[jj] = bs[k * LDB + ((wn + 16 * jj + fr) ^ sw)];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) acc[i][jj] = Acc<T>::mma(a[i], bv[jj], acc[i][jj]);
+        }
+        if (st + 1 < nst) {
+            la.store(As[cur ^ 1]);
+            lb.store(Bs[cur ^ 1]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = m0 + wm + 16 * i + Acc<T>::row(lane, r), n = n0 + wn + 16 * jj + fr;
+                if (m >= M || n >= N) continue;
+                T v = acc[i][jj][r];
+                if constexpr (EPI == HPNN_EPI_ACT) v = act_fp<T>(v);
+                if constexpr (EPI == HPNN_EPI_DACT) v *= dact_fp<T>(aux[(size_t)m * ldaux + n]);
+                C[(size_t)m * ldc + n] = v;
+            }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max_fp(T v) {
 #pragma unroll
@@ -266,6 +419,30 @@ int gemm_fp(const void *A, int lda, int ta, const void *B, int ldb, int tb, void
     if (epi == HPNN_EPI_DACT && !aux) return -2;
     const int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
     const int sp = (K + kchunk - 1) / kchunk;
+    /* 128 x 128 tiles once they fill the chip (>= 256 workgroups with the splits); the
+     * 64 x 64 kernel below for the small products of narrow layers (HPNN_FP_BIG=0: always) */
+    static const bool big_on = [] { const char *e = getenv("HPNN_FP_BIG"); return !(e && e[0] == '0'); }();
+    const long tiles_big = (long)((M + BB - 1) / BB) * ((N + BB - 1) / BB);
+    if (big_on && tiles_big * sp >= 256) {
+        const uintptr_t al = (uintptr_t)A | (uintptr_t)B;
+        const int vec = (al % 16 == 0 && lda % FpBig<T>::VW == 0 && ldb % FpBig<T>::VW == 0) ? 1 : 0;
+        const int tn = (N + BB - 1) / BB;
+        dim3 g2((unsigned)tiles_big, 1, sp);
+#define HPNN_GB(E, A_, B_)                                                                                          \
+    hipLaunchKernelGGL((gemm_fp_big_kernel<T, E, A_, B_>), g2, dim3(256), 0, s, (const T *)A, lda, (const T *)B, ldb, \
+                       (T *)C, ldc, (const T *)aux, ldaux, M, N, K, kchunk, slab_stride, vec, tn)
+#define HPNN_GBT(E)                                   \
+    if (ta && tb) HPNN_GB(E, true, true);             \
+    else if (ta) HPNN_GB(E, true, false);             \
+    else if (tb) HPNN_GB(E, false, true);             \
+    else HPNN_GB(E, false, false)
+        if (epi == HPNN_EPI_ACT) { HPNN_GBT(HPNN_EPI_ACT); }
+        else if (epi == HPNN_EPI_DACT) { HPNN_GBT(HPNN_EPI_DACT); }
+        else { HPNN_GBT(HPNN_EPI_NONE); }
+#undef HPNN_GBT
+#undef HPNN_GB
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, sp);
 #define HPNN_GF(E, A_, B_)                                                                                        \
     hipLaunchKernelGGL((gemm_fp_kernel<T, E, A_, B_>), grid, dim3(256), 0, s, (const T *)A, lda, (const T *)B, ldb, \

@@ -25,6 +25,7 @@ for s in "$@"; do
     rruff) step bench_rruff 300 python bench.py --model rruff --steps 100 --warmup 10 ;;
     synth) step bench_synth 300 python bench.py --model synth --steps 20 --warmup 5 ;;
     libbench) step libbench 900 python scripts/lib_vs_bench.py --out $O/lib_vs_bench.jsonl ;;
+    fpbench) step fpbench 300 python scripts/gemm_fp_bench.py --out $O/gemm_fp.jsonl ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -30,7 +30,11 @@ def _bip(x):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float64, torch.float32])
 @pytest.mark.parametrize("M,N,K,ta,tb,epi", [(300, 70, 130, 0, 0, 1), (257, 33, 65, 0, 1, 2), (40, 90, 1000, 1, 1, 0),
-                                             (128, 64, 64, 0, 0, 0)])
+                                             (128, 64, 64, 0, 0, 0),
+                                             # >= 256 tiles of 128 x 128: the large-GEMM kernel; odd
+                                             # strides (scalar loads) and edges, every operand layout
+                                             (2085, 2053, 303, 0, 0, 1), (2048, 2048, 512, 1, 1, 0),
+                                             (2200, 2100, 334, 1, 0, 2), (2304, 2176, 100, 0, 1, 1)])
 def test_gemm_fp_matches_torch(gpu, dt, M, N, K, ta, tb, epi):
     torch.manual_seed(M + N + K)
     A = torch.randn(K, M, dtype=dt, device="cuda") if ta else torch.randn(M, K, dtype=dt, device="cuda")
