@@ -163,7 +163,10 @@ int BPlan::configure(const int *sizes, int n_layers, int net_type, int batch_siz
         add("midslab", -1, BD_F32, {mid_grid, slab_f}, false);
         add("midtmp", -1, BD_F32, {16, slab_f}, false);
     }
-    if (mode == 't' || mode == 'x') add("W0f", -1, BD_BF16, {(long)Np[0] * Kp[0]}, true);
+    if (mode == 't' || mode == 'x') {
+        add("W0f", -1, BD_BF16, {(long)Np[0] * Kp[0]}, true);
+        add("g0cnt", -1, BD_I32, {256}, true); /* fused G0 step: tile counters + error word */
+    }
     if (mode == 'w') {
         const long pb = wide_ksplit == 2 ? hpnn_wide2_pbuf_bytes(Bp) : 16;
         add("wpbuf", -1, BD_F32, {pb / 4}, false);
@@ -195,6 +198,7 @@ void BPlan::name_pointers() {
     midslab = (float *)buf("midslab");
     midtmp = (float *)buf("midtmp");
     W0f = buf("W0f");
+    g0cnt = (unsigned int *)buf("g0cnt");
     wpbuf = (float *)buf("wpbuf");
     wwords = (unsigned int *)buf("wwords");
 }
@@ -348,6 +352,25 @@ int BPlan::g0_reduce(const XIn &x, hipStream_t s) {
                                     slab_f, slab_f, mid_groups, midtmp, s);
 }
 
+/* G0 + its split-K reduction + every layer's step in ONE launch (kernels_g0.hip); -1 when
+ * the shape or the input is not covered (the caller then runs G0 + the update launch) */
+int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s) {
+    const void *fm = fm_input(x);
+    if (!fm || !g0cnt || !g0_fused) return -1;
+    hpnn_g0_update u;
+    memset(&u, 0, sizeof u);
+    u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
+    u.cnt = g0cnt, u.err = g0cnt + 224;
+    u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;
+    u.mslab = midslab, u.mrows = mid_grid, u.mstride = slab_f, u.n12 = slab_f;
+    for (int l = 0; l < 2; l++) {
+        u.W32b[l] = W32[l + 1], u.V32b[l] = V32[l + 1], u.Wbb[l] = Wb[l + 1], u.Wtb[l] = Wt[l + 1];
+        u.Nb[l] = Np[l + 1], u.Kb[l] = Kp[l + 1];
+    }
+    return hpnn_gemm_fm_direct_update(D[0], fm, x.u8, x.u8 ? x.scale : 1.f, slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], &u,
+                                      s);
+}
+
 /* the weight gradient and the step can run as ONE 8-phase TN launch (no gradient in memory):
  * one split, 256 x 256 tiles, no fragment-major W0 copy to keep (HPNN_TN_UPD=0: off) */
 bool BPlan::tn_update_ok(int l) const {
@@ -383,6 +406,7 @@ int BPlan::step(const XIn &x, const int *labels, const float *T, int ldt, int n_
          * workgroups appended to its grid (they fill the CUs the GEMM tiles leave idle); every
          * layer's update in one launch */
         if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
+        if ((r = g0_fused_step(x, lr, alpha, scale, s)) != -1) return r; /* 2 launches */
         if ((r = g0_reduce(x, s))) return r;
         const long n1 = (long)Np[1] * Kp[1];
         hpnn_upd_layer u[3] = {
@@ -498,6 +522,15 @@ int BPlan::predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s)
     int r = forward(X, s);
     if (r) return r;
     return output(lab0, nullptr, 0, n_valid, O, ldo, false, s);
+}
+
+int BPlan::health(hipStream_t s) {
+    unsigned int e[2] = {0, 0};
+    if (g0cnt && hipMemcpyAsync(&e[0], g0cnt + 224, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
+    if (wwords && hipMemcpyAsync(&e[1], wwords + 2 * (Bp / TILE_W), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return -7;
+    if (hipStreamSynchronize(s) != hipSuccess) return -7;
+    return (e[0] || e[1]) ? -9 : 0;
 }
 
 int BPlan::read_stats(double *loss, unsigned int *hits, hipStream_t s) {

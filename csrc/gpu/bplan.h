@@ -15,8 +15,9 @@
  *
  * Modes (the step's kernel sequence):
  *   't'  MNIST-shaped n_in(800|256)-128-64-(<=32): mlp3_tile front (X -> delta1 + [G1|G2]
- *        block slabs) -> gemm_fm_direct G0 (+ first [G1|G2] reduction pass on tail
- *        workgroups) -> sgd_update_multi.  Input fragment-major (8-bit pixels or BF16).
+ *        block slabs) -> G0 with its split-K reduction and every layer's optimizer step in
+ *        the same launch (kernels_g0.hip g0_fused_kernel): two launches per step.  Input
+ *        fragment-major (8-bit pixels or BF16).
  *   'x'  same shape, 32-sample pipelined front (mlp3_fused), row-major BF16 input (plus an
  *        optional fragment-major 8-bit copy for G0).
  *   'm'  same shape, gemm_nt layer 0 + mlp3_mid.
@@ -80,6 +81,7 @@ class BPlan {
     int M[16], N[16], Kp[16], Np[16], S[16];
     char mode = 0;
     int mid_grid = 0, mid_groups = 1, wide_ksplit = 1, slab_f = 0;
+    bool g0_fused = true; /* modes t / x: G0 + reduction + every step in one launch when it applies */
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
 
@@ -129,6 +131,9 @@ class BPlan {
     int update_flat(const float *G, float lr, float alpha, float scale, hipStream_t s);
     /* network outputs O [Bp][ldo] FP32 of a row-major BF16 batch */
     int predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s);
+    /* 0, or -9 when an in-kernel hand-over (wide front partials, fused G0 splits) timed out
+     * since the plan was created (synchronises s) */
+    int health(hipStream_t s);
     /* (loss sum, hits) summed over the stat slots (synchronises s) */
     int read_stats(double *loss, unsigned int *hits, hipStream_t s);
 
@@ -138,7 +143,7 @@ class BPlan {
     float *Z = nullptr, *stats = nullptr, *gflat = nullptr, *midslab = nullptr, *midtmp = nullptr;
     void *W0f = nullptr;
     float *wpbuf = nullptr;
-    unsigned int *wwords = nullptr;
+    unsigned int *wwords = nullptr, *g0cnt = nullptr;
     int *lab0 = nullptr;
 
   private:
@@ -146,6 +151,7 @@ class BPlan {
     bool owns_ = false;
     int grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     int g0_reduce(const XIn &x, hipStream_t s);
+    int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     bool tn_update_ok(int l) const;
     const void *fm_input(const XIn &x) const;
     void name_pointers();

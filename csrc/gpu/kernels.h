@@ -85,6 +85,28 @@ int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_u8, float h
                                int M, int Bt, int splits, const float *rslab, int rS, long rstride, long rn,
                                int rgroups, float *rout, hipStream_t stream);
 
+/* the same GEMM with its split-K reduction and the optimizer step of layer 0 in the same
+ * launch, plus the [G1 | G2] block-slab reduction and the steps of layers 1, 2 on tail
+ * workgroups (the single-GPU fused MNIST step; kernels_g0.hip).  slab: scratch for the
+ * published partials.  Returns -1 when the shape is not covered (caller: the 3-launch form),
+ * HPNN_G0_FUSED=0 disables it. */
+typedef struct {
+    float *W32, *V32; /* layer 0 [N][M] FP32 master / momentum (V32 NULL for BP) */
+    void *Wb, *Wt, *Wf; /* BF16 W [N][M], W^T [M][N], fragment-major copy (may be NULL) */
+    unsigned int *cnt;  /* 256 words, zeroed once: tile counters (monotonic) */
+    unsigned int *err;  /* set when a wait for the other splits timed out */
+    float lr, alpha, scale;
+    int momentum;
+    const float *mslab; /* [G1 | G2] block slabs: mrows rows of n12 floats, mstride apart */
+    int mrows;
+    long mstride, n12;
+    float *W32b[2], *V32b[2]; /* layers 1, 2 */
+    void *Wbb[2], *Wtb[2];
+    int Nb[2], Kb[2];
+} hpnn_g0_update;
+int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
+                               int M, int Bt, int splits, const hpnn_g0_update *u, hipStream_t stream);
+
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)
  *   loss_acc[slot] += sum of per-sample loss over valid rows (slot array, above)

@@ -46,26 +46,25 @@ namespace {
 using hpnn::bf16x8;
 using hpnn::f32x4;
 using hpnn::TnTail;
+using hpnn::gu32;
+using hpnn::ld_sc1;
+using hpnn::st_sc1;
 
 /* Dg: [Bt/32][N/16][64][8], Hg: [Bt/32][M/16][64][8]; nbd = N / 16, nbh = M / 16.
  * HU8: Hg holds unsigned bytes (8 per lane per fragment), multiplied as exact integers;
  * hscale scales the FP32 result (G = hscale * D^T H) */
-template <int WF, int WH, int PD, int KW, bool HU8 = false>
-__global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
-                                                                  const void *__restrict__ Hg, int nbh, float hscale,
-                                                                  float *__restrict__ slab, int ldg, int N, int ksteps,
-                                                                  int splits, int tiles_n, int tiles, int xcd_map,
-                                                                  TnTail tail) {
-    if ((int)blockIdx.x >= tiles * splits) {
-        if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - tiles * splits);
-        return;
-    }
+/* the workgroup's partial product over its split of the batch: on return the waves of group
+ * kg == 0 hold the 32 WF x 32 WH tile (wave tile 16 WF x 16 WH) in acc; *tile_, *split_, m0 / n0
+ * (this wave's tile origin) are set.  Every wave returns (the caller's barriers need them). */
+template <int WF, int WH, int PD, int KW, bool HU8>
+__device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nbd, const void *__restrict__ Hg, int nbh,
+                                           int ksteps, int splits, int tiles_n, int tiles, int xcd_map,
+                                           f32x4 (&acc)[WF][WH], int &tile, int &split, int &m0, int &n0) {
     constexpr int R = PD + 1;
     constexpr int TMF = 32 * WF, TNH = 32 * WH; /* workgroup tile: features x delta columns */
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
-    int tile, split;
     if (xcd_map) { /* the tiles of one batch slice on one XCD: its Dt slice is fetched once into that L2 */
         const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
         tile = j % tiles;
@@ -74,7 +73,8 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
         tile = blockIdx.x % tiles;
         split = blockIdx.x / tiles;
     }
-    const int m0 = (tile / tiles_n) * TMF + wm * 16 * WF, n0 = (tile % tiles_n) * TNH + wn * 16 * WH;
+    m0 = (tile / tiles_n) * TMF + wm * 16 * WF;
+    n0 = (tile % tiles_n) * TNH + wn * 16 * WH;
     const int k0 = (int)((long)split * ksteps / splits), k1 = (int)((long)(split + 1) * ksteps / splits);
     /* this wave group's k-steps: k0 + kg, k0 + kg + KW, ... */
     const int nk = (k1 - k0 - kg + KW - 1) / KW;
@@ -85,7 +85,6 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
     const __bf16 *pb = Dg + ((size_t)(k0 + kg) * nbd + n0 / 16) * 512 + lane * 8;
     const size_t step_a = (size_t)KW * nbh * 512 * ES, step_b = (size_t)KW * nbd * 512; /* this group's next k-step */
 
-    f32x4 acc[WF][WH];
 #pragma unroll
     for (int i = 0; i < WF; i++)
 #pragma unroll
@@ -134,8 +133,6 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
             if (t + u < nk) mma(u);
     }
 
-    float *out = slab + (size_t)split * N * ldg;
-    const int q = lane >> 4;
     if constexpr (KW > 1) { /* groups 1.. hand their partial tiles to group 0 through LDS, in order */
         __shared__ f32x4 part[4][WF * WH][64];
 #pragma unroll
@@ -155,14 +152,198 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
             }
             if (g + 1 < KW) __syncthreads();
         }
-        if (kg != 0) return;
     }
+}
+
+template <int WF, int WH, int PD, int KW, bool HU8 = false>
+__global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
+                                                                  const void *__restrict__ Hg, int nbh, float hscale,
+                                                                  float *__restrict__ slab, int ldg, int N, int ksteps,
+                                                                  int splits, int tiles_n, int tiles, int xcd_map,
+                                                                  TnTail tail) {
+    if ((int)blockIdx.x >= tiles * splits) {
+        if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - tiles * splits);
+        return;
+    }
+    f32x4 acc[WF][WH];
+    int tile, split, m0, n0;
+    fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
+                                    n0);
+    if ((threadIdx.x >> 6) >= 4) return;
+    const int lane = threadIdx.x & 63, r16 = lane & 15, q = lane >> 4;
+    float *out = slab + (size_t)split * N * ldg;
 #pragma unroll
     for (int i = 0; i < WF; i++)
 #pragma unroll
         for (int j = 0; j < WH; j++)
             *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) =
                 HU8 ? acc[i][j] * hscale : acc[i][j];
+}
+
+/* ---- G0 with its split-K reduction and the optimizer step in the same launch ----------
+ * (the single-GPU MNIST step: front, then this, two launches).  Every GEMM workgroup
+ * publishes its FP32 partial tile with write-through (sc1) stores, drains them and adds one
+ * ticket to its tile's monotonic counter (agent scope); it then waits (sc1 polls, bounded)
+ * until all `splits` partials of the tile have arrived, reduces its 1/splits share of the
+ * tile over the splits in a FIXED order (sc1 loads; bitwise repeatable whatever the arrival
+ * order) and applies the BP / BPM step to those elements: FP32 master, momentum, BF16 W,
+ * W^T and the fragment-major copy the front reads.  Between its ticket and its wait every
+ * workgroup also sums 1/grid of the front's [G1 | G2] block slabs completely (fixed order)
+ * and steps layers 1 and 2 there (no tail workgroups: with 88 KB of LDS and 147 VGPRs they
+ * could not share a CU with a GEMM workgroup).  Replaces the
+ * separate sgd_update_multi launch (6.2 us) and its kernel boundary behind 20 MB of dirty
+ * slabs.  All GEMM workgroups are co-resident (grid <= CUs; a wait that times out sets
+ * *err instead of hanging).  Reference: the per-layer update of snn_kernel_train_momentum /
+ * cuda_snn.cu:2726-3717 (GER into dW, W += dW, dW *= alpha), batched. */
+constexpr unsigned long long G0_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
+
+__device__ __forceinline__ void bpm_step4(float *__restrict__ W32, float *__restrict__ V32, size_t idx, f32x4 g,
+                                          const hpnn_g0_update &u, f32x4 &w) {
+    w = *(const f32x4 *)(W32 + idx);
+    if (u.momentum) {
+        f32x4 v = *(const f32x4 *)(V32 + idx);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            v[r] += u.lr * (g[r] * u.scale);
+            w[r] += v[r];
+            v[r] *= u.alpha;
+        }
+        *(f32x4 *)(V32 + idx) = v;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) w[r] += u.lr * (g[r] * u.scale);
+    }
+    *(f32x4 *)(W32 + idx) = w;
+}
+
+/* element (n, k..k+3) of a [N][K] layer: FP32 master + BF16 W / W^T (+ fragment-major Wf) */
+__device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, __bf16 *Wt, __bf16 *Wf, int N, int K,
+                                           int n, int k, f32x4 g, const hpnn_g0_update &u) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    const size_t idx = (size_t)n * K + k;
+    f32x4 w;
+    bpm_step4(W32, V32, idx, g, u, w);
+    bf16x4 wb;
+#pragma unroll
+    for (int r = 0; r < 4; r++) wb[r] = (__bf16)w[r];
+    *(bf16x4 *)(Wb + idx) = wb;
+    if (Wf) { /* MFMA-fragment-major copy (kernels.h): 4 consecutive k stay contiguous */
+        const size_t fo = (((size_t)(n >> 4) * (K / 32) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+        *(bf16x4 *)(Wf + fo) = wb;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) Wt[(size_t)(k + r) * N + n] = wb[r];
+}
+
+/* [G1 | G2]: float4 columns [c0, c1) of the front's block slabs summed over all mrows rows in
+ * a fixed order (RG row groups of NT / 16 threads, met in LDS in order), then layers 1 / 2
+ * stepped at those elements */
+template <int NT>
+__device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long c1, f32x4 *red) {
+    constexpr int C4 = 16, RG = NT / C4;
+    const int t = threadIdx.x, c = t % C4, rg = t / C4;
+    for (long b0 = c0; b0 < c1; b0 += C4) {
+        const long e4 = b0 + c;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        if (e4 < c1)
+            for (int r = rg; r < u.mrows; r += RG) a += *(const f32x4 *)(u.mslab + (long)r * u.mstride + e4 * 4);
+        red[t] = a;
+        __syncthreads();
+        if (rg == 0 && e4 < c1) {
+            f32x4 g = red[c];
+            for (int r = 1; r < RG; r++) g += red[r * C4 + c];
+            long i = e4 * 4;
+            const int l = i < (long)u.Nb[0] * u.Kb[0] ? 0 : 1;
+            if (l) i -= (long)u.Nb[0] * u.Kb[0];
+            const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+            step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k,
+                       g, u);
+        }
+        __syncthreads();
+    }
+}
+
+template <int WF, int WH, int PD, int KW, bool HU8>
+__global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
+                                                            const void *__restrict__ Hg, int nbh, float hscale,
+                                                            float *__restrict__ slab, int ldg, int N, int ksteps,
+                                                            int splits, int tiles_n, int tiles, int xcd_map,
+                                                            hpnn_g0_update u) {
+    constexpr int NT = 256 * KW, TMF = 32 * WF, TNH = 32 * WH, NE4 = TMF * TNH / 4, PARTS = NT / 128;
+    __shared__ f32x4 red[NT];
+    f32x4 acc[WF][WH];
+    int tile, split, m0, n0;
+    fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
+                                    n0);
+    const int t = threadIdx.x, lane = t & 63;
+    /* publish this split's partial tile (write-through), then one ticket for the workgroup */
+    if ((t >> 6) < 4) {
+        const int r16 = lane & 15, q = lane >> 4;
+        float *out = slab + (size_t)split * N * ldg;
+#pragma unroll
+        for (int i = 0; i < WF; i++)
+#pragma unroll
+            for (int j = 0; j < WH; j++)
+                st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q, HU8 ? acc[i][j] * hscale : acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ unsigned int want_s;
+    if (t == 0) {
+        const unsigned int old = atomicAdd(u.cnt + 32 * tile, 1u);
+        want_s = old - old % (unsigned)splits + (unsigned)splits; /* this launch's last ticket */
+    }
+    /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
+    {
+        const long nb = (long)tiles * splits, nf = u.n12 / 4, b = blockIdx.x;
+        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red);
+    }
+    if (t == 0) {
+        unsigned int *cnt = u.cnt + 32 * tile;
+        const unsigned int want = want_s;
+        const unsigned long long t0 = wall_clock64();
+        while ((int)(__hip_atomic_load((gu32 *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > G0_TIMEOUT) {
+                __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
+     * float4, each summing a fixed run of splits; the runs meet in LDS in order */
+    const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
+    const int f = t % 128, part = t / 128;
+    const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
+    const int s0 = part * splits / PARTS, s1 = (part + 1) * splits / PARTS;
+    const size_t ss = (size_t)N * ldg;
+    for (int c0 = e0; c0 < e1; c0 += 128) {
+        const int e = c0 + f;
+        const int row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+        if (e < e1) {
+            const float *p = slab + (size_t)(nt0 + row) * ldg + col;
+            for (int s = s0; s < s1; s += 8) {
+                f32x4 v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    v[j] = s + j < s1 ? ld_sc1(p + (size_t)(s + j) * ss) : f32x4{0.f, 0.f, 0.f, 0.f};
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int j = 0; j < 8; j++) sum += v[j];
+            }
+        }
+        red[t] = sum;
+        __syncthreads();
+        if (part == 0 && e < e1) {
+            f32x4 g = red[f];
+#pragma unroll
+            for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
+            step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
+        }
+        __syncthreads();
+    }
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false>
@@ -203,6 +384,28 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
 }
 
 }  // namespace
+
+extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab,
+                                          int ldg, int N, int M, int Bt, int splits, const hpnn_g0_update *u,
+                                          hipStream_t stream) {
+    static const bool on = [] { const char *e = getenv("HPNN_G0_FUSED"); return !(e && e[0] == '0'); }();
+    /* the 160 x 128 tile configuration of fm_dispatch (8 waves) */
+    if (!on || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
+    if (!u->cnt || !u->err) return -1;
+    if (u->n12 % 4 || !u->mslab || u->mrows < 1 || (u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
+        return -2;
+    const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
+    if (tiles > 7) return -1; /* counters 32 words apart in a 256-word block, err at word 224 */
+    const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+#define HPNN_G0F(U8_)                                                                                              \
+    hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_>), dim3(tiles * splits), dim3(512), 0, stream,              \
+                       (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
+                       xcd_map, *u)
+    if (h_u8) HPNN_G0F(true);
+    else HPNN_G0F(false);
+#undef HPNN_G0F
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
                                    int M, int Bt, int splits, hipStream_t stream) {

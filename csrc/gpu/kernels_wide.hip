@@ -67,18 +67,7 @@ constexpr int LDS_TOTAL = OFF_RED + 5 * RED_W * 4 + 16;
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
 constexpr unsigned long long XCH_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
-typedef __attribute__((address_space(1))) unsigned int gu32;
 
-/* 16-byte write-through store / L1-bypassing load (global_*_dwordx4 ... sc1); the loads
- * are issued in a batch and drained by the caller's s_waitcnt vmcnt(0) */
-__device__ __forceinline__ void st_sc1(void *p, const f32x4 &v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ f32x4 ld_sc1(const void *p) {
-    f32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
 
 /* HPNN_WIDE_TRACE=1 (profiling only): s_memtime stamps of every workgroup's wave 0 at the
  * phase boundaries, [block][mark]; read back with hpnn_wide2_trace */

@@ -241,6 +241,18 @@ __device__ __forceinline__ float wave_sum(float v) {
     return rows_sum(v);
 }
 
+typedef __attribute__((address_space(1))) unsigned int gu32;
+/* 16-byte write-through store / L1-bypassing load (global_*_dwordx4 ... sc1); the loads
+ * are issued in a batch and drained by the caller's s_waitcnt vmcnt(0) */
+__device__ __forceinline__ void st_sc1(void *p, const f32x4 &v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_sc1(const void *p) {
+    f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
 /* Optional tail work of a TN launch: a grouped slab reduction (reduce_groups_kernel of
  * kernels_mlp3.hip: out[g*ostride + i] = sum of slabs [g*SG, min(S, (g+1)*SG)), float4 i)
  * run by extra workgroups appended to the GEMM grid.  The fused MNIST step reduces its

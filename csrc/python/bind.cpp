@@ -155,6 +155,8 @@ void bind_plan(py::module_ &m) {
              [](BPlan &p, uptr G, float lr, float alpha, float scale, uptr s) {
                  check(p.update_flat((const float *)P(G), lr, alpha, scale, S(s)), "BPlan.update_flat");
              })
+        .def("health", [](BPlan &p, uptr s) { return p.health(S(s)); })
+        .def_readwrite("g0_fused", &BPlan::g0_fused)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {
             check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
         });

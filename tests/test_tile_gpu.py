@@ -105,3 +105,36 @@ def test_tile_bitwise_repeatable(gpu):
         ms.append(m)
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(ms[0].W32, ms[1].W32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Bp", [24576, 4096])
+def test_fused_g0_update_matches_separate_update(gpu, Bp):
+    """G0 with its split-K reduction and every layer's step in one launch
+    (kernels_g0.hip g0_fused_kernel: write-through partials, per-tile tickets, fixed-order
+    reduction) == G0 slabs + the sgd_update_multi launch, up to the order of the FP32 sums;
+    and bitwise repeatable run to run (24576: 48 splits, the headline's split count)"""
+    runs = {}
+    for tag, fused in (("fused", True), ("fused2", True), ("sep", False)):
+        m, X = _case("SNN", 10, Bp, True, seed=5)
+        m.plan.g0_fused = fused
+        Xg = m.prepare_input(X.cuda())
+        g = torch.Generator(device="cuda").manual_seed(9)
+        W0 = [w.clone() for w in m.W32]
+        for _ in range(3):
+            lab = torch.randint(0, 10, (Bp,), dtype=torch.int32, device="cuda", generator=g)
+            m.train_step(Xg, labels=lab, lr=0.05)
+        torch.cuda.synchronize()
+        assert m.plan.health(torch.cuda.current_stream().cuda_stream) == 0
+        runs[tag] = (m, W0)
+    a, b = runs["fused"][0], runs["sep"][0]
+    for l in range(3):
+        assert torch.equal(a.W32[l], runs["fused2"][0].W32[l])  # repeatable
+        assert torch.equal(a.Wb[l], runs["fused2"][0].Wb[l]) and torch.equal(a.Wt[l], runs["fused2"][0].Wt[l])
+        dw = (b.W32[l] - runs["sep"][1][l]).abs().max().item()
+        assert (a.W32[l] - b.W32[l]).abs().max().item() <= 1e-4 * dw + 1e-7, l
+        assert torch.equal(a.Wb[l], a.W32[l].bfloat16()) and torch.equal(a.Wt[l], a.W32[l].bfloat16().t())
+        dv = (b.V32[l]).abs().max().item()
+        assert (a.V32[l] - b.V32[l]).abs().max().item() <= 1e-4 * dv + 1e-8, l
+    from hpnn_amd import ops
+    assert torch.equal(a.W0f, ops.frag_major(a.W32[0].bfloat16()))
