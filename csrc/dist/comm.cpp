@@ -322,6 +322,23 @@ extern "C" int hpnn_comm_all_reduce_async(hpnn_comm *c, void *buf, long count, h
     return 0;
 }
 
+extern "C" hipStream_t hpnn_comm_fork(hpnn_comm *c, hipStream_t compute) {
+    if (!c || !c->side) return nullptr;
+    const int i = c->next;
+    if (hipEventRecord(c->ev_in[i], compute) != hipSuccess) return nullptr;
+    if (hipStreamWaitEvent(c->side, c->ev_in[i], 0) != hipSuccess) return nullptr;
+    return c->side;
+}
+
+extern "C" int hpnn_comm_fork_done(hpnn_comm *c) {
+    if (!c) return -1;
+    const int i = c->next;
+    c->next = (c->next + 1) % EV_RING;
+    if (hipEventRecord(c->ev_out[i], c->side) != hipSuccess) return -2;
+    c->pending = i;
+    return 0;
+}
+
 extern "C" int hpnn_comm_join(hpnn_comm *c, hipStream_t compute) {
     if (!c) return -1;
     if (c->pending < 0) return 0;

@@ -1,0 +1,105 @@
+/*
+ * Native data-parallel step over RCCL: FP32 bucket all-reduce or BF16 reduce-scatter +
+ * sharded optimizer step + BF16 all-gather, overlapped with the backward (dp_exchange.h).
+ */
+#include "dp_exchange.h"
+
+#include <libhpnn.h>
+#include <libhpnn/devmem.h>
+
+namespace hpnn {
+
+DpExchange::~DpExchange() {
+    hpnn_dev_free(send16_);
+    hpnn_dev_free(recv16_);
+    hpnn_dev_free(gather32_);
+}
+
+int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
+    if (!plan || !comm) return -1;
+    p_ = plan;
+    c_ = comm;
+    rank_ = hpnn_comm_rank(comm);
+    world_ = hpnn_comm_size(comm);
+    mode_ = mode == BF16RS ? BF16RS : FP32;
+    sharded_.assign(p_->L, false);
+    if (mode_ == FP32) return 0;
+    if (p_->mode) {
+        NN_ERROR(stderr, "BF16 reduce-scatter exchange needs the per-layer plan (mode %c)\n", p_->mode);
+        return -2;
+    }
+    size_t mx = 0;
+    for (int l = 0; l < p_->L; l++) {
+        /* rows split evenly, each rank's block whole 32-row pieces (the transposes) */
+        sharded_[l] = world_ > 1 && p_->Np[l] % world_ == 0;
+        if (sharded_[l]) mx = mx > (size_t)p_->Np[l] * p_->Kp[l] ? mx : (size_t)p_->Np[l] * p_->Kp[l];
+    }
+    if (mx && (hpnn_dev_malloc(&send16_, mx * 2) != hipSuccess ||
+               hpnn_dev_malloc(&recv16_, mx * 2 / world_ + 64) != hipSuccess))
+        return -7;
+    return 0;
+}
+
+int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, int n_total, float lr,
+                     float alpha, hipStream_t s) {
+    const float scale = 1.0f / (float)(n_total > 0 ? n_total : 1);
+    const int mom = p_->momentum ? 1 : 0;
+    int err = 0;
+    auto layer_rs = [&](int l) -> int {
+        /* on the side stream, after the compute stream's work so far (this gradient) */
+        hipStream_t side = hpnn_comm_fork(c_, s);
+        if (!side) return -2;
+        const int N = p_->Np[l], K = p_->Kp[l], rp = N / world_;
+        const long cnt = (long)rp * K, off = (long)rank_ * cnt;
+        int r = hpnn_cast_f32_bf16(p_->gflat + p_->goff[l], send16_, (long)N * K, side);
+        if (!r) r = hpnn_comm_reduce_scatter(c_, send16_, recv16_, cnt, HPNN_DT_BF16, HPNN_OP_SUM, side);
+        if (!r)
+            r = hpnn_sgd_update_rows_bf16g(p_->W32[l] + off, p_->V32[l] ? p_->V32[l] + off : nullptr, recv16_, cnt, lr,
+                                           alpha, scale, mom, (char *)p_->Wb[l] + off * 2, side);
+        if (!r) r = hpnn_comm_all_gather(c_, (char *)p_->Wb[l] + off * 2, p_->Wb[l], cnt, HPNN_DT_BF16, side);
+        if (!r) r = hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], N, K, side);
+        const int rd = hpnn_comm_fork_done(c_);
+        return r ? r : rd;
+    };
+    auto ready = [&](int lo, int hi) -> bool {
+        if (err) return true; /* keep issuing nothing more; the step reports the error */
+        if (mode_ == BF16RS) {
+            for (int l = hi; l >= lo && !err; l--) {
+                if (sharded_[l]) err = layer_rs(l);
+                else err = hpnn_comm_all_reduce_async(c_, p_->gflat + p_->goff[l], (long)(p_->goff[l + 1] - p_->goff[l]),
+                                                      HPNN_DT_F32, s);
+            }
+            return err == 0;
+        }
+        err = hpnn_comm_all_reduce_async(c_, p_->gflat + p_->goff[lo], (long)(p_->goff[hi + 1] - p_->goff[lo]),
+                                         HPNN_DT_F32, s);
+        return err == 0;
+    };
+    int r = p_->grads(x, labels, T, ldt, n_valid, ready, s);
+    const int j = hpnn_comm_join(c_, s);
+    if (r || err || j) {
+        NN_ERROR(stderr, "data-parallel step failed (grads %d, exchange %d, join %d)\n", r, err, j);
+        return r ? r : (err ? err : j);
+    }
+    if (mode_ == FP32) return p_->update_flat(p_->gflat, lr, alpha, scale, s);
+    for (int l = 0; l < p_->L; l++)
+        if (!sharded_[l] && (r = p_->update_layer(l, lr, alpha, scale, true, s))) return r;
+    return 0;
+}
+
+int DpExchange::gather_masters(hipStream_t s) {
+    if (mode_ != BF16RS) return 0;
+    for (int l = 0; l < p_->L; l++) {
+        if (!sharded_[l]) continue;
+        const long cnt = (long)(p_->Np[l] / world_) * p_->Kp[l], off = (long)rank_ * cnt;
+        float *bufs[2] = {p_->W32[l], p_->V32[l]};
+        for (float *b : bufs) {
+            if (!b) continue;
+            /* in place: this rank's rows sit at rank * cnt already */
+            if (hpnn_comm_all_gather(c_, b + off, b, cnt, HPNN_DT_F32, s)) return -3;
+        }
+    }
+    return 0;
+}
+
+}  // namespace hpnn

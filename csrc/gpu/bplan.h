@@ -143,7 +143,7 @@ class BPlan {
     float *Z = nullptr, *stats = nullptr, *gflat = nullptr, *midslab = nullptr, *midtmp = nullptr;
     void *W0f = nullptr;
     float *wpbuf = nullptr;
-    unsigned int *wwords = nullptr, *g0cnt = nullptr;
+    unsigned int *wwords = nullptr, *g0cnt = nullptr, *tncnt = nullptr;
     int *lab0 = nullptr;
 
   private:

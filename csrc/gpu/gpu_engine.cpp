@@ -36,6 +36,7 @@
 #include "engine.h"
 #include "kernels.h"
 #include "bplan.h"
+#include "../dist/dp_exchange.h"
 
 #define HIPCHK(x)                                                                           \
     do {                                                                                    \
@@ -742,6 +743,20 @@ struct Batched {
         return p.update_flat(G, lr, alpha, scale, s) == 0;
     }
 
+    /* one process per GPU: the library's data-parallel step (dp_exchange.h) */
+    std::unique_ptr<hpnn::DpExchange> dpx;
+    bool attach_dpx(hpnn_comm *c, int mode) {
+        dpx.reset(new hpnn::DpExchange());
+        if (dpx->init(&p, c, mode)) dpx.reset();
+        return (bool)dpx;
+    }
+    BOOL dp_step(const XSet &xs, long row, const float *T, int ldt, int nv, int total, float lr, float alpha) {
+        return dpx && dpx->step(at(xs, row), nullptr, T, ldt, nv, total, lr, alpha, s) == 0;
+    }
+    BOOL gather_masters() { return !dpx || dpx->gather_masters(s) == 0; }
+    bool has_dpx() const { return (bool)dpx; }
+    void detach_dpx() { dpx.reset(); }
+
     /* FP32 master weights (and BPM momentum, into k->dw) -> host FP64 */
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
@@ -996,6 +1011,12 @@ struct BatchedFP {
                 return FALSE;
         return TRUE;
     }
+
+    bool attach_dpx(hpnn_comm *, int) { return false; } /* FP32 / FP64: the generic bucket loop */
+    BOOL dp_step(const XSet &, long, const T *, int, int, int, double, double) { return FALSE; }
+    BOOL gather_masters() { return TRUE; }
+    bool has_dpx() const { return false; }
+    void detach_dpx() {}
 
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
@@ -1431,8 +1452,13 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const int Bg = (B + W - 1) / W;
     const bool mom = o->train == NN_TRAIN_BPM;
     const int n_out = (int)k->n_outputs;
+    /* HPNN_GRAD_COMM=bf16rs: BF16 reduce-scatter + sharded step + BF16 all-gather (RCCL,
+     * per-layer plan); every rank reads the same environment */
+    const char *gce = getenv("HPNN_GRAD_COMM");
+    const bool bf16rs = gce && !strcmp(gce, "bf16rs");
     Net net;
-    if (!net.init(k, Bg, o->type, mom, s, B % 32 == 0 && Bg % 32 == 0) || !net.alloc_flat()) return FALSE;
+    if (!net.init(k, Bg, o->type, mom, s, B % 32 == 0 && Bg % 32 == 0, bf16rs ? 0 : -1) || !net.alloc_flat())
+        return FALSE;
     if (mom && o->resume && !net.upload_momentum(k)) return FALSE;
     const size_t count = net.flat_count();
     /* gradient exchange: one-shot xGMI all-reduce when every rank is on this node and the
@@ -1443,7 +1469,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const char *lws = getenv("LOCAL_WORLD_SIZE");
     /* the xGMI all-reduce sums FP32; FP64 gradients go through RCCL */
     bool use_xar = Net::comm_dt == HPNN_DT_F32 && !(xe && xe[0] == '0') && lws && atoi(lws) == W &&
-                   W <= HPNN_XAR_MAX_RANKS && count * 4 <= ((size_t)4 << 20);
+                   W <= HPNN_XAR_MAX_RANKS && count * 4 <= ((size_t)4 << 20) && !bf16rs;
     if (use_xar) {
         xar = hpnn_xar_create(R, W, count * 4);
         std::vector<char> h(HPNN_XAR_HANDLE_BYTES, 0), all((size_t)W * HPNN_XAR_HANDLE_BYTES);
@@ -1472,6 +1498,10 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         if (hpnn_boot_allgather(id, sizeof id, all.data()) != 0) return FALSE;
         comm = hpnn_comm_init_rank(all.data(), W, R, dev); /* rank 0's id */
         if (!comm) return FALSE;
+        /* BF16 batched engine: the library's overlapped data-parallel step (dp_exchange.h);
+         * FP32 / FP64 engines: the bucket loop below */
+        if (!net.attach_dpx(comm, bf16rs ? hpnn::DpExchange::BF16RS : hpnn::DpExchange::FP32) && bf16rs)
+            NN_WARN(stderr, "bf16rs exchange unavailable for this net: FP32 all-reduce\n");
     }
     NN_OUT(stdout, "data-parallel batched training: %d processes (%s, %s), %d samples per rank per step\n", W,
            use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Net::name(), Bg);
@@ -1497,6 +1527,11 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             int nv = end - start;
             nv = nv < 0 ? 0 : (nv > Bg ? Bg : nv);
             const TT *tb = Td + (size_t)start * n_out;
+            const int total = end - b * B;
+            if (net.has_dpx()) {
+                ok = net.dp_step(Xd, start, tb, n_out, nv, total, o->lr, o->alpha);
+                continue;
+            }
             if (use_xar) {
                 /* small gradients: ONE latency-bound xGMI all-reduce of the whole buffer */
                 ok = net.grads(Xd, start, tb, n_out, nv);
@@ -1516,7 +1551,6 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                 for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
                 ok = (hpnn_comm_join(comm, s) == 0) && ok;
             }
-            const int total = end - b * B;
             if (ok) ok = net.update_flat(net.gflat, o->lr, o->alpha, 1.0 / (double)(total > 0 ? total : 1),
                                          mom);
         }
@@ -1544,6 +1578,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                                (UINT64)n * (e + 1));
     }
     auto t1 = std::chrono::steady_clock::now();
+    if (ok) ok = net.gather_masters(); /* bf16rs: every rank's rows of the FP32 masters */
     if (ok) ok = net.download(k);
     if (ok && st) {
         st->seconds = std::chrono::duration<double>(t1 - t0).count();
@@ -1553,6 +1588,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         st->last_loss = st->epoch_loss;
     }
     hipStreamSynchronize(s);
+    net.detach_dpx(); /* before the communicator goes */
     hpnn_boot_finish(); /* every rank is past its last all-reduce before any buffer goes */
     Xd.release();
     if (Td) hpnn_dev_free(Td);

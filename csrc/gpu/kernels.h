@@ -54,6 +54,12 @@ int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, vo
  * slab.  N % 256 == 0, M % 256 == 0, Bt % 128 == 0, else -1. */
 int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
                          void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum, hipStream_t stream);
+/* the same with the gradient over `splits` (>= 2) split-K slabs reduced inside the launch (each
+ * split publishes its partial write-through; the splits of a tile meet through tickets in
+ * cnt, 1024 words zeroed once; err set on a timeout): -1 when not covered */
+int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, int splits,
+                               float *slab, float *W32, float *V32, void *Wbf, void *Wt, float lr, float alpha,
+                               float scale, int momentum, unsigned int *cnt, unsigned int *err, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
@@ -158,6 +164,14 @@ int hpnn_pack_bf16(const void *src, int src_f64, int rows, int cols, int lds, vo
 
 /* FP32 master <-> BF16 copies without an update (after load/broadcast) */
 int hpnn_cast_weights(const float *W32, void *Wbf, void *Wt, int N, int K, hipStream_t stream);
+
+/* BF16 reduce-scatter data parallelism (csrc/dist/dp_exchange.cpp): dst = bf16(src), n % 4 == 0;
+ * the step of n consecutive master elements from a BF16 gradient sum (W32, V32, Wbf rows);
+ * Wt [K][N] = Wbf^T */
+int hpnn_cast_f32_bf16(const float *src, void *dst, long n, hipStream_t stream);
+int hpnn_sgd_update_rows_bf16g(float *W32, float *V32, const void *G16, long n, float lr, float alpha, float scale,
+                               int momentum, void *Wbf, hipStream_t stream);
+int hpnn_transpose_bf16(const void *Wbf, void *Wt, int N, int K, hipStream_t stream);
 
 /* zero-fill helper usable inside graphs */
 int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream);

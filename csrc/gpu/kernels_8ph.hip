@@ -280,9 +280,17 @@ struct Tn8Upd {
     __bf16 *Wb, *Wt;
     float lr, alpha, scale;
     int momentum;
+    unsigned int *cnt, *err; /* MODE 2: per-tile tickets (32 words apart, zeroed once), error word */
 };
 
-template <bool UPD>
+constexpr unsigned long long TN8_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
+
+/* MODE 0: split-K slabs; 1: one split, the optimizer step in the epilogue; 2: several splits,
+ * each publishes its partial tile write-through and takes a ticket, then -- once every split
+ * of the tile has arrived -- reduces 1/splits of the tile over the splits in a fixed order
+ * and applies the step there (the split-K reduction and the update launch of the RRUFF-shaped
+ * first layer move into this launch; the protocol of kernels_g0.hip g0_fused_kernel) */
+template <int MODE>
 __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict__ D, int ldd,
                                                        const __bf16 *__restrict__ H, int ldh,
                                                        float *__restrict__ slab, int ldg, int N, int units,
@@ -460,7 +468,75 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 
     float *out = slab + (size_t)split * N * ldg;
     const int r16 = lane & 15, q = lane >> 4;
-    if constexpr (UPD) {
+    if constexpr (MODE == 2) {
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
+                        const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                        hpnn::st_sc1(out + (size_t)n * ldg + m, acc[mi][ni][i][j]);
+                    }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            unsigned int *cnt = upd.cnt + 32 * tile;
+            const unsigned int old = atomicAdd(cnt, 1u);
+            const unsigned int want = old - old % (unsigned)splits + (unsigned)splits;
+            const unsigned long long t0 = wall_clock64();
+            while ((int)(__hip_atomic_load((hpnn::gu32 *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > TN8_TIMEOUT) {
+                    __hip_atomic_store((hpnn::gu32 *)upd.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        constexpr int NE4 = 256 * 256 / 4;
+        const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
+        const size_t ss = (size_t)N * ldg;
+        for (int e = e0 + tid; e < e1; e += 512) {
+            const int n = n0 + e / 64, m = m0 + 4 * (e % 64);
+            const float *p = slab + (size_t)n * ldg + m;
+            f32x4 g = {0.f, 0.f, 0.f, 0.f};
+            for (int s0 = 0; s0 < splits; s0 += 8) {
+                f32x4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    v[k] = s0 + k < splits ? hpnn::ld_sc1(p + (size_t)(s0 + k) * ss) : f32x4{0.f, 0.f, 0.f, 0.f};
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int k = 0; k < 8; k++) g += v[k];
+            }
+            const size_t idx = (size_t)n * ldg + m;
+            f32x4 ww = *(const f32x4 *)(upd.W32 + idx);
+            if (upd.momentum) {
+                f32x4 vv = *(const f32x4 *)(upd.V32 + idx);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    vv[r] += upd.lr * (g[r] * upd.scale);
+                    ww[r] += vv[r];
+                    vv[r] *= upd.alpha;
+                }
+                *(f32x4 *)(upd.V32 + idx) = vv;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; r++) ww[r] += upd.lr * (g[r] * upd.scale);
+            }
+            *(f32x4 *)(upd.W32 + idx) = ww;
+            bf16x4 wb;
+#pragma unroll
+            for (int r = 0; r < 4; r++) wb[r] = (__bf16)ww[r];
+            *(bf16x4 *)(upd.Wb + idx) = wb;
+#pragma unroll
+            for (int r = 0; r < 4; r++) upd.Wt[(size_t)(m + r) * N + n] = wb[r];
+        }
+    } else if constexpr (MODE == 1) {
         /* W [N][ldg]: W32 / V32 / Wb row-major, Wt [ldg][N].  Per quadrant: all loads
          * first (8 fragments in flight), then the step, then the stores -- a load / use /
          * store chain per fragment would leave the epilogue latency-bound */
@@ -648,7 +724,7 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     if (units % splits || (units / splits) % 2) return -1;
     if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    hipLaunchKernelGGL(gemm_tn8_kernel<false>, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream,
+    hipLaunchKernelGGL(gemm_tn8_kernel<0>, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream,
                        (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles,
                        tail, Tn8Upd{});
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -667,9 +743,40 @@ extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int l
     if (((uintptr_t)W32 | (uintptr_t)(momentum ? V32 : W32) | (uintptr_t)Wbf | (uintptr_t)Wt) & 15) return -1;
     if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum};
-    hipLaunchKernelGGL(gemm_tn8_kernel<true>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
+    const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, nullptr, nullptr};
+    hipLaunchKernelGGL(gemm_tn8_kernel<1>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
                        (const __bf16 *)H, ldh, nullptr, M, N, Bt / 64, 1, tiles_n, ntiles, hpnn::TnTail{}, u);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* the same step for a gradient over `splits` splits (>= 2), reduced inside the launch
+ * (MODE 2 above): slab is the scratch the partials are published through ([splits][N][M]).
+ * -1: shape not covered, or more workgroups than CUs (every split of a tile must be
+ * resident at once), or HPNN_TN8_FUSED=0. */
+extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt,
+                                          int splits, float *slab, float *W32, float *V32, void *Wbf, void *Wt,
+                                          float lr, float alpha, float scale, int momentum, unsigned int *cnt,
+                                          unsigned int *err, hipStream_t stream) {
+    static const bool on = [] { const char *e = getenv("HPNN_TN8_FUSED"); return !(e && e[0] == '0'); }();
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
+            cus = -1;
+    }
+    if (!on || splits < 2 || !slab || !cnt || !err) return -1;
+    if (N % 256 || M % 256 || Bt % 128 || ldd % 8 || ldh % 8 || !W32 || !Wbf || !Wt || (momentum && !V32)) return -1;
+    if (((uintptr_t)W32 | (uintptr_t)(momentum ? V32 : W32) | (uintptr_t)Wbf | (uintptr_t)slab) & 15) return -1;
+    if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
+    const int units = Bt / 64;
+    if (units % splits || (units / splits) % 2) return -1;
+    const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
+    /* tickets: 32 words apart in 1024; at least half the CUs busy (a few-tile gradient, e.g.
+     * RRUFF's 256 x 256 second layer, would reduce megabytes per workgroup) */
+    if (ntiles > 31 || ntiles * splits > cus || 2 * ntiles * splits < cus) return -1;
+    const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, cnt, err};
+    hipLaunchKernelGGL(gemm_tn8_kernel<2>, dim3(ntiles * splits), dim3(512), 0, stream, (const __bf16 *)D, ldd,
+                       (const __bf16 *)H, ldh, slab, M, N, units, splits, tiles_n, ntiles, hpnn::TnTail{}, u);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

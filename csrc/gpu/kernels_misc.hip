@@ -742,6 +742,63 @@ __global__ __launch_bounds__(512) void sgd_update_multi_sub_kernel(UpdArgs a) {
     }
 }
 
+/* ---- pieces of the BF16 reduce-scatter data-parallel step (csrc/dist/dp_exchange.cpp) ---- */
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float *__restrict__ src, __bf16 *__restrict__ dst,
+                                                            long n4) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const f32x4 v = ((const f32x4 *)src)[i];
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; r++) o[r] = (__bf16)v[r];
+        ((bf16x4_t *)dst)[i] = o;
+    }
+}
+
+/* the optimizer step of this rank's rows from their BF16 gradient sum: W32 / V32 rows (FP32
+ * masters, sharded) and the BF16 compute rows Wb (all-gathered afterwards) */
+__global__ __launch_bounds__(256) void sgd_rows_bf16g_kernel(float *__restrict__ W32, float *__restrict__ V32,
+                                                             const __bf16 *__restrict__ G, long n4, float lr,
+                                                             float alpha, float scale, int momentum,
+                                                             __bf16 *__restrict__ Wb) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const bf16x4_t g16 = ((const bf16x4_t *)G)[i];
+        f32x4 w = ((const f32x4 *)W32)[i];
+        if (momentum) {
+            f32x4 v = ((const f32x4 *)V32)[i];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                v[r] += lr * ((float)g16[r] * scale);
+                w[r] += v[r];
+                v[r] *= alpha;
+            }
+            ((f32x4 *)V32)[i] = v;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) w[r] += lr * ((float)g16[r] * scale);
+        }
+        ((f32x4 *)W32)[i] = w;
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; r++) o[r] = (__bf16)w[r];
+        ((bf16x4_t *)Wb)[i] = o;
+    }
+}
+
+/* Wt [K][N] = Wb^T for a [N][K] BF16 matrix, 32 x 32 tiles through LDS */
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16 *__restrict__ Wb, __bf16 *__restrict__ Wt,
+                                                             int N, int K) {
+    __shared__ __bf16 t[32][34];
+    const int tk = K / 32, tn = blockIdx.x / tk, tkk = blockIdx.x % tk;
+    const int x = threadIdx.x & 31, y = threadIdx.x >> 5; /* y 0..7 */
+#pragma unroll
+    for (int j = 0; j < 4; j++) t[y + 8 * j][x] = Wb[(size_t)(tn * 32 + y + 8 * j) * K + tkk * 32 + x];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; j++) Wt[(size_t)(tkk * 32 + y + 8 * j) * N + tn * 32 + x] = t[x][y + 8 * j];
+}
+
 __global__ void pack_bf16_kernel(const void *__restrict__ src, int src_f64, int rows, int cols, int lds,
                                  __bf16 *__restrict__ dst, int prow, int pcol, int ldd) {
     const long total = (long)prow * pcol;
@@ -866,6 +923,30 @@ extern "C" int hpnn_sgd_update_multi(const hpnn_upd_layer *layers, int n, float 
         hipLaunchKernelGGL(sgd_update_multi_sub_kernel, dim3(4 * t), dim3(512), 0, stream, a);
     } else
         hipLaunchKernelGGL(sgd_update_multi_kernel, dim3(t), dim3(256), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_cast_f32_bf16(const float *src, void *dst, long n, hipStream_t stream) {
+    if (n <= 0 || n % 4 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 7)) return -2;
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, stream, src, (__bf16 *)dst,
+                       n / 4);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_sgd_update_rows_bf16g(float *W32, float *V32, const void *G16, long n, float lr, float alpha,
+                                          float scale, int momentum, void *Wbf, hipStream_t stream) {
+    if (n <= 0 || n % 4 || (momentum && !V32) || (((uintptr_t)W32 | (uintptr_t)(momentum ? V32 : W32)) & 15) ||
+        (((uintptr_t)G16 | (uintptr_t)Wbf) & 7))
+        return -2;
+    hipLaunchKernelGGL(sgd_rows_bf16g_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, stream, W32, V32,
+                       (const __bf16 *)G16, n / 4, lr, alpha, scale, momentum, (__bf16 *)Wbf);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_transpose_bf16(const void *Wbf, void *Wt, int N, int K, hipStream_t stream) {
+    if (N <= 0 || K <= 0 || N % 32 || K % 32) return -2;
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N / 32) * (K / 32)), dim3(256), 0, stream, (const __bf16 *)Wbf,
+                       (__bf16 *)Wt, N, K);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

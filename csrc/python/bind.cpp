@@ -18,6 +18,7 @@
 
 #include "../gpu/kernels.h"
 #include "../gpu/bplan.h"
+#include "../dist/dp_exchange.h"
 #include <libhpnn/comm.h>
 #include <libhpnn/xar.h>
 #include <libhpnn/devmem.h>
@@ -161,10 +162,34 @@ void bind_plan(py::module_ &m) {
             check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
         });
 }
+/* native data-parallel step (csrc/dist/dp_exchange.h): keeps its plan alive */
+void bind_dpx(py::module_ &m) {
+    py::class_<hpnn::DpExchange>(m, "DpExchange")
+        .def(py::init([](BPlan &plan, uptr comm, int mode) {
+                 auto *d = new hpnn::DpExchange();
+                 const int rc = d->init(&plan, (hpnn_comm *)comm, mode);
+                 if (rc) {
+                     delete d;
+                     throw std::runtime_error("DpExchange init failed (rc=" + std::to_string(rc) + ")");
+                 }
+                 return d;
+             }),
+             py::keep_alive<1, 2>())
+        .def("step",
+             [](hpnn::DpExchange &d, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid,
+                int n_total, float lr, float alpha, uptr s) {
+                 check(d.step(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid, n_total,
+                              lr, alpha, S(s)),
+                       "DpExchange.step");
+             })
+        .def("gather_masters", [](hpnn::DpExchange &d, uptr s) { check(d.gather_masters(S(s)), "gather_masters"); })
+        .def("sharded", &hpnn::DpExchange::sharded);
+}
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
     bind_plan(m);
+    bind_dpx(m);
     m.doc() = "libhpnn gfx950 kernels (MFMA GEMMs, fused output/optimizer kernels)";
     m.attr("EPI_NONE") = (int)HPNN_EPI_NONE;
     m.attr("EPI_ACT") = (int)HPNN_EPI_ACT;

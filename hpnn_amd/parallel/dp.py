@@ -53,6 +53,7 @@ class DataParallel:
             self.sharded = {l for l in range(model.L) if model.Np[l] % self.world == 0}
         self.buckets = self._plan(bucket_bytes)
         self.native = None
+        self.dpx = None
         on_gpu = getattr(model, "device", torch.device("cpu")).type == "cuda"
         if self.active and on_gpu and comm == "xar":
             from .comm import NativeComm
@@ -60,6 +61,14 @@ class DataParallel:
         elif self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
             from .comm import NativeComm
             self.native = NativeComm(group, device=model.device.index)
+        if self.native is not None and self.native.h and self.world > 1:
+            # the library's data-parallel step (csrc/dist/dp_exchange.h): per-layer exchange on
+            # the communicator's side stream, overlapped with the backward; BF16 reduce-scatter
+            # + sharded step + BF16 all-gather for grad_comm="bf16rs" (no per-step allocation)
+            from .._lib import native as _native
+            self.dpx = _native().DpExchange(model.plan, self.native.h, 1 if self.sharded else 0)
+            if self.sharded:
+                self.sharded = {l for l in range(model.L) if self.dpx.sharded(l)}
 
     def _plan(self, bucket_bytes):
         """Group layers (descending = production order) into contiguous buckets."""
@@ -144,6 +153,10 @@ class DataParallel:
         if (self.native is not None and self.native.xar and getattr(m, "fused_mode", None) in ("x", "t")
                 and m.grad_flat.numel() * 4 <= self.native.xar_max):
             return self._fused_xgmi_step(X, labels, T, n_valid, lr, alpha)
+        if self.dpx is not None:
+            self.dpx.step(*m._x(X), *m._tgt(labels, T), int(n_valid), int(n_valid) * self.world, float(lr),
+                          float(alpha), torch.cuda.current_stream().cuda_stream)
+            return
         works = []
         done = set()
 
@@ -191,6 +204,8 @@ class DataParallel:
             out.copy_(torch.cat(parts))
 
     def _sharded_step(self, X, labels, T, n_valid, lr, alpha):
+        """bf16rs over torch.distributed (gloo / CPU tests: the emulation of the native
+        DpExchange step's math; GPU runs with the native communicator take self.dpx)"""
         m, W = self.m, self.world
         m.backward_grads(X, labels=labels, T=T, n_valid=n_valid, reduce=True)
         scale = 1.0 / (n_valid * W)
@@ -219,6 +234,9 @@ class DataParallel:
     def gather_masters(self):
         """bf16rs: the FP32 master weights / momentum rows of every rank onto every rank"""
         m = self.m
+        if self.dpx is not None:
+            self.dpx.gather_masters(torch.cuda.current_stream().cuda_stream)
+            return
         for l in sorted(self.sharded):
             rp = m.Np[l] // self.world
             r0 = self.rank * rp

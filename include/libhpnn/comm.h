@@ -77,6 +77,11 @@ int hpnn_comm_group_end(void);
 
 /* overlapped sum all-reduce on the side stream (see header comment) */
 int hpnn_comm_all_reduce_async(hpnn_comm *c, void *buf, long count, hpnn_comm_dtype dt, hipStream_t compute);
+/* general fork: the side stream, ordered after what `compute` has enqueued so far; the caller
+ * enqueues kernels and collectives on it, then hpnn_comm_fork_done so hpnn_comm_join covers
+ * them.  NULL on failure. */
+hipStream_t hpnn_comm_fork(hpnn_comm *c, hipStream_t compute);
+int hpnn_comm_fork_done(hpnn_comm *c);
 /* compute stream waits for every collective issued with *_async so far */
 int hpnn_comm_join(hpnn_comm *c, hipStream_t compute);
 

@@ -137,8 +137,37 @@ def test_rruff_step_wide_vs_layerwise(gpu):
         mw.train_step(Xw, labels=lab, lr=0.01, alpha=0.2)
         ml.train_step(Xl, labels=lab, lr=0.01, alpha=0.2)
     torch.cuda.synchronize()
-    mw.wide_ws.check()
+    assert mw.plan.health(torch.cuda.current_stream().cuda_stream) == 0
     for a, b in zip(mw.host_weights(), ml.host_weights()):
         assert (a - b).abs().max().item() < 2e-3 * (b.abs().max().item() + 1e-3)
     (la, ca), (lb, cb) = mw.read_stats(), ml.read_stats()
     assert abs(la - lb) <= 1e-3 * abs(lb) and abs(ca - cb) <= 0.002 * 3 * B
+
+
+@pytest.mark.parametrize("B", [8192])
+def test_rruff_fused_tn8_update_matches_separate_update(gpu, B):
+    """the RRUFF-shaped first layer's gradient over 16 split-K slices reduced and stepped
+    inside the 8-phase TN launch (kernels_8ph.hip MODE 2: write-through partials, per-tile
+    tickets, fixed-order sums) == slabs + the separate update launch, up to the order of the
+    FP32 sums; bitwise repeatable run to run"""
+    sizes = [4096, 230, 230]
+    runs = {}
+    for tag, fused in (("fused", True), ("fused2", True), ("sep", False)):
+        torch.manual_seed(4)
+        m = MLP(sizes, "SNN", batch=B, momentum=True, seed=8)
+        assert m.fused_mode == "w" and m.S[0] > 1
+        m.plan.g0_fused = fused
+        X = m.prepare_input(torch.rand(B, sizes[0]).cuda())
+        W0 = [w.clone() for w in m.W32]
+        for i in range(3):
+            lab = torch.randint(0, sizes[-1], (B,), dtype=torch.int32, device="cuda")
+            m.train_step(X, labels=lab, lr=0.01, alpha=0.2)
+        torch.cuda.synchronize()
+        assert m.plan.health(torch.cuda.current_stream().cuda_stream) == 0
+        runs[tag] = (m, W0)
+    a, b = runs["fused"][0], runs["sep"][0]
+    for l in range(2):
+        assert torch.equal(a.W32[l], runs["fused2"][0].W32[l]) and torch.equal(a.Wt[l], runs["fused2"][0].Wt[l])
+        dw = (b.W32[l] - runs["sep"][1][l]).abs().max().item()
+        assert (a.W32[l] - b.W32[l]).abs().max().item() <= 1e-4 * dw + 1e-7, l
+        assert torch.equal(a.Wb[l], a.W32[l].bfloat16()) and torch.equal(a.Wt[l], a.W32[l].bfloat16().t())
