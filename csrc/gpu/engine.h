@@ -50,7 +50,7 @@ typedef struct {
     UINT n_gpu;       /* data-parallel replicas driven by this process */
     BOOL resume;      /* BPM: start from the momentum in k->dw (exact resume)  */
     UINT epoch0;      /* epochs completed before this call (metrics numbering) */
-    UINT tp;          /* 1: row-sharded tensor parallelism ([parallel] tp; f64 / f32) */
+    UINT tp;          /* 1: row-sharded tensor parallelism ([parallel] tp; f64 / f32 / bf16) */
 } hpnn_batched_opts;
 
 typedef struct {

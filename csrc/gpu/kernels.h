@@ -173,6 +173,11 @@ int hpnn_sgd_update_rows_bf16g(float *W32, float *V32, const void *G16, long n, 
                                int momentum, void *Wbf, hipStream_t stream);
 int hpnn_transpose_bf16(const void *Wbf, void *Wt, int N, int K, hipStream_t stream);
 
+/* BF16 row-sharded tensor parallelism (tp_engine.cpp): dst [rows][P n] <- src [P][rows][n]
+ * (n % 8 == 0); out = bf16(in * f'(H)) elementwise (n % 4 == 0) */
+int hpnn_block_permute_bf16(const void *src, void *dst, int P, long rows, int n, hipStream_t stream);
+int hpnn_dact_f32_bf16(void *out, const float *in, const void *H, long n, hipStream_t stream);
+
 /* zero-fill helper usable inside graphs */
 int hpnn_fill_f32(float *p, long n, float v, hipStream_t stream);
 

@@ -799,6 +799,40 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16 *__res
     for (int j = 0; j < 4; j++) Wt[(size_t)(tkk * 32 + y + 8 * j) * N + tn * 32 + x] = t[x][y + 8 * j];
 }
 
+/* ---- pieces of the BF16 row-sharded tensor-parallel step (tp_engine.cpp TpNetBf16) ---- */
+/* dst [rows][P n] <- src [P][rows][n]: the all-gathered per-rank feature blocks of a layer's
+ * activations into the batch-major input of the next GEMM (8 bf16 per thread) */
+__global__ __launch_bounds__(256) void block_permute_bf16_kernel(const __bf16 *__restrict__ src,
+                                                                 __bf16 *__restrict__ dst, int P, long rows, int n) {
+    typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+    const int n8 = n / 8;
+    const long total = (long)P * rows * n8;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int c8 = (int)(i % n8);
+        const long pr = i / n8;
+        const long r = pr % rows;
+        const int p = (int)(pr / rows);
+        ((bf16x8_t *)(dst + r * (long)P * n + (long)p * n))[c8] = ((const bf16x8_t *)(src + pr * n))[c8];
+    }
+}
+
+/* out = bf16(in * f'(H)), f'(y) = -0.5 (y^2 - 1): the f' epilogue on reduce-scattered FP32
+ * partial deltas (4 per thread) */
+__global__ __launch_bounds__(256) void dact_f32_bf16_kernel(__bf16 *__restrict__ out, const float *__restrict__ in,
+                                                            const __bf16 *__restrict__ H, long n4) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const f32x4 v = ((const f32x4 *)in)[i];
+        const bf16x4_t h = ((const bf16x4_t *)H)[i];
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float y = (float)h[r];
+            o[r] = (__bf16)(v[r] * (-0.5f * (y * y - 1.0f)));
+        }
+        ((bf16x4_t *)out)[i] = o;
+    }
+}
+
 __global__ void pack_bf16_kernel(const void *__restrict__ src, int src_f64, int rows, int cols, int lds,
                                  __bf16 *__restrict__ dst, int prow, int pcol, int ldd) {
     const long total = (long)prow * pcol;
@@ -940,6 +974,20 @@ extern "C" int hpnn_sgd_update_rows_bf16g(float *W32, float *V32, const void *G1
         return -2;
     hipLaunchKernelGGL(sgd_rows_bf16g_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, stream, W32, V32,
                        (const __bf16 *)G16, n / 4, lr, alpha, scale, momentum, (__bf16 *)Wbf);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_block_permute_bf16(const void *src, void *dst, int P, long rows, int n, hipStream_t stream) {
+    if (P < 1 || rows < 1 || n < 8 || n % 8 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return -2;
+    hipLaunchKernelGGL(block_permute_bf16_kernel, dim3(grid_for((long)P * rows * (n / 8), 256)), dim3(256), 0, stream,
+                       (const __bf16 *)src, (__bf16 *)dst, P, rows, n);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_dact_f32_bf16(void *out, const float *in, const void *H, long n, hipStream_t stream) {
+    if (n <= 0 || n % 4 || ((uintptr_t)in & 15) || (((uintptr_t)out | (uintptr_t)H) & 7)) return -2;
+    hipLaunchKernelGGL(dact_f32_bf16_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, stream, (__bf16 *)out, in,
+                       (const __bf16 *)H, n / 4);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

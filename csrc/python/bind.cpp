@@ -256,6 +256,12 @@ PYBIND11_MODULE(_native, m) {
     m.def("cast_weights", [](uptr W32, uptr Wbf, uptr Wt, int N, int K, uptr stream) {
         check(hpnn_cast_weights((const float *)P(W32), P(Wbf), P(Wt), N, K, S(stream)), "cast_weights");
     });
+    m.def("block_permute_bf16", [](uptr src, uptr dst, int Pn, long rows, int n, uptr stream) {
+        check(hpnn_block_permute_bf16(P(src), P(dst), Pn, rows, n, S(stream)), "block_permute_bf16");
+    });
+    m.def("dact_f32_bf16", [](uptr out, uptr in, uptr H, long n, uptr stream) {
+        check(hpnn_dact_f32_bf16(P(out), (const float *)P(in), P(H), n, S(stream)), "dact_f32_bf16");
+    });
     m.def("pack_bf16", [](uptr src, int src_f64, int rows, int cols, int lds, uptr dst, int prow, int pcol, int ldd,
                           uptr stream) {
         check(hpnn_pack_bf16(P(src), src_f64, rows, cols, lds, P(dst), prow, pcol, ldd, S(stream)), "pack_bf16");

@@ -409,6 +409,28 @@ def cast_weights(W32, Wbf, Wt, Wf=None):
     native().cast_weights(W32.data_ptr(), Wbf.data_ptr(), Wt.data_ptr(), N, K, _stream())
 
 
+def block_permute(src, dst):
+    """dst [rows, P*n] <- src [P, rows, n] (BF16): rank-major all-gather output -> feature-
+    concatenated activations (the tensor-parallel forward)."""
+    Pn, rows, n = src.shape
+    assert dst.shape == (rows, Pn * n) and src.is_contiguous() and dst.is_contiguous()
+    if _cpu(src):
+        dst.copy_(src.permute(1, 0, 2).reshape(rows, Pn * n))
+        return dst
+    native().block_permute_bf16(src.data_ptr(), dst.data_ptr(), Pn, rows, n, _stream())
+    return dst
+
+
+def dact_cast(out, x, H):
+    """out (BF16) = bf16(x * f'(H)), x FP32 (the reduced partial deltas), H BF16 activations."""
+    assert out.shape == x.shape == H.shape and out.is_contiguous() and x.is_contiguous() and H.is_contiguous()
+    if _cpu(x):
+        out.copy_((x * dbipolar(H.float())).bfloat16())
+        return out
+    native().dact_f32_bf16(out.data_ptr(), x.data_ptr(), H.data_ptr(), x.numel(), _stream())
+    return out
+
+
 def pack_bf16(src, dst):
     """dst (bf16, padded) <- src (float32/float64 [rows, cols]); padding zero-filled."""
     rows, cols = src.shape

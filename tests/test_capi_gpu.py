@@ -221,14 +221,33 @@ def test_batched_tensor_parallel_matches_single(tmp_path, dtype, ranks, dims):
         assert rel < (1e-12 if dtype == "f64" else 1e-5), rel
 
 
-def test_tensor_parallel_refuses_bf16(tmp_path):
-    d = str(tmp_path)
-    _data(os.path.join(d, "samples"), 20, 10, 3, True)
-    formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=10, hiddens=[8],
-                       outputs=3, train="BP", sample_dir="./samples", test_dir="./samples", mode="batched",
-                       batch=16, dtype="bf16", parallel="tp")
-    env = dict(os.environ)
-    env.pop("HPNN_FORCE_CPU", None)
-    r = subprocess.run([os.path.join(BIN, "train_nn"), "nn.conf"], cwd=d, env=env, capture_output=True, text=True,
-                       timeout=300)
-    assert "[parallel] tp needs [dtype] f64 or f32" in r.stdout + r.stderr
+@pytest.mark.parametrize("ranks,dims,batch", [(2, (100, [48, 37], 7), 128), (3, (64, [50], 9), 100),
+                                               (4, (784, [128, 64], 10), 256)])
+def test_batched_tensor_parallel_bf16(tmp_path, ranks, dims, batch):
+    """[parallel] tp with [dtype] bf16 (tp_engine.cpp TpNetBf16): the row sharding on the BF16
+    MFMA kernels, batch-major activations all-gathered in BF16 and block-permuted, partial
+    deltas reduce-scattered in FP32 with f' fused into the BF16 cast.  P ranks == one rank of
+    the same engine up to the FP32 summation order of the deltas (BF16 rounding flips: 1e-2),
+    and both close to the data-parallel-free single-GPU batched engine (different kernels,
+    3e-2).  batch 100: the batch padded to 128 with zero samples."""
+    n_in, hid, n_out = dims
+    res = {}
+    for tag, env, par in (("single", {}, "dp"), ("tp1", {}, "tp"), ("tp", {"HPNN_LOOPBACK_RANKS": str(ranks)}, "tp")):
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 300, n_in, n_out, True, seed=6)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=n_in, hiddens=hid,
+                           outputs=n_out, train="BPM", sample_dir="./samples", test_dir="./samples",
+                           mode="batched", batch=batch, epochs=2, lr=0.05, dtype="bf16", parallel=par)
+        out = _run([os.path.join(BIN, "train_nn"), "-vv", "nn.conf"], d, extra_env=env)
+        assert ("tensor-parallel batched training" in out) == (tag != "single"), out[-2000:]
+        if tag != "single":
+            assert "bf16" in out
+        res[tag] = (formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"],
+                    formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"])
+    for (w0, ws, w1, wt) in zip(res["single"][0], res["single"][1], res["tp1"][1], res["tp"][1]):
+        ds, d1, dt = ws - w0, w1 - w0, wt - w0
+        assert np.linalg.norm(d1) > 0
+        rel = np.linalg.norm(d1 - dt) / np.linalg.norm(d1)
+        assert rel < 1e-2, rel
+        rel = np.linalg.norm(ds - dt) / (np.linalg.norm(ds) + 1e-30)
+        assert rel < 3e-2, rel

@@ -1,6 +1,8 @@
 """Row-sharded tensor parallelism on the GPU kernels with two processes sharing the box's
-one MI355X (gloo carries the activation all-gathers and partial-delta all-reduces through
-host memory; RCCL refuses two ranks on one device): == single-process GPU training."""
+one MI355X (gloo carries the activation all-gathers and partial-delta reduce-scatters
+through host memory; RCCL refuses two ranks on one device): every step on the native
+kernels (gemm_nt / block_permute / dact_cast / gemm_tn / sgd_update_multi) == single-process
+GPU training."""
 import os
 import socket
 
@@ -18,32 +20,6 @@ def _inputs():
     return torch.rand(B, SIZES[0], generator=g), torch.randint(0, SIZES[-1], (B,), generator=g, dtype=torch.int32)
 
 
-class _GlooOnCuda:
-    """route the two collectives tp.py uses through host tensors (gloo)"""
-
-    def __init__(self):
-        self.ag, self.ar = dist.all_gather_into_tensor, dist.all_reduce
-
-    def __enter__(self):
-        ag, ar = self.ag, self.ar
-
-        def all_gather_into_tensor(out, inp, group=None):
-            o = out.cpu()
-            ag(o, inp.cpu(), group=group)
-            out.copy_(o)
-
-        def all_reduce(t, op=dist.ReduceOp.SUM, group=None):
-            c = t.cpu()
-            ar(c, op=op, group=group)
-            t.copy_(c)
-
-        dist.all_gather_into_tensor, dist.all_reduce = all_gather_into_tensor, all_reduce
-        return self
-
-    def __exit__(self, *a):
-        dist.all_gather_into_tensor, dist.all_reduce = self.ag, self.ar
-
-
 def _worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
@@ -51,13 +27,12 @@ def _worker(rank, world, port, q):
         from hpnn_amd.parallel import TensorParallelMLP
         dev = torch.device("cuda", 0)
         X, L = _inputs()
-        with _GlooOnCuda():
-            tp = TensorParallelMLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=21)
-            Xp = torch.zeros(tp.Bp, tp.Kp[0], dtype=torch.bfloat16, device=dev)
-            Xp[:B, :SIZES[0]] = X.to(dev).bfloat16()
-            for _ in range(3):
-                tp.train_step(Xp, labels=L.to(dev), lr=0.05, alpha=0.2)
-            w = tp.full_weights()
+        tp = TensorParallelMLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=21)
+        Xp = torch.zeros(tp.Bp, tp.Kp[0], dtype=torch.bfloat16, device=dev)
+        Xp[:B, :SIZES[0]] = X.to(dev).bfloat16()
+        for _ in range(3):
+            tp.train_step(Xp, labels=L.to(dev), lr=0.05, alpha=0.2)
+        w = tp.full_weights()
         q.put((rank, w))
         dist.barrier()
         dist.destroy_process_group()
