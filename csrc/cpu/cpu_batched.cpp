@@ -27,7 +27,7 @@ static inline DOUBLE act(DOUBLE x) { return 2.0 / (1.0 + exp(-1.0 * x)) - 1.0; }
 static inline DOUBLE dact(DOUBLE y) { return -0.5 * (y * y - 1.0); }
 
 extern "C" DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBLE *X, const DOUBLE *T,
-                                        UINT B, DOUBLE lr, BOOL momentum, DOUBLE alpha) {
+                                        UINT B, DOUBLE lr, BOOL momentum, DOUBLE alpha, UINT *hits) {
     const UINT L = k->n_hiddens + 1;
     std::vector<const layer_ann *> layers(L);
     for (UINT l = 0; l + 1 < L; l++) layers[l] = &k->hiddens[l];
@@ -40,6 +40,7 @@ extern "C" DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBL
     }
     const UINT n_out = k->n_outputs;
     std::vector<DOUBLE> loss(B, 0.0);
+    std::vector<unsigned char> hit(B, 0);
     const int nt = _NN(return, omp_threads)();
 #pragma omp parallel for num_threads(nt) schedule(static)
     for (long b = 0; b < (long)B; b++) {
@@ -78,6 +79,12 @@ extern "C" DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBL
             Ep *= 0.5;
         }
         loss[b] = Ep;
+        UINT g = 0, tr = 0; /* argmax hit (first maximum, as the GPU kernels) */
+        for (UINT i = 1; i < n_out; i++) {
+            if (o[i] > o[g]) g = i;
+            if (t[i] > t[tr]) tr = i;
+        }
+        hit[b] = g == tr;
         for (UINT i = 0; i < n_out; i++) d[i] = (type == NN_TYPE_ANN) ? (t[i] - o[i]) * dact(o[i]) : (t[i] - o[i]);
         /* hidden deltas */
         for (long l = (long)L - 2; l >= 0; l--) {
@@ -121,7 +128,12 @@ extern "C" DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBL
         }
     }
     DOUBLE s = 0.0;
-    for (UINT b = 0; b < B; b++) s += loss[b];
+    UINT c = 0;
+    for (UINT b = 0; b < B; b++) {
+        s += loss[b];
+        c += hit[b];
+    }
+    if (hits) *hits += c;
     return s * inv_b;
 }
 
@@ -140,18 +152,18 @@ extern "C" BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
     DOUBLE last = 0.0;
     for (UINT e = 0; e < o->epochs; e++) {
         DOUBLE acc = 0.0;
-        UINT nb = 0;
+        UINT nb = 0, hits = 0;
         for (UINT s = 0; s < n; s += B) {
             UINT b = (n - s < B) ? n - s : B;
             last = hpnn_cpu_batched_step(k, o->type, X + (size_t)s * k->n_inputs, T + (size_t)s * k->n_outputs, b,
-                                         o->lr, mom, o->alpha);
+                                         o->lr, mom, o->alpha, &hits);
             acc += last;
             nb++;
             samples += b;
         }
         if (st) st->epoch_loss = acc / (nb ? nb : 1);
         if (hpnn_metrics_active())
-            hpnn_metrics_epoch("cpu", o->epoch0 + e + 1, acc / (nb ? nb : 1), 0, n,
+            hpnn_metrics_epoch("cpu", o->epoch0 + e + 1, acc / (nb ? nb : 1), hits, n,
                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), samples);
     }
     auto t1 = std::chrono::steady_clock::now();

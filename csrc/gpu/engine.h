@@ -79,7 +79,7 @@ BOOL hpnn_cpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UIN
                             const hpnn_batched_opts *o, hpnn_batched_stats *st);
 /* one minibatch step on the CPU: returns mean loss before the update */
 DOUBLE hpnn_cpu_batched_step(kernel_ann *k, nn_type type, const DOUBLE *X, const DOUBLE *T, UINT b,
-                             DOUBLE lr, BOOL momentum, DOUBLE alpha);
+                             DOUBLE lr, BOOL momentum, DOUBLE alpha, UINT *hits /* may be NULL: += argmax hits */);
 
 #ifdef __cplusplus
 }

@@ -1662,19 +1662,63 @@ BOOL infer_fp(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, h
 }  // namespace
 
 /* batched evaluation (run_nn on the GPU): the whole test set through the batched engine
- * of the requested precision instead of one online forward per file */
+ * of the requested precision instead of one online forward per file.  With n_gpu > 1
+ * (run_nn -G N) the samples are split into N contiguous shards, one host thread and one
+ * device each (forward only: no communication; outputs land in place).  HPNN_INFER_SHARDS
+ * = V runs V shards as threads on device 0, each on its own stream (tests on one GPU). */
 extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
                                        DOUBLE *Y) {
     if (!k || n == 0) return FALSE;
-    hpnn_gpu_sync_host(k);
-    HIPCHK(hipSetDevice(hpnn_rt_device(0)));
-    hipStream_t s = hpnn_rt_stream(0, 0);
-    switch (dtype) {
-    case NN_DTYPE_BF16: return infer_bf16(k, type, X, n, Y, s);
-    case NN_DTYPE_F32: return infer_fp<float>(k, type, X, n, Y, s);
-    case NN_DTYPE_F64: return infer_fp<double>(k, type, X, n, Y, s);
-    default:
+    if (dtype != NN_DTYPE_BF16 && dtype != NN_DTYPE_F32 && dtype != NN_DTYPE_F64) {
         NN_ERROR(stderr, "GPU inference: unsupported dtype %d\n", (int)dtype);
         return FALSE;
     }
+    hpnn_gpu_sync_host(k);
+    const nn_runtime *rt = hpnn_rt_get();
+    const int G = rt && rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
+    const char *vs = getenv("HPNN_INFER_SHARDS");
+    const int V = vs ? atoi(vs) : 0;
+    const bool virt = V >= 2;
+    int P = virt ? V : G;
+    if ((UINT)P > n) P = (int)n;
+    const UINT ni = k->n_inputs, no = k->n_outputs;
+    auto shard = [&](int g, hipStream_t s) -> BOOL {
+        const UINT lo = (UINT)((UINT64)n * g / P), hi = (UINT)((UINT64)n * (g + 1) / P);
+        if (hi == lo) return TRUE;
+        const DOUBLE *Xs = X + (size_t)lo * ni;
+        DOUBLE *Ys = Y + (size_t)lo * no;
+        switch (dtype) {
+        case NN_DTYPE_BF16: return infer_bf16(k, type, Xs, hi - lo, Ys, s);
+        case NN_DTYPE_F32: return infer_fp<float>(k, type, Xs, hi - lo, Ys, s);
+        default: return infer_fp<double>(k, type, Xs, hi - lo, Ys, s);
+        }
+    };
+    if (P <= 1) {
+        HIPCHK(hipSetDevice(hpnn_rt_device(0)));
+        return shard(0, hpnn_rt_stream(0, 0));
+    }
+    NN_DBG(stdout, "batched evaluation: %u samples over %d %s\n", n, P, virt ? "shards on one GPU" : "GPUs");
+    std::vector<int> ok(P, 0);
+    std::vector<std::thread> th;
+    for (int g = 0; g < P; g++)
+        th.emplace_back([&, g]() {
+            const int dev = hpnn_rt_device(virt ? 0 : (UINT)g);
+            if (hipSetDevice(dev) != hipSuccess) return;
+            hipStream_t s = nullptr;
+            if (virt) {
+                if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+            } else {
+                s = hpnn_rt_stream((UINT)g, 0);
+            }
+            ok[g] = shard(g, s) ? 1 : 0;
+            if (virt) hipStreamDestroy(s);
+        });
+    for (auto &t : th) t.join();
+    hipSetDevice(hpnn_rt_device(0));
+    for (int g = 0; g < P; g++)
+        if (!ok[g]) {
+            NN_ERROR(stderr, "batched GPU evaluation: shard %d failed\n", g);
+            return FALSE;
+        }
+    return TRUE;
 }

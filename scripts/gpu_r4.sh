@@ -1,7 +1,8 @@
 #!/bin/bash
 # round-4 GPU call: steps by name, each under its own time limit; a crash / fault / timeout
 # (rc not 0 or 1) ends the call.   usage: scripts/gpu_r4.sh <tag> <step> [<step> ...]
-#   steps: tests | tests:<pytest -k expr> | smoke | bench | rruff | libbench | prof | prof_rruff
+#   steps: tests | tests:<pytest -k expr> | smoke | bench | rruff | synth | synthrs | libbench | fpbench |
+#          learn | prof | prof_rruff
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag=$1; shift
 O=gpurun_out/$tag; mkdir -p $O
@@ -28,6 +29,8 @@ for s in "$@"; do
     fpbench) step fpbench 300 python scripts/gemm_fp_bench.py --out $O/gemm_fp.jsonl ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
+    learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
+    synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
