@@ -356,11 +356,12 @@ int BPlan::g0_reduce(const XIn &x, hipStream_t s) {
 
 /* G0 + its split-K reduction + every layer's step in ONE launch (kernels_g0.hip); -1 when
  * the shape or the input is not covered (the caller then runs G0 + the update launch) */
-int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s) {
+int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout) {
     const void *fm = fm_input(x);
     if (!fm || !g0cnt || !g0_fused) return -1;
     hpnn_g0_update u;
     memset(&u, 0, sizeof u);
+    u.gout = gout;
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
     u.cnt = g0cnt, u.err = g0cnt + 224;
     u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;
@@ -495,11 +496,30 @@ int BPlan::grads(const XIn &x, const int *labels, const float *T, int ldt, int n
     }
 }
 
+int BPlan::grads_local(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, hipStream_t s) {
+    if (mode != 't' && mode != 'x' && mode != 'm') return -1;
+    int r;
+    if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
+    if ((r = g0_fused_step(x, 0.f, 0.f, 0.f, s, gflat)) != -1) return r;
+    /* not covered: slabs, then the reductions into the buffer */
+    if ((r = g0_reduce(x, s))) return r;
+    if ((r = hpnn_reduce_slabs(slab[0], S[0], (long)Np[0] * Kp[0], (long)Np[0] * Kp[0], gflat, s))) return r;
+    return hpnn_reduce_slabs(midtmp, mid_groups, slab_f, slab_f, gflat + goff[1], s);
+}
+
 int BPlan::grads_slabs(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, SlabSegs *segs,
                        hipStream_t s) {
     if (mode != 't' && mode != 'x' && mode != 'm') return -1;
     int r;
     if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
+    if (g0_fused_step(x, 0.f, 0.f, 0.f, s, gflat) == 0) {
+        /* G0 and [G1 | G2] reduced in the G0 launch: the exchange moves ONE copy */
+        segs->count = 1;
+        segs->base[0] = gflat;
+        segs->cnt[0] = 1;
+        segs->n[0] = segs->stride[0] = (long)goff[L];
+        return 0;
+    }
     if ((r = g0_reduce(x, s))) return r;
     segs->count = 2;
     segs->base[0] = slab[0];

@@ -125,9 +125,14 @@ class BPlan {
               hipStream_t s);
     std::vector<std::pair<int, int>> buckets() const;
     /* fused modes: front + G0 with the gradient left in slabs (the xGMI all-reduce's copy-in
-     * sums them); segs[0] = G0 slabs, segs[1] = [G1|G2] groups */
+     * sums them); segs[0] = G0 slabs, segs[1] = [G1|G2] groups -- or, when the G0 launch
+     * reduces in-kernel, ONE segment: gflat itself, fully reduced */
     int grads_slabs(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, SlabSegs *segs,
                     hipStream_t s);
+    /* fused modes: front + every layer's gradient summed over this replica's samples into
+     * gflat, with G0's split-K and [G1|G2] reductions inside the G0 launch when it applies
+     * (two launches; the exchange then moves one copy) */
+    int grads_local(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, hipStream_t s);
     int update_flat(const float *G, float lr, float alpha, float scale, hipStream_t s);
     /* network outputs O [Bp][ldo] FP32 of a row-major BF16 batch */
     int predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s);
@@ -151,7 +156,7 @@ class BPlan {
     bool owns_ = false;
     int grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     int g0_reduce(const XIn &x, hipStream_t s);
-    int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
+    int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout = nullptr);
     bool tn_update_ok(int l) const;
     const void *fm_input(const XIn &x) const;
     void name_pointers();

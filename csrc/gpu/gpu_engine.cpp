@@ -736,6 +736,13 @@ struct Batched {
         return r == 0;
     }
     BOOL grads(const XSet &xs, long row, const float *T, int ldt, int n_valid) {
+        /* no exchange to overlap (the xGMI all-reduce of the whole buffer follows): the fused
+         * modes reduce G0 and [G1|G2] inside the G0 launch */
+        const int r = p.grads_local(at(xs, row), nullptr, T, ldt, n_valid, s);
+        if (r != -1) {
+            if (r) NN_ERROR(stderr, "batched gradients failed: %d\n", r);
+            return r == 0;
+        }
         return grads(xs, row, T, ldt, n_valid, [](int, int) { return true; });
     }
     std::vector<std::pair<int, int>> buckets() const { return p.buckets(); }

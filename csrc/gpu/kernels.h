@@ -109,6 +109,9 @@ typedef struct {
     float *W32b[2], *V32b[2]; /* layers 1, 2 */
     void *Wbb[2], *Wtb[2];
     int Nb[2], Kb[2];
+    /* non-NULL: no step -- the fully reduced gradients are stored instead, G0 [N][M] at gout,
+     * [G1 | G2] right after it (the flat layout of the plan's gradient buffer; data parallel) */
+    float *gout;
 } hpnn_g0_update;
 int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
                                int M, int Bt, int splits, const hpnn_g0_update *u, hipStream_t stream);

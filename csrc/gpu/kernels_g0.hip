@@ -239,7 +239,7 @@ __device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, _
  * a fixed order (RG row groups of NT / 16 threads, met in LDS in order), then layers 1 / 2
  * stepped at those elements */
 template <int NT>
-__device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long c1, f32x4 *red) {
+__device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long c1, f32x4 *red, float *g12out) {
     constexpr int C4 = 16, RG = NT / C4;
     const int t = threadIdx.x, c = t % C4, rg = t / C4;
     for (long b0 = c0; b0 < c1; b0 += C4) {
@@ -253,11 +253,15 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
             f32x4 g = red[c];
             for (int r = 1; r < RG; r++) g += red[r * C4 + c];
             long i = e4 * 4;
-            const int l = i < (long)u.Nb[0] * u.Kb[0] ? 0 : 1;
-            if (l) i -= (long)u.Nb[0] * u.Kb[0];
-            const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
-            step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k,
-                       g, u);
+            if (g12out) {
+                *(f32x4 *)(g12out + i) = g;
+            } else {
+                const int l = i < (long)u.Nb[0] * u.Kb[0] ? 0 : 1;
+                if (l) i -= (long)u.Nb[0] * u.Kb[0];
+                const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+                step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n,
+                           k, g, u);
+            }
         }
         __syncthreads();
     }
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
     {
         const long nb = (long)tiles * splits, nf = u.n12 / 4, b = blockIdx.x;
-        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red);
+        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red, u.gout ? u.gout + (size_t)N * ldg : nullptr);
     }
     if (t == 0) {
         unsigned int *cnt = u.cnt + 32 * tile;
@@ -340,7 +344,10 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
             f32x4 g = red[f];
 #pragma unroll
             for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
-            step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
+            if (u.gout)
+                *(f32x4 *)(u.gout + (size_t)(nt0 + row) * ldg + col) = g;
+            else
+                step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
         }
         __syncthreads();
     }
@@ -392,7 +399,8 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     /* the 160 x 128 tile configuration of fm_dispatch (8 waves) */
     if (!on || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
     if (!u->cnt || !u->err) return -1;
-    if (u->n12 % 4 || !u->mslab || u->mrows < 1 || (u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
+    if (u->n12 % 4 || !u->mslab || u->mrows < 1 ||
+        (!u->gout && u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
         return -2;
     const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
     if (tiles > 7) return -1; /* counters 32 words apart in a 256-word block, err at word 224 */

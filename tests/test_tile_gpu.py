@@ -138,3 +138,35 @@ def test_fused_g0_update_matches_separate_update(gpu, Bp):
         assert (a.V32[l] - b.V32[l]).abs().max().item() <= 1e-4 * dv + 1e-8, l
     from hpnn_amd import ops
     assert torch.equal(a.W0f, ops.frag_major(a.W32[0].bfloat16()))
+
+
+@pytest.mark.gpu
+def test_fused_g0_gradient_out_matches_slab_sums(gpu):
+    """data-parallel form of the fused G0 launch (hpnn_g0_update.gout): no step, the reduced
+    G0 and [G1|G2] land in the plan's flat gradient buffer -> grads_slabs returns ONE segment
+    (the xGMI exchange then moves one copy instead of summing 48 + groups slabs) equal to the
+    sums of the unfused slab segments; bitwise repeatable"""
+    Bp = 24576
+    out = {}
+    for tag, fused in (("fused", True), ("fused2", True), ("sep", False)):
+        m, X = _case("SNN", 10, Bp, True, seed=5)
+        m.plan.g0_fused = fused
+        Xg = m.prepare_input(X.cuda())
+        lab = torch.randint(0, 10, (Bp,), dtype=torch.int32, device="cuda",
+                            generator=torch.Generator(device="cuda").manual_seed(9))
+        segs = m.grads_slabs(Xg, labels=lab)
+        torch.cuda.synchronize()
+        if fused:
+            assert len(segs) == 1 and segs[0][0] == m.grad_flat.data_ptr() and segs[0][2] == 1, segs
+            out[tag] = m.grad_flat.clone()
+        else:
+            assert len(segs) == 2
+            parts = []
+            for addr, stride, cnt, n in segs:
+                base = [t for t in (m.slab[0], m.midtmp) if t.data_ptr() == addr][0].view(-1)
+                parts.append(torch.stack([base[s * stride:s * stride + n] for s in range(cnt)]).sum(0))
+            out[tag] = torch.cat(parts)[:m.grad_flat.numel()]
+        assert m.plan.health(torch.cuda.current_stream().cuda_stream) == 0
+    assert torch.equal(out["fused"], out["fused2"])
+    ref = out["sep"]
+    assert ((out["fused"] - ref).abs().max() <= 1e-5 * ref.abs().max()).item()
