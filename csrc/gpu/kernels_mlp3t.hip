@@ -157,6 +157,12 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         const int row = 16 * xcbh + 2 * (xi & 7) + e;
         xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
     }
+    /* write order: lanes k = xi & 7 with bit 1 set write their odd row first.  Lane k's rows
+     * 2k + e sit at bank group 4 e + g(k) (g = t32_g(2k): 0 1 0 1 2 3 2 3), so in-order
+     * writes put each 8-lane ds_write_b128 group on 4 bank groups (2-way conflict); the
+     * swapped order spreads it over all 8 */
+    const int xp = (xi >> 1) & 1;
+    const int xa0 = xoff[xp], xa1 = xoff[xp ^ 1];
     const char *xbase = (const char *)Xg + ((size_t)wave * NCB + xcbh) * CHUNK + (size_t)xi * XB;
 
     /* transposed-read addresses of this wave's STA sample tiles in an X^T stage: sample tile
@@ -206,8 +212,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 v[0] = __builtin_bit_cast(bf16x8, xr[s][0]);
                 v[1] = __builtin_bit_cast(bf16x8, xr[s][1]);
             }
-            *(bf16x8 *)(img + xoff[0]) = v[0];
-            *(bf16x8 *)(img + xoff[1]) = v[1];
+            *(bf16x8 *)(img + xa0) = xp ? v[1] : v[0];
+            *(bf16x8 *)(img + xa1) = xp ? v[0] : v[1];
         };
 
         f32x4 acc[2][STA];
