@@ -1669,10 +1669,12 @@ BOOL infer_fp(kernel_ann *k, nn_type type, const DOUBLE *X, UINT n, DOUBLE *Y, h
 }  // namespace
 
 /* batched evaluation (run_nn on the GPU): the whole test set through the batched engine
- * of the requested precision instead of one online forward per file.  With n_gpu > 1
- * (run_nn -G N) the samples are split into N contiguous shards, one host thread and one
- * device each (forward only: no communication; outputs land in place).  HPNN_INFER_SHARDS
- * = V runs V shards as threads on device 0, each on its own stream (tests on one GPU). */
+ * of the requested precision instead of one online forward per file.  With n_gpu x
+ * n_streams > 1 (run_nn -G N -S M, the reference's forward over n_gpu x n_streams,
+ * cuda_ann.cu:426-1276) the samples are split into N M contiguous shards, one host thread
+ * each on its own (device, stream) (forward only: no communication; outputs land in
+ * place).  HPNN_INFER_SHARDS = V runs V shards on device 0, each on its own new stream
+ * (tests on one GPU). */
 extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dtype, const DOUBLE *X, UINT n,
                                        DOUBLE *Y) {
     if (!k || n == 0) return FALSE;
@@ -1683,10 +1685,11 @@ extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dty
     hpnn_gpu_sync_host(k);
     const nn_runtime *rt = hpnn_rt_get();
     const int G = rt && rt->cudas.n_gpu > 1 ? (int)rt->cudas.n_gpu : 1;
+    const int NS = rt && rt->cudas.cuda_n_streams > 1 ? (int)rt->cudas.cuda_n_streams : 1;
     const char *vs = getenv("HPNN_INFER_SHARDS");
     const int V = vs ? atoi(vs) : 0;
     const bool virt = V >= 2;
-    int P = virt ? V : G;
+    int P = virt ? V : G * NS;
     if ((UINT)P > n) P = (int)n;
     const UINT ni = k->n_inputs, no = k->n_outputs;
     auto shard = [&](int g, hipStream_t s) -> BOOL {
@@ -1704,18 +1707,20 @@ extern "C" BOOL hpnn_gpu_infer_batched(kernel_ann *k, nn_type type, nn_dtype dty
         HIPCHK(hipSetDevice(hpnn_rt_device(0)));
         return shard(0, hpnn_rt_stream(0, 0));
     }
-    NN_DBG(stdout, "batched evaluation: %u samples over %d %s\n", n, P, virt ? "shards on one GPU" : "GPUs");
+    NN_DBG(stdout, "batched evaluation: %u samples over %d %s\n", n, P,
+           virt ? "shards on one GPU" : "(GPU, stream) shards");
     std::vector<int> ok(P, 0);
     std::vector<std::thread> th;
     for (int g = 0; g < P; g++)
         th.emplace_back([&, g]() {
-            const int dev = hpnn_rt_device(virt ? 0 : (UINT)g);
+            /* shard g: device g / NS, stream g % NS (consecutive shards on one device) */
+            const int dev = hpnn_rt_device(virt ? 0 : (UINT)(g / NS));
             if (hipSetDevice(dev) != hipSuccess) return;
             hipStream_t s = nullptr;
             if (virt) {
                 if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
             } else {
-                s = hpnn_rt_stream((UINT)g, 0);
+                s = hpnn_rt_stream((UINT)(g / NS), (UINT)(g % NS));
             }
             ok[g] = shard(g, s) ? 1 : 0;
             if (virt) hipStreamDestroy(s);

@@ -256,8 +256,8 @@ def test_batched_tensor_parallel_bf16(tmp_path, ranks, dims, batch):
 @pytest.mark.parametrize("dtype", ["bf16", "f64"])
 def test_run_nn_sharded_evaluation_matches(tmp_path, dtype):
     """run_nn's batched GPU evaluation split into contiguous sample shards, one host thread
-    and device each (run_nn -G N; here HPNN_INFER_SHARDS=3 shards on the box's one GPU, each
-    on its own stream) == the unsplit evaluation, line for line."""
+    each on its own (device, stream) (run_nn -G N -S M; here -S 2 on the box's one GPU, and
+    HPNN_INFER_SHARDS=3 shards on new streams) == the unsplit evaluation, line for line."""
     d = str(tmp_path)
     _data(os.path.join(d, "samples"), 301, 60, 5, True, seed=3)
     formats.write_conf(os.path.join(d, "nn.conf"), name="t", type="SNN", seed=5, inputs=60, hiddens=[48, 32],
@@ -265,8 +265,10 @@ def test_run_nn_sharded_evaluation_matches(tmp_path, dtype):
     one = _run([os.path.join(BIN, "run_nn"), "-vvv", "nn.conf"], d)
     three = _run([os.path.join(BIN, "run_nn"), "-vvv", "nn.conf"], d, extra_env={"HPNN_INFER_SHARDS": "3"})
     assert "over 3 shards" in three
+    streams = _run([os.path.join(BIN, "run_nn"), "-vvv", "-S", "2", "nn.conf"], d)  # -S: (GPU, stream) shards
+    assert "over 2 (GPU, stream) shards" in streams
     import re
     # the per-class probabilities (10 digits) and the verdict of every file
     lines = lambda out: [x for x in out.splitlines() if "BEST CLASS" in x or re.match(r"^\s*\d+ \|", x)]  # noqa
     assert sum("BEST CLASS" in x for x in lines(one)) == 301
-    assert lines(one) == lines(three)
+    assert lines(one) == lines(three) == lines(streams)
