@@ -29,6 +29,7 @@ for s in "$@"; do
     fpbench) step fpbench 300 python scripts/gemm_fp_bench.py --out $O/gemm_fp.jsonl ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
+    fpsteps) step fpsteps 600 python scripts/lib_vs_bench.py --dtype f64 --configs mnist,rruff,wide --batches 2 --epochs 3 --out $O/fp64_steps.jsonl ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -23,10 +23,12 @@ sys.path.insert(0, ROOT)
 from hpnn_amd import capi  # noqa: E402
 from hpnn_amd.utils import formats  # noqa: E402
 
-CONFIGS = {"mnist": ((784, [128, 64], 10), 65536, True), "rruff": ((4096, [230], 230), 16384, False)}
+CONFIGS = {"mnist": ((784, [128, 64], 10), 65536, True), "rruff": ((4096, [230], 230), 16384, False),
+           # FP64 / FP32 only (no bench.py counterpart): 4096-wide hidden layers
+           "wide": ((4096, [4096, 4096], 10), 4096, False)}
 
 
-def run_train_nn(name, batches, epochs, work):
+def run_train_nn(name, batches, epochs, work, dtype="bf16"):
     (n_in, hid, n_out), B, pixels = CONFIGS[name]
     n = B * batches
     rng = np.random.default_rng(3)
@@ -40,7 +42,7 @@ def run_train_nn(name, batches, epochs, work):
     del X, T
     formats.write_conf(os.path.join(d, "nn.conf"), name=name, type="SNN", seed=10958, inputs=n_in, hiddens=hid,
                        outputs=n_out, train="BPM", sample_dir="./train.hpnb", test_dir="./train.hpnb",
-                       mode="batched", batch=B, epochs=epochs, dtype="bf16", lr=0.01)
+                       mode="batched", batch=B, epochs=epochs, dtype=dtype, lr=0.01)
     env = dict(os.environ)
     env.pop("HPNN_FORCE_CPU", None)
     r = subprocess.run([os.path.join(ROOT, "bin", "train_nn"), "-vvv", "nn.conf"], cwd=d, env=env,
@@ -69,14 +71,21 @@ def main():
     ap.add_argument("--configs", default="mnist,rruff")
     ap.add_argument("--batches", type=int, default=4)
     ap.add_argument("--epochs", type=int, default=50)
+    ap.add_argument("--dtype", default="bf16", help="bf16 (compared with bench.py) | f32 | f64 (train_nn only)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as work:
         for name in a.configs.split(","):
-            lib = run_train_nn(name, a.batches, a.epochs, work)
-            b = run_bench(name, 200)
-            rec = {"config": name, "batch": CONFIGS[name][1], "train_nn": lib, "bench": b,
-                   "ratio": round(lib["us_per_step"] / b["us_per_step"], 4)}
+            lib = run_train_nn(name, a.batches, a.epochs, work, a.dtype)
+            rec = {"config": name, "dtype": a.dtype, "batch": CONFIGS[name][1], "train_nn": lib}
+            if a.dtype == "bf16":
+                b = run_bench(name, 200)
+                rec.update(bench=b, ratio=round(lib["us_per_step"] / b["us_per_step"], 4))
+            else:
+                (n_in, hid, n_out), B, _ = CONFIGS[name]
+                dims = [n_in] + hid + [n_out]
+                flops = 6.0 * B * sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+                rec["step_tflops"] = round(flops / (lib["us_per_step"] * 1e-6) / 1e12, 2)
             print(json.dumps(rec), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
