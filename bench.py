@@ -85,8 +85,11 @@ def main():
     sizes, net, batch, scaling, metric, model_name = MODELS[args.model]
     if not args.batch:
         args.batch = batch // world if scaling == "strong" else batch
+    # HPNN_SPLITS="s0,s1,..." (tuning only): per-layer split-K override of the plan
+    sp = os.environ.get("HPNN_SPLITS")
     m = MLP(sizes, net, batch=args.batch, device=dev, momentum=True, seed=10958,
-            init="reference" if args.model == "mnist" else "fast")
+            init="reference" if args.model == "mnist" else "fast",
+            splits=[int(v) for v in sp.split(",")] if sp else None)
     dp = DataParallel(m, comm="xar" if rehearse and world > 1 else "auto",
                       grad_comm=args.grad_comm if m.fused_mode is None else "fp32")
     dp.broadcast_parameters()

@@ -771,9 +771,10 @@ extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H,
     const int units = Bt / 64;
     if (units % splits || (units / splits) % 2) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    /* tickets: 32 words apart in 1024; at least half the CUs busy (a few-tile gradient, e.g.
-     * RRUFF's 256 x 256 second layer, would reduce megabytes per workgroup) */
-    if (ntiles > 31 || ntiles * splits > cus || 2 * ntiles * splits < cus) return -1;
+    /* tickets: 32 words apart in 1024; at least min_wg workgroups (HPNN_TN8_MINWG, default
+     * half the CUs: fewer splits leave the chip idle while each reduces a larger share) */
+    static const int min_wg = [] { const char *e = getenv("HPNN_TN8_MINWG"); return e ? atoi(e) : 0; }();
+    if (ntiles > 31 || ntiles * splits > cus || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;
     const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, cnt, err};
     hipLaunchKernelGGL(gemm_tn8_kernel<2>, dim3(ntiles * splits), dim3(512), 0, stream, (const __bf16 *)D, ldd,
                        (const __bf16 *)H, ldh, slab, M, N, units, splits, tiles_n, ntiles, hpnn::TnTail{}, u);

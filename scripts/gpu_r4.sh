@@ -30,6 +30,11 @@ for s in "$@"; do
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
     fpsteps) step fpsteps 600 python scripts/lib_vs_bench.py --dtype f64 --configs mnist,rruff,wide --batches 2 --epochs 3 --out $O/fp64_steps.jsonl ;;
+    rruffab)  # G1 split variants on the fused 8-phase TN reduction + update
+      step rruff_s32 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=16,64 HPNN_TN8_MINWG=64 step rruff_s64 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=16,128 step rruff_s128 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=16,64 step rruff_s64u 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
