@@ -570,15 +570,42 @@ inline int pad_rows(int v, int m) { return (v + m - 1) / m * m; }
  * r * row_bytes in (fragment-major layouts keep that for r % 32 == 0) */
 struct XSet {
     void *x = nullptr, *xg = nullptr;
+    int *lab = nullptr; /* class index per row when every target row is one-hot (else null) */
     size_t row_bytes = 0, row_bytes_g = 0;
     int u8 = 0;
     float scale = 1.f;
     void release() {
         hpnn_dev_free(x);
         hpnn_dev_free(xg);
+        hpnn_dev_free(lab);
         x = xg = nullptr;
+        lab = nullptr;
     }
 };
+
+/* one-hot targets (1 at the class, t_lo = 0 for SNN / -1 otherwise, every row of the set) ->
+ * int32 class indices on the device (rows_p entries, 0 past n): the BF16 plan then takes the
+ * label form of its output layer (no dense target rows to read).  FALSE only on a device
+ * error; xs->lab stays null when the targets are not one-hot. */
+BOOL attach_labels(XSet *xs, const DOUBLE *T, UINT n, int n_out, int rows_p, nn_type type, hipStream_t s) {
+    const char *e = getenv("HPNN_LABELS");
+    if (e && e[0] == '0') return TRUE;
+    const DOUBLE t_lo = type == NN_TYPE_SNN ? 0.0 : -1.0;
+    std::vector<int> lab((size_t)rows_p, 0);
+    for (UINT i = 0; i < n; i++) {
+        int c = -1;
+        for (int j = 0; j < n_out; j++) {
+            const DOUBLE t = T[(size_t)i * n_out + j];
+            if (t == 1.0 && c < 0) c = j;
+            else if (t != t_lo) return TRUE; /* dense targets */
+        }
+        if (c < 0) return TRUE;
+        lab[i] = c;
+    }
+    if (hpnn_dev_malloc(&xs->lab, lab.size() * sizeof(int)) != hipSuccess) return FALSE;
+    return hipMemcpyAsync(xs->lab, lab.data(), lab.size() * sizeof(int), hipMemcpyHostToDevice, s) == hipSuccess &&
+           hipStreamSynchronize(s) == hipSuccess;
+}
 
 BOOL upload_bf16(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, void **dst, hipStream_t s);
 
@@ -717,7 +744,8 @@ struct Batched {
     }
 
     BOOL step(const XSet &xs, long row, const float *T, int ldt, int n_valid, float lr, float alpha, bool) {
-        const int r = p.step(at(xs, row), nullptr, T, ldt, n_valid, lr, alpha, s);
+        const int *L = xs.lab ? xs.lab + row : nullptr;
+        const int r = p.step(at(xs, row), L, L ? nullptr : T, ldt, n_valid, lr, alpha, s);
         if (r) NN_ERROR(stderr, "batched step failed: %d\n", r);
         return r == 0 && hpnn_debug_check("batched training step") == 0;
     }
@@ -731,14 +759,16 @@ struct Batched {
     size_t flat_count() const { return p.goff[L]; }
     template <class Ready>
     BOOL grads(const XSet &xs, long row, const float *T, int ldt, int n_valid, Ready &&ready) {
-        const int r = p.grads(at(xs, row), nullptr, T, ldt, n_valid, hpnn::ReadyFn(ready), s);
+        const int *L = xs.lab ? xs.lab + row : nullptr;
+        const int r = p.grads(at(xs, row), L, L ? nullptr : T, ldt, n_valid, hpnn::ReadyFn(ready), s);
         if (r) NN_ERROR(stderr, "batched gradients failed: %d\n", r);
         return r == 0;
     }
     BOOL grads(const XSet &xs, long row, const float *T, int ldt, int n_valid) {
         /* no exchange to overlap (the xGMI all-reduce of the whole buffer follows): the fused
          * modes reduce G0 and [G1|G2] inside the G0 launch */
-        const int r = p.grads_local(at(xs, row), nullptr, T, ldt, n_valid, s);
+        const int *L = xs.lab ? xs.lab + row : nullptr;
+        const int r = p.grads_local(at(xs, row), L, L ? nullptr : T, ldt, n_valid, s);
         if (r != -1) {
             if (r) NN_ERROR(stderr, "batched gradients failed: %d\n", r);
             return r == 0;
@@ -758,7 +788,8 @@ struct Batched {
         return (bool)dpx;
     }
     BOOL dp_step(const XSet &xs, long row, const float *T, int ldt, int nv, int total, float lr, float alpha) {
-        return dpx && dpx->step(at(xs, row), nullptr, T, ldt, nv, total, lr, alpha, s) == 0;
+        const int *L = xs.lab ? xs.lab + row : nullptr;
+        return dpx && dpx->step(at(xs, row), L, L ? nullptr : T, ldt, nv, total, lr, alpha, s) == 0;
     }
     BOOL gather_masters() { return !dpx || dpx->gather_masters(s) == 0; }
     bool has_dpx() const { return (bool)dpx; }
@@ -1166,6 +1197,7 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
     XSet xs;
     TT *Td = nullptr;
     if (!net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &xs)) return FALSE;
+    if (!attach_labels(&xs, T, n, (int)k->n_outputs, rows_p, o->type, s)) return FALSE;
     {
         std::vector<TT> tf((size_t)rows_p * k->n_outputs, (TT)0);
         for (size_t i = 0; i < (size_t)n * k->n_outputs; i++) tf[i] = (TT)T[i];
@@ -1307,6 +1339,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
         if (!ok) break;
         if (!loopback || g == 0) {
             ok = nets[g]->upload_x(X, (int)n, (int)k->n_inputs, rows_p, &Xd[g]);
+            if (ok) ok = attach_labels(&Xd[g], T, n, n_out, rows_p, o->type, str[g]);
             if (ok) {
                 std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
                 for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];
@@ -1517,6 +1550,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     XSet Xd;
     TT *Td = nullptr;
     BOOL ok = net.upload_x(X, (int)n, (int)k->n_inputs, rows_p, &Xd);
+    if (ok) ok = attach_labels(&Xd, T, n, n_out, rows_p, o->type, s);
     if (ok) {
         std::vector<TT> tf((size_t)rows_p * n_out, (TT)0);
         for (size_t i = 0; i < (size_t)n * n_out; i++) tf[i] = (TT)T[i];

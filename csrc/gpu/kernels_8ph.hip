@@ -504,15 +504,7 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
             const int n = n0 + e / 64, m = m0 + 4 * (e % 64);
             const float *p = slab + (size_t)n * ldg + m;
             f32x4 g = {0.f, 0.f, 0.f, 0.f};
-            for (int s0 = 0; s0 < splits; s0 += 8) {
-                f32x4 v[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    v[k] = s0 + k < splits ? hpnn::ld_sc1(p + (size_t)(s0 + k) * ss) : f32x4{0.f, 0.f, 0.f, 0.f};
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int k = 0; k < 8; k++) g += v[k];
-            }
+            for (int s0 = 0; s0 < splits; s0 += 8) g += hpnn::sum_sc1_x8(p + (size_t)s0 * ss, ss, splits - s0);
             const size_t idx = (size_t)n * ldg + m;
             f32x4 ww = *(const f32x4 *)(upd.W32 + idx);
             if (upd.momentum) {

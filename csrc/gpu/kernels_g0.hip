@@ -47,7 +47,7 @@ using hpnn::bf16x8;
 using hpnn::f32x4;
 using hpnn::TnTail;
 using hpnn::gu32;
-using hpnn::ld_sc1;
+using hpnn::sum_sc1_x8;
 using hpnn::st_sc1;
 
 /* Dg: [Bt/32][N/16][64][8], Hg: [Bt/32][M/16][64][8]; nbd = N / 16, nbh = M / 16.
@@ -328,15 +328,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
         if (e < e1) {
             const float *p = slab + (size_t)(nt0 + row) * ldg + col;
-            for (int s = s0; s < s1; s += 8) {
-                f32x4 v[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    v[j] = s + j < s1 ? ld_sc1(p + (size_t)(s + j) * ss) : f32x4{0.f, 0.f, 0.f, 0.f};
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int j = 0; j < 8; j++) sum += v[j];
-            }
+            for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
         }
         red[t] = sum;
         __syncthreads();

@@ -233,9 +233,10 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
         }
         __syncthreads();
         f32x4 v[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = ld_sc1(pin + e * 64);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {
+            const float *q = (const float *)pin; /* 8 float4 rows, 64 float4 apart */
+            ld_sc1_x8(v, q, q + 256, q + 512, q + 768, q + 1024, q + 1280, q + 1536, q + 1792);
+        }
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll

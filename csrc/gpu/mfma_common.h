@@ -252,6 +252,41 @@ __device__ __forceinline__ f32x4 ld_sc1(const void *p) {
     asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
+/* 8 such loads AND their drain in ONE asm block.  With separate asm statements (loads, then
+ * "s_waitcnt vmcnt(0)") the compiler may read a destination register -- a select, a copy,
+ * an add -- between them, i.e. while the load is still in flight, and get stale data: the
+ * outputs of this block only exist once the wait has retired them. */
+__device__ __forceinline__ void ld_sc1_x8(f32x4 (&v)[8], const float *p0, const float *p1, const float *p2,
+                                          const float *p3, const float *p4, const float *p5, const float *p6,
+                                          const float *p7) {
+    asm volatile(
+        "global_load_dwordx4 %0, %8, off sc1\n\t"
+        "global_load_dwordx4 %1, %9, off sc1\n\t"
+        "global_load_dwordx4 %2, %10, off sc1\n\t"
+        "global_load_dwordx4 %3, %11, off sc1\n\t"
+        "global_load_dwordx4 %4, %12, off sc1\n\t"
+        "global_load_dwordx4 %5, %13, off sc1\n\t"
+        "global_load_dwordx4 %6, %14, off sc1\n\t"
+        "global_load_dwordx4 %7, %15, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+        : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7)
+        : "memory");
+}
+/* sum over n <= 8 consecutive slabs (stride ss floats) of the float4 at p, via ld_sc1_x8:
+ * the slots past n load slab 0 again and are dropped after the wait */
+__device__ __forceinline__ f32x4 sum_sc1_x8(const float *p, size_t ss, int n) {
+    f32x4 v[8];
+    const float *q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = p + (size_t)(j < n ? j : 0) * ss;
+    ld_sc1_x8(v, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
+    f32x4 g = v[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++)
+        if (j < n) g += v[j];
+    return g;
+}
 
 /* Optional tail work of a TN launch: a grouped slab reduction (reduce_groups_kernel of
  * kernels_mlp3.hip: out[g*ostride + i] = sum of slabs [g*SG, min(S, (g+1)*SG)), float4 i)

@@ -67,7 +67,8 @@ def test_train_nn_batched_equals_python_plan(tmp_path, gpu, net, train, dims, B,
     assert m.fused_mode == {"t": "t", "x": "x", "w": "w", None: None}[mode]
     tmp = formats.read_kernel(os.path.join(d, "kernel.tmp"))["weights"]
     for a, b in zip(tmp, m.host_weights()):
-        assert np.abs(a - b.numpy()).max() < 1e-14  # same seeded init (ann.c:632-766)
+        # same seeded init (ann.c:632-766); the plan keeps FP32 masters
+        assert np.abs(a - b.numpy()).max() <= 2.0 ** -24 * np.abs(a).max()
     order = _order(n, seed)
     Xo, To = X[order], T[order]
     for s in range(steps):
