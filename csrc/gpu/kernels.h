@@ -112,6 +112,8 @@ typedef struct {
     /* non-NULL: no step -- the fully reduced gradients are stored instead, G0 [N][M] at gout,
      * [G1 | G2] right after it (the flat layout of the plan's gradient buffer; data parallel) */
     float *gout;
+    int proto; /* hand-off diagnostics (HPNN_G0_PROTO): 1 producer agent release, 2 consumer agent
+                * acquire, 4 system-scope (sc0 sc1) partial loads */
 } hpnn_g0_update;
 int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
                                int M, int Bt, int splits, const hpnn_g0_update *u, hipStream_t stream);

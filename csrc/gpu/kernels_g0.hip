@@ -294,6 +294,10 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     __syncthreads();
     __shared__ unsigned int want_s;
     if (t == 0) {
+        if (u.proto & 1) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         const unsigned int old = atomicAdd(u.cnt + 32 * tile, 1u);
         want_s = old - old % (unsigned)splits + (unsigned)splits; /* this launch's last ticket */
     }
@@ -313,6 +317,10 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
                 break;
             }
         }
+        if (u.proto & 2) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
     __syncthreads();
     /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
@@ -328,7 +336,10 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
         if (e < e1) {
             const float *p = slab + (size_t)(nt0 + row) * ldg + col;
-            for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
+            if (u.proto & 4)
+                for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8<true>(p + (size_t)s * ss, ss, s1 - s);
+            else
+                for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
         }
         red[t] = sum;
         __syncthreads();
@@ -397,10 +408,13 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
     if (tiles > 7) return -1; /* counters 32 words apart in a 256-word block, err at word 224 */
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+    static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
+    hpnn_g0_update uu = *u;
+    uu.proto |= proto;
 #define HPNN_G0F(U8_)                                                                                              \
     hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_>), dim3(tiles * splits), dim3(512), 0, stream,              \
                        (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
-                       xcd_map, *u)
+                       xcd_map, uu)
     if (h_u8) HPNN_G0F(true);
     else HPNN_G0F(false);
 #undef HPNN_G0F

@@ -244,8 +244,13 @@ __device__ __forceinline__ float wave_sum(float v) {
 typedef __attribute__((address_space(1))) unsigned int gu32;
 /* 16-byte write-through store / L1-bypassing load (global_*_dwordx4 ... sc1); the loads
  * are issued in a batch and drained by the caller's s_waitcnt vmcnt(0) */
+/* The s_nop: a VALU write of a >8-byte store's data VGPRs right behind the store corrupts the
+ * stored bytes (a CDNA VMEM store-data hazard).  The compiler's hazard recognizer pads its own
+ * stores, not this one, and it does reuse the data registers at once (seen: the next
+ * instruction rewrote v[2:3] of a global_store_dwordx4 v[..], v[2:5]: the first 8 bytes of
+ * some lanes' float4 were lost); two wait states inside the asm cover it. */
 __device__ __forceinline__ void st_sc1(void *p, const f32x4 &v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ f32x4 ld_sc1(const void *p) {
     f32x4 v;
@@ -256,31 +261,37 @@ __device__ __forceinline__ f32x4 ld_sc1(const void *p) {
  * "s_waitcnt vmcnt(0)") the compiler may read a destination register -- a select, a copy,
  * an add -- between them, i.e. while the load is still in flight, and get stale data: the
  * outputs of this block only exist once the wait has retired them. */
+#define HPNN_LDX8(BITS)                                                                                         \
+    asm volatile("global_load_dwordx4 %0, %8, off " BITS "\n\t"                                                   \
+                 "global_load_dwordx4 %1, %9, off " BITS "\n\t"                                                   \
+                 "global_load_dwordx4 %2, %10, off " BITS "\n\t"                                                  \
+                 "global_load_dwordx4 %3, %11, off " BITS "\n\t"                                                  \
+                 "global_load_dwordx4 %4, %12, off " BITS "\n\t"                                                  \
+                 "global_load_dwordx4 %5, %13, off " BITS "\n\t"                                                  \
+                 "global_load_dwordx4 %6, %14, off " BITS "\n\t"                                                  \
+                 "global_load_dwordx4 %7, %15, off " BITS "\n\t"                                                  \
+                 "s_waitcnt vmcnt(0)"                                                                            \
+                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),      \
+                   "=&v"(v[7])                                                                                   \
+                 : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7)                       \
+                 : "memory")
+template <bool SYS = false>
 __device__ __forceinline__ void ld_sc1_x8(f32x4 (&v)[8], const float *p0, const float *p1, const float *p2,
                                           const float *p3, const float *p4, const float *p5, const float *p6,
                                           const float *p7) {
-    asm volatile(
-        "global_load_dwordx4 %0, %8, off sc1\n\t"
-        "global_load_dwordx4 %1, %9, off sc1\n\t"
-        "global_load_dwordx4 %2, %10, off sc1\n\t"
-        "global_load_dwordx4 %3, %11, off sc1\n\t"
-        "global_load_dwordx4 %4, %12, off sc1\n\t"
-        "global_load_dwordx4 %5, %13, off sc1\n\t"
-        "global_load_dwordx4 %6, %14, off sc1\n\t"
-        "global_load_dwordx4 %7, %15, off sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
-        : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7)
-        : "memory");
+    if constexpr (SYS) HPNN_LDX8("sc0 sc1");
+    else HPNN_LDX8("sc1");
 }
+#undef HPNN_LDX8
 /* sum over n <= 8 consecutive slabs (stride ss floats) of the float4 at p, via ld_sc1_x8:
  * the slots past n load slab 0 again and are dropped after the wait */
+template <bool SYS = false>
 __device__ __forceinline__ f32x4 sum_sc1_x8(const float *p, size_t ss, int n) {
     f32x4 v[8];
     const float *q[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) q[j] = p + (size_t)(j < n ? j : 0) * ss;
-    ld_sc1_x8(v, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
+    ld_sc1_x8<SYS>(v, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
     f32x4 g = v[0];
 #pragma unroll
     for (int j = 1; j < 8; j++)
