@@ -171,7 +171,9 @@ int BPlan::configure(const int *sizes, int n_layers, int net_type, int batch_siz
         const long pb = wide_ksplit == 2 ? hpnn_wide2_pbuf_bytes(Bp) : 16;
         add("wpbuf", -1, BD_F32, {pb / 4}, false);
         add("wwords", -1, BD_I32, {2L * (Bp / TILE_W) + 4}, true);
-        add("tncnt", -1, BD_I32, {1024}, true); /* fused split-K TN steps: tickets + error word */
+        /* fused split-K TN steps: a ticket block of its own per layer (the counters are monotonic
+         * and the S of each layer differs), then the error word */
+        add("tncnt", -1, BD_I32, {(long)(L + 1) * 1024}, true);
     }
     return 0;
 }
@@ -390,10 +392,11 @@ int BPlan::grad_and_update_layers(const XIn &x, float lr, float alpha, float sca
                                                     Wt[l], lr, alpha, scale, momentum ? 1 : 0, s) == 0)
             continue;
         /* several splits: reduced and stepped inside the 8-phase TN launch (one layer at a
-         * time: the tickets of tncnt are per launch) */
+         * time: each layer has its own ticket block, every launch of it adds S[l] per tile) */
         if (tncnt && g0_fused && S[l] > 1 && !(l == 0 && W0f) &&
             hpnn_gemm_tn8_fused_update(D[l], Np[l], Hin, Kp[l], Np[l], Kp[l], Bp, S[l], slab[l], W32[l], V32[l], Wb[l],
-                                       Wt[l], lr, alpha, scale, momentum ? 1 : 0, tncnt, tncnt + 1023, s) == 0)
+                                       Wt[l], lr, alpha, scale, momentum ? 1 : 0, tncnt + 1024 * l, tncnt + 1024 * L,
+                                       s) == 0)
             continue;
         int r = grad_layer(l, x, false, s);
         if (!r) r = update_layer(l, lr, alpha, scale, false, s);
@@ -556,7 +559,7 @@ int BPlan::health(hipStream_t s) {
     unsigned int e[2] = {0, 0};
     if (g0cnt && hipMemcpyAsync(&e[0], g0cnt + 224, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
     unsigned int e2 = 0;
-    if (tncnt && hipMemcpyAsync(&e2, tncnt + 1023, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
+    if (tncnt && hipMemcpyAsync(&e2, tncnt + 1024 * L, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
     if (wwords && hipMemcpyAsync(&e[1], wwords + 2 * (Bp / TILE_W), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return -7;
     if (hipStreamSynchronize(s) != hipSuccess) return -7;

@@ -763,7 +763,8 @@ extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H,
     const int units = Bt / 64;
     if (units % splits || (units / splits) % 2) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    /* tickets: 32 words apart in 1024; at least min_wg workgroups (HPNN_TN8_MINWG, default
+    /* tickets: 32 words apart in 1024 (a block the caller keeps for this GEMM shape: the
+     * counters are monotonic, every launch must add `splits` per tile); at least min_wg workgroups (HPNN_TN8_MINWG, default
      * half the CUs: fewer splits leave the chip idle while each reduces a larger share) */
     static const int min_wg = [] { const char *e = getenv("HPNN_TN8_MINWG"); return e ? atoi(e) : 0; }();
     if (ntiles > 31 || ntiles * splits > cus || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;

@@ -586,7 +586,10 @@ struct TpNetBf16 {
                                   HPNN_EPI_ACT, 0, s),
                 "forward GEMM");
             if (P > 1) {
-                if (!coll->all_gather((const float *)Hloc[l], (float *)hstage, (long)Bp * n[l] / 2, s)) return FALSE;
+                if (!coll->all_gather((const float *)Hloc[l], (float *)hstage, (long)Bp * n[l] / 2, s)) {
+                    NN_ERROR(stderr, "tensor-parallel activation all-gather failed (layer %d)\n", l);
+                    return FALSE;
+                }
                 TPK(hpnn_block_permute_bf16(hstage, Hfull[l], P, Bp, n[l], s), "activation permute");
             }
         }
@@ -616,7 +619,10 @@ struct TpNetBf16 {
                         "partial delta GEMM");
                 const float *sum = part;
                 if (P > 1) {
-                    if (!coll->reduce_scatter(part, dred, (long)Bp * m, s)) return FALSE;
+                    if (!coll->reduce_scatter(part, dred, (long)Bp * m, s)) {
+                        NN_ERROR(stderr, "tensor-parallel delta reduce-scatter failed (layer %d)\n", l);
+                        return FALSE;
+                    }
                     sum = dred;
                 }
                 TPK(hpnn_dact_f32_bf16(Dloc[l - 1], sum, Hloc[l - 1], (long)Bp * m, s), "f' epilogue");
@@ -638,11 +644,11 @@ struct TpNetBf16 {
     BOOL batch_step(int b, int, int nv, double lr, double alpha, bool mom) {
         return step((const char *)X16 + (size_t)b * Bp * Mp[0] * 2, T32 + (size_t)b * Bp * n_out, nv, lr, alpha, mom);
     }
-    size_t stage_elems() const { /* in floats */
+    size_t stage_elems() const { /* in floats: every rank's whole send buffer */
         size_t st = 0;
         for (int l = 0; l < L - 1; l++) {
-            st = std::max(st, (size_t)P * Bp * n[l] / 2);
-            if (l + 1 < L - 1) st = std::max(st, (size_t)P * Bp * n[l]);
+            st = std::max(st, (size_t)P * Bp * n[l] / 2);                     /* all-gather (BF16) */
+            if (l + 1 < L - 1) st = std::max(st, (size_t)P * P * Bp * n[l]); /* reduce-scatter */
         }
         for (int l = 0; l < L; l++) st = std::max(st, (size_t)P * n[l] * Mp[l]);
         return st;

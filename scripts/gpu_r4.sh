@@ -35,6 +35,11 @@ for s in "$@"; do
       HPNN_SPLITS=16,64 HPNN_TN8_MINWG=64 step rruff_s64 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       HPNN_SPLITS=16,128 step rruff_s128 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       HPNN_SPLITS=16,64 step rruff_s64u 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
+    mnistab)  # fused G0 (2 launches) vs G0 + update launch, interleaved on one box
+      step mnist_f1 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_FUSED=0 step mnist_f0 200 python bench.py --steps 200 --warmup 20 &&
+      step mnist_f1b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_FUSED=0 step mnist_f0b 200 python bench.py --steps 200 --warmup 20 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
