@@ -40,6 +40,9 @@ for s in "$@"; do
       HPNN_G0_FUSED=0 step mnist_f0 200 python bench.py --steps 200 --warmup 20 &&
       step mnist_f1b 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_G0_FUSED=0 step mnist_f0b 200 python bench.py --steps 200 --warmup 20 ;;
+    pmc) PMC_TAG=_$tag step pmc 600 bash scripts/pmc_step.sh ;;
+    pmc_rruff) PMC_TAG=_${tag}_rruff step pmc_rruff 600 bash scripts/pmc_step.sh --model rruff ;;
+    trace) HPNN_TILE_TRACE=1 step tile_trace 200 python scripts/tile_trace.py ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
