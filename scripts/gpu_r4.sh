@@ -28,6 +28,7 @@ for s in "$@"; do
     libbench) step libbench 900 python scripts/lib_vs_bench.py --out $O/lib_vs_bench.jsonl ;;
     fpbench) step fpbench 300 python scripts/gemm_fp_bench.py --out $O/gemm_fp.jsonl ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
+    prof0) HPNN_G0_FUSED=0 step rocprof0 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof0 -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
     fpsteps) step fpsteps 600 python scripts/lib_vs_bench.py --dtype f64 --configs mnist,rruff,wide --batches 2 --epochs 3 --out $O/fp64_steps.jsonl ;;
     rruffab)  # G1 split variants on the fused 8-phase TN reduction + update
