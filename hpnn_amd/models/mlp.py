@@ -231,7 +231,9 @@ class MLP:
         if X.shape[0] < self.Bp or X.shape[1] != self.Kp[0] or X.stride(0) != self.Kp[0]:
             raise ValueError(f"batch {tuple(X.shape)} does not fit this plan (Bp {self.Bp}, Kp0 {self.Kp[0]})")
         xg = self._fm_input(X) if self.fused_mode == "x" else None
-        return X.data_ptr(), _p(xg), int(xg is not None), float(getattr(X, "hpnn_fm_scale", 1.0))
+        # mode x: the u8 flag describes the fragment-major copy (8-bit pixels or BF16)
+        return (X.data_ptr(), _p(xg), int(xg is not None and xg.dtype == torch.uint8),
+                float(getattr(X, "hpnn_fm_scale", 1.0)))
 
     @staticmethod
     def _tgt(labels, T):
