@@ -245,8 +245,21 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
     for (long b0 = c0; b0 < c1; b0 += C4) {
         const long e4 = b0 + c;
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
-        if (e4 < c1)
-            for (int r = rg; r < u.mrows; r += RG) a += *(const f32x4 *)(u.mslab + (long)r * u.mstride + e4 * 4);
+        if (e4 < c1) {
+            /* 8 rows' loads in flight per batch (a dependent one-at-a-time walk over the rows is
+             * latency-bound: ~8 L2 / Infinity-Cache round trips back to back) */
+            const float *col = u.mslab + e4 * 4;
+            for (int r0 = rg; r0 < u.mrows; r0 += 8 * RG) {
+                f32x4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int r = r0 + k * RG;
+                    v[k] = r < u.mrows ? *(const f32x4 *)(col + (long)r * u.mstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) a += v[k];
+            }
+        }
         red[t] = a;
         __syncthreads();
         if (rg == 0 && e4 < c1) {

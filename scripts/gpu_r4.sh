@@ -44,6 +44,11 @@ for s in "$@"; do
     pmc) PMC_TAG=_$tag step pmc 600 bash scripts/pmc_step.sh ;;
     pmc_rruff) PMC_TAG=_${tag}_rruff step pmc_rruff 600 bash scripts/pmc_step.sh --model rruff ;;
     trace) HPNN_TILE_TRACE=1 step tile_trace 200 python scripts/tile_trace.py ;;
+    rruffab2)  # fused 8-phase TN split-K reduction + step (layer 0) vs slabs + update launch
+      step rruff_t1 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN8_FUSED=0 step rruff_t0 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      step rruff_t1b 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN8_FUSED=0 step rruff_t0b 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
