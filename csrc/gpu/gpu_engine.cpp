@@ -1386,6 +1386,10 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
+    /* RCCL replicas: one HIP graph per replica epoch (HPNN_GRAPH=0: eager) */
+    const bool dp_graphs = !loopback && graphs_enabled() && n_batches <= 4096;
+    std::vector<hipGraphExec_t> gexec(G, nullptr);
+    std::vector<int> gtried(G, 0);
     for (UINT e = 0; e < o->epochs && ok; e++) {
         for (int g = 0; g < G; g++) {
             hipSetDevice(dev[g]);
@@ -1423,6 +1427,9 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                         return;
                     }
                     Net &net = *nets[g];
+                    /* the replica's epoch (HIP graph: captured on the first epoch, the RCCL
+                     * collectives and the side-stream fork / join included; replayed after) */
+                    auto epoch_body = [&]() -> bool {
                     for (int b = 0; b < n_batches; b++) {
                         const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
                         const int start = b * B + g * Bg;
@@ -1449,6 +1456,18 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                             NN_ERROR(stderr, "data-parallel step failed on replica %d\n", g);
                             tok[g] = 0;
                         }
+                    }
+                    return tok[g] != 0;
+                    };
+                    if (dp_graphs && !gtried[g]) {
+                        gtried[g] = 1;
+                        if (!capture_epoch(str[g], epoch_body, &gexec[g]))
+                            NN_DBG(stdout, "data-parallel replica %d: epoch not capturable, eager launches\n", g);
+                    }
+                    if (gexec[g]) {
+                        if (hipGraphLaunch(gexec[g], str[g]) != hipSuccess) tok[g] = 0;
+                    } else {
+                        epoch_body();
                     }
                     if (hipStreamSynchronize(str[g]) != hipSuccess) tok[g] = 0;
                 });
@@ -1477,6 +1496,11 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
                                (UINT64)n * (e + 1));
     }
     auto t1 = std::chrono::steady_clock::now();
+    for (int g = 0; g < G; g++)
+        if (gexec[g]) {
+            hipSetDevice(dev[g]);
+            hipGraphExecDestroy(gexec[g]);
+        }
     if (ok) {
         hipSetDevice(dev[0]);
         ok = nets[0]->download(k);
