@@ -49,6 +49,8 @@ for s in "$@"; do
       HPNN_TN8_FUSED=0 step rruff_t0 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       step rruff_t1b 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       HPNN_TN8_FUSED=0 step rruff_t0b 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
+    dpforce)  # the N > 1 MNIST step path (xGMI all-reduce + update) timed with one rank on this GPU
+      HPNN_DP_FORCE=1 step dpforce 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --steps 200 --warmup 20 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
