@@ -316,9 +316,7 @@ int BPlan::front(const XIn &x, const int *labels, const float *T, int ldt, int n
     int r;
     switch (mode) {
     case 't':
-        /* the front reads the row-fragment-major copy (xg), G0 the fragment-major batch (x) */
-        if (!x.xg) return -2;
-        r = hpnn_mlp3_tile(x.xg, x.u8, x.u8 ? x.scale : 1.f, Kp[0], W0f, Wb[1], Wb[2], Wt[2], labels, T, ldt, 1.f, t_lo,
+        r = hpnn_mlp3_tile(x.x, x.u8, x.u8 ? x.scale : 1.f, Kp[0], W0f, Wb[1], Wb[2], Wt[2], labels, T, ldt, 1.f, t_lo,
                            D[0], midslab, stats, hits, Bp, n_valid, n_out, type, mid_grid, s);
         return r > 0 ? 0 : (r ? r : -1);
     case 'x':

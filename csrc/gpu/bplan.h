@@ -51,11 +51,9 @@ struct BufSpec {
     size_t bytes() const;
 };
 
-/* one prepared minibatch: x = row-major [Bp][Kp0] BF16, or for mode 't' fragment-major
- * [Bp/32][Kp0/16][64][8] (8-bit when u8; the first-layer gradient's operand); xg = mode 't':
- * the row-fragment-major copy [Bp/16][Kp0/32][64][8] the tile front reads (required), mode
- * 'x': a fragment-major copy for the first-layer gradient (8-bit when u8, may be null); the
- * network sees bf16(byte * scale) */
+/* one prepared minibatch: x = the front's input (row-major [Bp][Kp0] BF16, or fragment-major
+ * [Bp/32][Kp0/16][64][8] for mode 't', 8-bit when u8), xg = fragment-major 8-bit copy for the
+ * first-layer gradient (mode 'x' only, may be null); the network sees bf16(byte * scale) */
 struct XIn {
     const void *x = nullptr;
     const void *xg = nullptr;

@@ -632,23 +632,6 @@ std::vector<E> to_fragment_major(const DOUBLE *src, int rows, int cols, int rows
     return out;
 }
 
-/* host [rows][cols] -> ROW-fragment-major [rows_p/16][cols_p/32][64][8]
- * (hpnn_amd.ops.to_row_fragment_major: lane 16 h + r of fragment (u, s) holds
- * A[16 u + r][32 s + 8 h + j], j < 8), zero padded: the tile front's operand layout */
-template <typename E, typename Cvt>
-std::vector<E> to_row_fragment_major(const DOUBLE *src, int rows, int cols, int rows_p, int cols_p, Cvt cvt) {
-    std::vector<E> out((size_t)rows_p * cols_p, (E)0);
-    const int nks = cols_p / 32;
-    for (int r = 0; r < rows; r++) {
-        const int u = r / 16, rr = r % 16;
-        for (int c = 0; c < cols; c++) {
-            const size_t idx = ((((size_t)u * nks + c / 32) * 64) + 16 * ((c % 32) / 8) + rr) * 8 + c % 8;
-            out[idx] = cvt(src[(size_t)r * cols + c]);
-        }
-    }
-    return out;
-}
-
 /* BF16 batched engine: an adapter of the library's batched plan (bplan.h, the same object
  * hpnn_amd.models.MLP binds) to the precision-generic drivers below */
 struct Batched {
@@ -730,21 +713,16 @@ struct Batched {
             HIPCHK(hipStreamSynchronize(s));
             return TRUE;
         };
-        if (lay == 1) { /* fragment-major (G0) + row-fragment-major (the tile front) */
+        if (lay == 1) {
             if (u8) {
-                auto cv = [](DOUBLE v) { return (uint8_t)v; };
-                auto h = to_fragment_major<uint8_t>(src, rows, cols, rows_p, Kp0, cv);
-                xs->row_bytes = xs->row_bytes_g = Kp0;
-                if (!put(h.data(), h.size(), &xs->x)) return FALSE;
-                h = to_row_fragment_major<uint8_t>(src, rows, cols, rows_p, Kp0, cv);
-                return put(h.data(), h.size(), &xs->xg);
+                auto h = to_fragment_major<uint8_t>(src, rows, cols, rows_p, Kp0, [](DOUBLE v) { return (uint8_t)v; });
+                xs->row_bytes = Kp0;
+                return put(h.data(), h.size(), &xs->x);
             }
-            auto cv = [](DOUBLE v) { return bf16_bits((float)v); };
-            auto h = to_fragment_major<uint16_t>(src, rows, cols, rows_p, Kp0, cv);
-            xs->row_bytes = xs->row_bytes_g = (size_t)Kp0 * 2;
-            if (!put(h.data(), h.size() * 2, &xs->x)) return FALSE;
-            h = to_row_fragment_major<uint16_t>(src, rows, cols, rows_p, Kp0, cv);
-            return put(h.data(), h.size() * 2, &xs->xg);
+            auto h = to_fragment_major<uint16_t>(src, rows, cols, rows_p, Kp0,
+                                                 [](DOUBLE v) { return bf16_bits((float)v); });
+            xs->row_bytes = (size_t)Kp0 * 2;
+            return put(h.data(), h.size() * 2, &xs->x);
         }
         if (!upload_bf16(src, rows, cols, rows_p, Kp0, &xs->x, s)) return FALSE;
         xs->row_bytes = (size_t)Kp0 * 2;

@@ -6,23 +6,26 @@
  * (ann.c:883-888, 1279-1592; snn.c:280-335, 481-794; cuda_ann.cu:426-2093,
  * cuda_snn.cu:156-976 softmax, 2726-3717 train_momentum), batched.
  *
- * Input: the minibatch ROW-fragment-major ([Bp/16][K0/32][64 lanes][8], lane l = 16 h + r
- * of fragment (u, s) holding X[16 u + r][32 s + 8 h + j], j < 8; ops.to_row_fragment_major),
- * either 8-bit pixels (the exact integers in BF16, the pixel scale xscale applied to the FP32
- * accumulator: H1 = f(xscale * X W0^T)) or BF16 (xscale 1).
+ * Input: the minibatch in FRAGMENT-MAJOR order ([Bp/32][K0/16][64 lanes][8], lane
+ * l = 16 g + r of chunk (t, cb) holding X[32 t + 8 g + j][16 cb + r], j < 8; see
+ * ops.to_fragment_major), either 8-bit pixels (the exact integers in BF16, the pixel scale
+ * xscale applied to the FP32 accumulator: H1 = f(xscale * X W0^T)) or BF16 (xscale 1).
+ * It is the SAME buffer the first-layer gradient kernel (kernels_g0.hip,
+ * gemm_fm_direct) streams right after this one, so a step reads the batch from HBM
+ * once; the second read is served by the 256 MB Infinity Cache.
  *
  * One 512-thread workgroup (8 waves) per CU; per 256-sample tile:
  *
  *  A  H1 = f(X W0^T)  [256 x 128]: K0/32 k-steps.  Wave (ng = w&3, sh = w>>2) owns 32
  *     neurons x 128 samples (16 MFMA 16x16x32 per k-step, 64 accumulator registers).
- *     Both operands come straight into registers: its two W0 fragments per k-step from the
- *     L2-resident fragment-major copy, its eight X fragments from the ROW-fragment-major
- *     copy of the batch (ops.to_row_fragment_major: each fragment already the MFMA B
- *     operand, 8-bit pixels converted in registers); the four neuron-group waves of a sample
- *     half read the same X fragments (vector-L1 hits).  Loads run D k-steps ahead (register
- *     ring); no LDS and no barrier inside phase A.  The K loop is fully unrolled (K0 is a
- *     template parameter) so every ring index is static and the compiler's counted vmcnt
- *     waits stay exact.
+ *     Its two W0 fragments per k-step come straight from the L2-resident fragment-major
+ *     copy into registers (1 KiB per wave load); the X slice (256 samples x 32 features,
+ *     8 KiB of pixels) is loaded once per workgroup, one 16-byte load per lane,
+ *     converted in registers and written as the transposed image X^T [32 feat][256
+ *     samples] into one of two LDS stages; MFMA B operands are read from it with
+ *     ds_read_b64_tr_b16.  Loads run D k-steps ahead (register ring), one barrier per
+ *     k-step.  The K loop is fully unrolled (K0 is a template parameter) so every ring
+ *     index is static and the compiler's counted vmcnt waits stay exact.
  *  B  back chain, per wave on ITS OWN 32 samples (no workgroup barrier inside):
  *     H2 = f(H1 W1^T), logits, softmax / sigmoid + loss + delta3 + argmax,
  *     delta2 = (delta3 W2) f'(H2), delta1 = (delta2 W1) f'(H1) -> HBM (fragment-major,
@@ -36,14 +39,11 @@
  * latency-bound back chain runs once per 256 samples with 8x the independent MFMA work
  * per phase, and needs 2 barriers per tile instead of 4 per 32 samples.
  *
- * LDS (160 KiB): H1 [256][128] 64 KiB | H2 [256][64] 32 KiB | delta2 [256][64] 32 KiB |
- * delta3 [256][32] 16 KiB | W1 [64][128] 16 KiB.  All images use the T32 layout of
- * mfma_common.h.  (W1 / W1^T operands straight from the L2 into registers instead of the W1
- * image measured slower: 62.5-62.8 vs 60.2-60.7 us per step -- an L2 hit costs ~2-3K shader
- * clocks under the streaming of phase A.)
- *
- * Inputs: Xg = the batch ROW-fragment-major ([Bp/16][K0/32][64][8]); the first-layer
- * gradient (kernels_g0.hip) streams the fragment-major copy ([Bp/32][K0/16][64][8]).
+ * LDS (160 KiB, exactly): H1 [256][128] 64 KiB | X^T stages 2 x 16 KiB, aliased by
+ * H2 [256][64] in the chain | delta2 [256][64] 32 KiB | delta3 [256][32] 16 KiB |
+ * W1 [64][128] 16 KiB.  All images use the T32 layout of mfma_common.h.  (W1 / W1^T operands
+ * straight from the L2 into registers instead of the W1 image measured slower: 62.5-62.8 vs
+ * 60.2-60.7 us per step -- under phase A's streaming an L2 hit costs ~2-3K shader clocks.)
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -61,12 +61,16 @@ using namespace hpnn::mlp3;
 namespace {
 
 constexpr int TS = 256;              /* samples per tile */
+constexpr int XR = 32;               /* features per k-step (rows of the X^T stage) */
+constexpr int IMG_XT = XR * TS * 2;  /* 16 KiB */
 constexpr int OFF_H1 = 0;
-constexpr int OFF_H2 = OFF_H1 + TS * H1 * 2;
-constexpr int OFF_D2 = OFF_H2 + TS * H2 * 2;
+constexpr int OFF_XT = OFF_H1 + TS * H1 * 2;
+constexpr int OFF_H2 = OFF_XT; /* chain only: the X^T stages are dead then */
+constexpr int OFF_D2 = OFF_XT + 2 * IMG_XT;
 constexpr int OFF_D3 = OFF_D2 + TS * H2 * 2;
 constexpr int OFF_W1 = OFF_D3 + TS * NO * 2;
 constexpr int LDS_TOTAL = OFF_W1 + IMG_W1;
+static_assert(TS * H2 * 2 <= 2 * IMG_XT, "H2 aliases the X^T stages");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
 
 /* within-wave ordering of LDS writes before other lanes' reads (one wave's LDS
@@ -99,8 +103,12 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
      * per-wave latency).  Phase A on 32 x 128 wave tiles: 64 x 64 (half the B reads, twice
      * the W0 fragments) measured 59.1-59.9 vs 58.1-58.9 us same box. */
     constexpr int NW = 8;
-    constexpr int FB = XU8 ? 512 : 1024; /* bytes of one row-fragment-major X fragment */
-    using XF = typename std::conditional<XU8, uint2, bf16x8>::type; /* one lane's share of it */
+    constexpr int CHUNK = XU8 ? 512 : 1024; /* bytes of one 32 x 16 input chunk */
+    constexpr int NCB = 2 * KS;             /* 16-feature blocks per 32-sample row of chunks */
+    /* per k-step the workgroup loads 16 chunks (8 sample rows x 2 feature halves): wave w
+     * takes row w, lane half h = l >> 5 takes feature half h, XB bytes per lane (2 fm lanes) */
+    constexpr int XB = 16 * (XU8 ? 1 : 2); /* bytes per lane per k-step */
+    constexpr int XV = XB / 16;            /* 16-byte vectors per lane */
     constexpr int SG = NW / 4;           /* phase A: sample groups (waves per neuron group) */
     constexpr int SPA = TS / SG;         /* phase A: samples per wave */
     constexpr int STA = SPA / 16;        /* phase A: 16-sample tiles per wave */
@@ -140,37 +148,72 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
     const int n_ot = n_out > 16 ? 2 : 1;
     const float inv_nout = 1.0f / (float)n_out;
 
-    /* this lane's 8 elements of a row-fragment-major fragment: fragment (16-sample tile u,
-     * k-step s) is 64 lanes x 8 elements at ((u KS + s) 64 + lane) 8, lane 16 h + r holding
-     * X[16 u + r][32 s + 8 h + j] -- the B operand of v_mfma_f32_16x16x32_bf16 as stored */
-    const char *xlane = (const char *)Xg + (size_t)lane * (FB / 64);
+    /* X^T stage image: row = feature within the k-step, column = sample of the tile.
+     * This lane converts fm slots 2i, 2i+1 (i = lane & 31) of chunk (t = wave, cb = 2s + lane/32). */
+    int xoff[2];
+    const int xi = lane & 31, xcbh = lane >> 5, xg = xi >> 3;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int row = 16 * xcbh + 2 * (xi & 7) + e;
+        xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
+    }
+    /* write order: lanes k = xi & 7 with bit 1 set write their odd row first.  Lane k's rows
+     * 2k + e sit at bank group 4 e + g(k) (g = t32_g(2k): 0 1 0 1 2 3 2 3), so in-order
+     * writes put each 8-lane ds_write_b128 group on 4 bank groups (2-way conflict); the
+     * swapped order spreads it over all 8 */
+    const int xp = (xi >> 1) & 1;
+    const int xa0 = xoff[xp], xa1 = xoff[xp ^ 1];
+    const char *xbase = (const char *)Xg + ((size_t)wave * NCB + xcbh) * CHUNK + (size_t)xi * XB;
+
+    /* transposed-read addresses of this wave's STA sample tiles in an X^T stage: sample tile
+     * st sits in 32-column sub-tile (STA/2) sh + st/2, with the T32 chunk swap (lo.tr ^ 32)
+     * on odd st; two bases + immediate offsets */
+    const char *xt_e = lds + OFF_XT + (STA / 2 * sh) * (XR * 64) + lo.tr;
+    const char *xt_o = lds + OFF_XT + (STA / 2 * sh) * (XR * 64) + (lo.tr ^ 32);
 
     for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile (delta1 out) */
-        /* this wave's STA 16-sample tiles: u = tile TS/16 + sh STA + st */
-        const char *xw = xlane + ((size_t)tile * (TS / 16) + sh * STA) * KS * FB;
+        const int T0 = tile * (TS / 32); /* first 32-sample chunk row of the tile */
+        const char *xtile = xbase + (size_t)T0 * NCB * CHUNK;
         const __bf16 *wbase = W0f + ((size_t)(2 * ng) * KS * 64 + lane) * 8;
 
-        XF xr[KS][STA];
+        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+        u32x4 xr[KS][XV];
         bf16x8 wr[KS][2];
-        /* the operands of k-step s in one batch: every wave loads its STA X fragments and two
-         * W0 fragments straight into registers (the 4 neuron-group waves of a sample half load
-         * the same X fragments: vector-L1 hits), D k-steps ahead; an opaque zero pins the loads
-         * to this point of the k-loop (the operands are read-only, so the compiler would
-         * otherwise hoist every load out of the tile loop: spills).  No LDS and no barrier in
-         * phase A (round 3 staged X^T through LDS: a ds_write + barrier + transposed reads per
-         * k-step, 1080 clocks a k-step against 512 of MFMA) */
-        auto issue = [&](int s) {
+        /* X(sx) and W0(sw) in one batch: an opaque zero pins the loads to this point of the
+         * k-loop (the operands are read-only, so the compiler would otherwise hoist every W0
+         * load out of the tile loop: spills).  X(k) is consumed two k-steps before W0(k)
+         * (converted into the LDS stage the B reads of step k come from), so the batch at
+         * step s carries X(s + D + 1) and W0(s + D - 1): step s then waits for exactly one
+         * batch, X(s + 2) for its conversion and W0(s) for its MFMAs. */
+        auto issue = [&](int sx, int sw) {
             unsigned int z = 0;
             asm volatile("" : "+s"(z));
-            if (s < KS) {
+            /* ABL (profiling only): 1 = W0 loaded by the sh = 0 waves only, 2 = no X loads */
+            if (sx < KS) {
 #pragma unroll
-                for (int st = 0; st < STA; st++)
-                    xr[s][st] = ABL == 2 ? XF{} : *(const XF *)(xw + z + ((size_t)st * KS + s) * FB);
+                for (int n = 0; n < XV; n++)
+                    xr[sx][n] = ABL == 2 ? u32x4{z, z, z, z}
+                                         : *(const u32x4 *)(xtile + z + (size_t)(2 * sx) * CHUNK + 16 * n);
+            }
+            if (sw >= 0 && sw < KS) {
 #pragma unroll
                 for (int i = 0; i < 2; i++)
-                    wr[s][i] = (ABL == 1 && sh == 1) ? bf16x8{} : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + s) * 512);
+                    wr[sw][i] = (ABL == 1 && sh == 1) ? bf16x8{}
+                                                      : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
             }
+        };
+        auto convert = [&](int s) {
+            char *img = lds + OFF_XT + (s & 1) * IMG_XT;
+            bf16x8 v[2];
+            if constexpr (XU8) {
+                v[0] = u8x8_int_bf16(xr[s][0][0], xr[s][0][1]);
+                v[1] = u8x8_int_bf16(xr[s][0][2], xr[s][0][3]);
+            } else {
+                v[0] = __builtin_bit_cast(bf16x8, xr[s][0]);
+                v[1] = __builtin_bit_cast(bf16x8, xr[s][1]);
+            }
+            *(bf16x8 *)(img + xa0) = xp ? v[1] : v[0];
+            *(bf16x8 *)(img + xa1) = xp ? v[0] : v[1];
         };
 
         f32x4 acc[2][STA];
@@ -179,30 +222,50 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
             for (int st = 0; st < STA; st++) acc[i][st] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-        /* the previous tile's chain and phase C read H1 / H2: every wave past them before this
-         * tile's H1 is written (phase A itself touches no LDS) */
+        /* B operand fragments of this wave's STA sample tiles from X^T stage s & 1 */
+        auto read_b = [&](int s, bf16x8 (&b)[STA]) {
+#pragma unroll
+            for (int st = 0; st < STA; st++) {
+                const char *pb = ((st & 1) ? xt_o : xt_e) + (s & 1) * IMG_XT + (st >> 1) * (XR * 64);
+                const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)pb);
+                const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(pb + 256));
+                const s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+                b[st] = __builtin_bit_cast(bf16x8, v);
+            }
+        };
+        /* the previous tile's chain read H2 (= the X^T stages) and H1 */
         lds_barrier();
 #pragma unroll
-        for (int s = 0; s < D && s < KS; s++) issue(s);
+        for (int s = 0; s <= D && s < KS; s++) issue(s, s - 2);
+        convert(0);
+        if (KS > 1) convert(1);
+        lds_barrier();
+        bf16x8 bb[2][STA]; /* B fragments of k-step s in bb[s & 1], read one k-step ahead */
+        read_b(0, bb[0]);
+        lds_barrier(); /* every wave's stage-0 reads are done before convert(2) refills it */
         mark(2);
-        /* ================= phase A: H1 = f(X W0^T) ================= */
+        /* ================= phase A: H1 = f(X W0^T) =================
+         * k-step s: the B reads of step s + 1 (stage (s+1) & 1, filled at step s - 1) go out
+         * before the MFMAs of step s, so their LDS latency hides behind them; then X(s + 2)
+         * is converted into stage s & 1 (its step-s reads finished before the last barrier)
+         * and one barrier publishes it and retires the step-(s+1) reads. */
 #pragma unroll
         for (int s = 0; s < KS; s++) {
-            issue(s + D);
+            issue(s + D + 1, s + D - 1);
+            if (s + 1 < KS && ABL != 4) read_b(s + 1, bb[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int st = 0; st < STA; st++) {
-                bf16x8 b;
-                if constexpr (XU8) b = u8x8_int_bf16(xr[s][st].x, xr[s][st].y);
-                else b = xr[s][st];
                 if constexpr (ABL != 3) {
-                    acc[0][st] = mfma(wr[s][0], b, acc[0][st]);
-                    acc[1][st] = mfma(wr[s][1], b, acc[1][st]);
+                    acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
+                    acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
                 } else {
-                    acc[0][st] += __builtin_bit_cast(f32x4, b) * 0.f + __builtin_bit_cast(f32x4, wr[s][0]) * 0.f;
+                    acc[0][st] += __builtin_bit_cast(f32x4, wr[s][0]) * 0.f;
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+            if (s + 2 < KS && ABL != 5) convert(s + 2);
+            lds_barrier();
         }
         mark(3);
         /* H1 tile -> LDS image [sample][neuron] */

@@ -162,9 +162,8 @@ class MLP:
         images): the network sees bf16(X * PIXEL_SCALE) (1/255; HPNN_PIXEL_SCALE overrides, 1 =
         the raw 0..255 values the reference's pmnist writes).  Layouts (BPlan.input_layout):
         the tile path ("t") takes the batch fragment-major ([Bp/32, Kp0/16, 64, 8],
-        ops.to_fragment_major, for the first-layer gradient) with a row-fragment-major copy
-        (attribute `hpnn_rfm`, ops.to_row_fragment_major, for the front); 8-bit pixels kept as
-        bytes, exact integers in the MFMAs with the scale on the accumulators; "x" takes row-major BF16 plus, for 8-bit data, a
+        ops.to_fragment_major; 8-bit pixels kept as bytes, exact integers in the MFMAs with
+        the scale on the accumulators); "x" takes row-major BF16 plus, for 8-bit data, a
         fragment-major copy of the bytes (attribute `hpnn_fm`) for the first-layer gradient;
         every other mode row-major BF16.  pixel_scale overrides PIXEL_SCALE for this batch
         (1.0: the bytes are the values, as train_nn takes integer 0..255 data)."""
@@ -182,7 +181,6 @@ class MLP:
                 ops.pack_bf16(Xd.contiguous(), src)
             out = ops.to_fragment_major(src).view(rows // 32, self.Kp[0] // 16, 64, 8)
             out.hpnn_fm_scale = ps if u8 else 1.0
-            out.hpnn_rfm = ops.to_row_fragment_major(src)  # the tile front's operand layout
             return out
         out = torch.empty(rows, self.Kp[0], dtype=torch.bfloat16, device=self.device)
         if u8:
@@ -227,11 +225,7 @@ class MLP:
                 raise ValueError(f"fragment-major batch {tuple(X.shape)} does not fit this plan "
                                  f"(mode {self.fused_mode}, Bp {self.Bp}, Kp0 {self.Kp[0]})")
             u8 = X.dtype == torch.uint8
-            Xr = getattr(X, "hpnn_rfm", None)  # the front reads it, G0 the fragment-major X
-            if self._gpu and (Xr is None or Xr.numel() != X.numel() or Xr.dtype != X.dtype):
-                raise ValueError("fragment-major batch without its row-fragment-major copy "
-                                 "(MLP.prepare_input attaches it as hpnn_rfm)")
-            return X.data_ptr(), _p(Xr), int(u8), float(getattr(X, "hpnn_fm_scale", 1.0))
+            return X.data_ptr(), 0, int(u8), float(getattr(X, "hpnn_fm_scale", 1.0))
         if self.fused_mode == "t":
             raise ValueError("the tile path takes fragment-major batches (MLP.prepare_input)")
         if X.shape[0] < self.Bp or X.shape[1] != self.Kp[0] or X.stride(0) != self.Kp[0]:

@@ -118,19 +118,6 @@ def from_fragment_major(Ag, rows, cols):
     return Ag.view(rows // 32, cols // 16, 4, 16, 8).permute(0, 2, 4, 1, 3).reshape(rows, cols)
 
 
-def to_row_fragment_major(A):
-    """[Bt, K] (batch rows) -> ROW-fragment-major [Bt/16, K/32, 64, 8]: lane l = 16 h + r of
-    fragment (u, s) holds A[16 u + r, 32 s + 8 h + j], j < 8 -- the B operand of
-    v_mfma_f32_16x16x32_bf16 with k running over the features (the tile front's X)"""
-    Bt, K = A.shape
-    return A.reshape(Bt // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(Bt // 16, K // 32, 64, 8)
-
-
-def from_row_fragment_major(Ar, rows, cols):
-    """inverse of to_row_fragment_major"""
-    return Ar.view(rows // 16, cols // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(rows, cols)
-
-
 def gemm_fm_direct(Dg, Hg, N, M, splits=1, out=None, hscale=1.0):
     """slab[s, N, M] = sum over batch slice s of D[b, n] * H[b, m] (gemm_tn) with D, H
     given fragment-major (to_fragment_major), direct-to-register loads
@@ -278,9 +265,7 @@ def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=
               n_valid=None, loss_acc=None, correct=None, xscale=1.0):
     """The n_in-128-64-(<=32) step up to delta1 with 256-sample tiles
     (csrc/gpu/kernels_mlp3t.hip): Xg fragment-major [Bp/32, K0/16, 64, 8] (to_fragment_major)
-    uint8 (exact integers, H1 = f(xscale * X W0^T)) or bf16, carrying its row-fragment-major
-    copy as attribute `hpnn_rfm` (to_row_fragment_major; the kernel's input; MLP.prepare_input
-    attaches it) -> delta1 fragment-major into D1g
+    uint8 (exact integers, H1 = f(xscale * X W0^T)) or bf16 -> delta1 fragment-major into D1g
     [Bp/32, 8, 64, 8] bf16, per-block [G1 | G2] slabs into gslab [grid, MLP3_SLAB],
     loss / hits.  W0f: fragment-major BF16 W0 (frag_major); W0 (row-major) is used by the
     CPU emulation only; W2t: W2^T [64, 32] BF16."""
@@ -295,10 +280,7 @@ def mlp3_tile(Xg, K0, W0, W0f, W1, W2, W2t, D1g, gslab, n_out, net_type, labels=
                       correct)
         D1g.view(-1).copy_(to_fragment_major(D1).view(-1))
         return D1g
-    Xr = getattr(Xg, "hpnn_rfm", None)
-    if Xr is None or Xr.numel() != Xg.numel() or Xr.dtype != Xg.dtype:
-        raise ValueError("mlp3_tile: the batch needs its row-fragment-major copy (attribute hpnn_rfm)")
-    native().mlp3_tile(Xr.data_ptr(), int(u8), float(xscale), K0, W0f.data_ptr(), W1.data_ptr(), W2.data_ptr(),
+    native().mlp3_tile(Xg.data_ptr(), int(u8), float(xscale), K0, W0f.data_ptr(), W1.data_ptr(), W2.data_ptr(),
                        W2t.data_ptr(), _ptr(labels), _ptr(T), T.stride(0) if T is not None else 0, float(t_hi),
                        float(t_lo), D1g.data_ptr(), gslab.data_ptr(), _ptr(loss_acc), _ptr(correct), Bp, n_valid,
                        n_out, net_type, gslab.shape[0], _stream())
