@@ -380,7 +380,7 @@ int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipSt
  * one split, 256 x 256 tiles, no fragment-major W0 copy to keep (HPNN_TN_UPD=0: off) */
 bool BPlan::tn_update_ok(int l) const {
     static const bool on = !env_off("HPNN_TN_UPD");
-    return on && S[l] == 1 && Np[l] % 256 == 0 && Kp[l] % 256 == 0 && Bp % 128 == 0 && !(l == 0 && W0f);
+    return on && tn_update && l >= 0 && l < L && S[l] == 1 && Np[l] % 256 == 0 && Kp[l] % 256 == 0 && Bp % 128 == 0 && !(l == 0 && W0f);
 }
 
 /* from the last layer to the first: gradient + step per layer (the deltas were all computed

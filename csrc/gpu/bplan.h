@@ -82,6 +82,7 @@ class BPlan {
     char mode = 0;
     int mid_grid = 0, mid_groups = 1, wide_ksplit = 1, slab_f = 0;
     bool g0_fused = true; /* modes t / x: G0 + reduction + every step in one launch when it applies */
+    bool tn_update = true; /* the step in the 8-phase TN gradient's epilogue where it applies */
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
 
@@ -134,6 +135,8 @@ class BPlan {
      * (two launches; the exchange then moves one copy) */
     int grads_local(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, hipStream_t s);
     int update_flat(const float *G, float lr, float alpha, float scale, hipStream_t s);
+    /* layer l's weight gradient and step run as ONE 8-phase TN launch */
+    bool tn_update_ok(int l) const;
     /* network outputs O [Bp][ldo] FP32 of a row-major BF16 batch */
     int predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s);
     /* 0, or -9 when an in-kernel hand-over (wide front partials, fused G0 splits) timed out
@@ -157,7 +160,6 @@ class BPlan {
     int grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     int g0_reduce(const XIn &x, hipStream_t s);
     int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout = nullptr);
-    bool tn_update_ok(int l) const;
     const void *fm_input(const XIn &x) const;
     void name_pointers();
 };

@@ -23,7 +23,11 @@
  *     8 KiB of pixels) is loaded once per workgroup, one 16-byte load per lane,
  *     converted in registers and written as the transposed image X^T [32 feat][256
  *     samples] into one of two LDS stages; MFMA B operands are read from it with
- *     ds_read_b64_tr_b16.  Loads run D k-steps ahead (register ring), one barrier per
+ *     ds_read_b64_tr_b16.  (Measured and not kept, round 4: every wave loading its X
+ *     fragments straight into registers from a row-fragment-major copy -- no X^T stage, no
+ *     barrier in phase A: the four neuron-group waves then pull 4x the X bytes through the
+ *     vector L1; phase A 31.2K vs 27.0K ticks, the drifted waves meeting at the H1 barrier
+ *     16.6K vs 4.7K, 76 vs 61 us per step.)  Loads run D k-steps ahead (register ring), one barrier per
  *     k-step.  The K loop is fully unrolled (K0 is a template parameter) so every ring
  *     index is static and the compiler's counted vmcnt waits stay exact.
  *  B  back chain, per wave on ITS OWN 32 samples (no workgroup barrier inside):

@@ -158,6 +158,8 @@ void bind_plan(py::module_ &m) {
              })
         .def("health", [](BPlan &p, uptr s) { return p.health(S(s)); })
         .def_readwrite("g0_fused", &BPlan::g0_fused)
+        .def_readwrite("tn_update", &BPlan::tn_update)
+        .def("tn_update_ok", &BPlan::tn_update_ok)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {
             check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
         });

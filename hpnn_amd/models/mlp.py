@@ -138,6 +138,18 @@ class MLP:
     def _gpu(self):
         return self.device.type == "cuda"
 
+    @property
+    def tn_update(self):
+        """the optimizer step in the 8-phase TN gradient's epilogue where it applies (plan)"""
+        return self.plan.tn_update
+
+    @tn_update.setter
+    def tn_update(self, on):
+        self.plan.tn_update = bool(on)
+
+    def _tn_update_ok(self, l):
+        return self.plan.tn_update_ok(int(l))
+
     @staticmethod
     def _pick_splits(N, K, Bp):
         """the plan's split-K rule (bplan.cpp BPlan::pick_splits)"""
