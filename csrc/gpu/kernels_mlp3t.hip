@@ -90,7 +90,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
-template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0>
+template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -249,13 +249,19 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         lds_barrier(); /* every wave's stage-0 reads are done before convert(2) refills it */
         mark(2);
         /* ================= phase A: H1 = f(X W0^T) =================
-         * k-step s: the B reads of step s + 1 (stage (s+1) & 1, filled at step s - 1) go out
-         * before the MFMAs of step s, so their LDS latency hides behind them; then X(s + 2)
-         * is converted into stage s & 1 (its step-s reads finished before the last barrier)
-         * and one barrier publishes it and retires the step-(s+1) reads. */
+         * k-step s: X(s + 2) is converted into stage s & 1 (its step-s reads finished before
+         * the last barrier; EARLY) and the B reads of step s + 1 (stage (s+1) & 1, filled at
+         * step s - 1) go out before the MFMAs of step s, so the LDS traffic hides behind
+         * them; one barrier publishes stage s & 1 and retires the step-(s+1) reads. */
 #pragma unroll
         for (int s = 0; s < KS; s++) {
             issue(s + D + 1, s + D - 1);
+            /* EARLY: X(s + 2) goes into stage s & 1 BEFORE the MFMAs of step s -- that stage's
+             * operands already sit in registers (read at step s - 1, retired by its barrier), so
+             * the conversion and its LDS writes overlap the MFMAs and the barrier only waits
+             * for them; otherwise after the MFMAs, in series with them */
+            if constexpr (EARLY)
+                if (s + 2 < KS && ABL != 5) convert(s + 2);
             if (s + 1 < KS && ABL != 4) read_b(s + 1, bb[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -268,7 +274,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (s + 2 < KS && ABL != 5) convert(s + 2);
+            if constexpr (!EARLY)
+                if (s + 2 < KS && ABL != 5) convert(s + 2);
             lds_barrier();
         }
         mark(3);
@@ -520,7 +527,10 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
      * 59.8-60.3 at D = 2 (B reads one k-step ahead; a deeper ring costs the registers the B
      * prefetch needs), profiles/r3/SUMMARY.md */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
-        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+        static const bool late = [] { const char *e = getenv("HPNN_TILE_EARLY"); return e && e[0] == '0'; }();
+        if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)
+                               : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+        if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
 #ifdef HPNN_ABLATIONS
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);

@@ -51,6 +51,13 @@ for s in "$@"; do
       HPNN_TN8_FUSED=0 step rruff_t0b 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
     dpforce)  # the N > 1 MNIST step path (xGMI all-reduce + update) timed with one rank on this GPU
       HPNN_DP_FORCE=1 step dpforce 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --steps 200 --warmup 20 ;;
+    earlyab)  # tile front: X(s+2) conversion before (default) / after (HPNN_TILE_EARLY=0) the MFMAs
+      step early1 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_EARLY=0 step early0 200 python bench.py --steps 200 --warmup 20 &&
+      step early1b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_EARLY=0 step early0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_TRACE=1 step trace1 200 python scripts/tile_trace.py &&
+      HPNN_TILE_EARLY=0 HPNN_TILE_TRACE=1 step trace0 200 python scripts/tile_trace.py ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
