@@ -287,7 +287,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
-                *(bf16x4 *)wr_ptr<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i) = o;
+                st_d4<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i, o, lane);
             }
         lds_barrier();
 
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     bf16x4 o;
 #pragma unroll
                     for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[st][ht][r]);
-                    *(bf16x4 *)wr_ptr<TS>(imgH2, lo, sw + 16 * st, 16 * ht) = o;
+                    st_d4<TS>(imgH2, lo, sw + 16 * st, 16 * ht, o, lane);
                 }
         }
         mark(5);
@@ -375,11 +375,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
             for (int ht = 0; ht < 4; ht++) {
                 const f32x4 a = mfma(w2tf[ht], b, f32x4{0.f, 0.f, 0.f, 0.f});
-                const bf16x4 h = *(const bf16x4 *)wr_ptr<TS>(imgH2, lo, r0, 16 * ht);
+                const bf16x4 h = ld_d4<TS>(imgH2, lo, r0, 16 * ht, lane);
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)h[r]));
-                *(bf16x4 *)wr_ptr<TS>(imgD2, lo, r0, 16 * ht) = o;
+                st_d4<TS>(imgD2, lo, r0, 16 * ht, o, lane);
             }
         }
         mark(7);

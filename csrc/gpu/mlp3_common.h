@@ -57,6 +57,40 @@ __device__ __forceinline__ char *wr_ptr(char *img, const LaneOff &lo, int r0, in
     return img + (c0 >> 5) * (R * 64) + r0 * 64 + (lo.wr ^ (((c0 >> 4) & 1) << 5));
 }
 
+/* The same 8 bytes stored / loaded without wr_ptr's 2-way bank conflicts.  A 64-bit LDS
+ * access is serviced 16 (store) or 32 (load) lanes at a time, and in wr_ptr's layout those
+ * lanes cover 8 / 16 of the 16 / 32 eight-byte bank slots: rows r and r + 4 share a slot
+ * (same 16-byte chunk, same half).  Lanes whose row has bit 2 set trade with lane l ^ 16 --
+ * same row, other 8-byte half of the same chunk (address ^ 8) -- through v_permlane16_swap,
+ * so every group covers all slots.  Both lanes of a pair trade, so each byte is still
+ * written / read once. */
+template <int R>
+__device__ __forceinline__ void st_d4(char *img, const LaneOff &lo, int r0, int c0, bf16x4 v, int lane) {
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+    const u32x2 w = __builtin_bit_cast(u32x2, v);
+    const bool trade = (lane >> 2) & 1;
+    u32x2 o;
+    o[0] = (unsigned int)shfl_xor16((int)w[0], lane);
+    o[1] = (unsigned int)shfl_xor16((int)w[1], lane);
+    char *p = wr_ptr<R>(img, lo, r0, c0);
+    /* the partner's half: bit 3 of the offset is 8 (q & 1) (everything else in wr_ptr's
+     * offset is a multiple of 16); pointer arithmetic keeps the access a ds_write */
+    const int dh = trade ? (((lane >> 4) & 1) ? -8 : 8) : 0;
+    *(u32x2 *)(p + dh) = trade ? o : w;
+}
+template <int R>
+__device__ __forceinline__ bf16x4 ld_d4(const char *img, const LaneOff &lo, int r0, int c0, int lane) {
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+    const bool trade = (lane >> 2) & 1;
+    const char *p = wr_ptr<R>((char *)img, lo, r0, c0);
+    const int dh = trade ? (((lane >> 4) & 1) ? -8 : 8) : 0;
+    const u32x2 w = *(const u32x2 *)(p + dh);
+    u32x2 o;
+    o[0] = (unsigned int)shfl_xor16((int)w[0], lane);
+    o[1] = (unsigned int)shfl_xor16((int)w[1], lane);
+    return __builtin_bit_cast(bf16x4, trade ? o : w);
+}
+
 /* Output layer for 16 samples (one wave): logits z (D[row = o 4q+r][col = sample r16],
  * NOT = 1 or 2 o-tiles of 16), targets from the label (LABELS) or dense T, writes delta3
  * (bf16) into the D3 image at rows [r0, r0+16) (zeros in an unused second o-tile),
