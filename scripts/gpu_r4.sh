@@ -61,7 +61,9 @@ for s in "$@"; do
     dpprof)  # kernel table of the N > 1 MNIST step path, one process (env rendezvous, no launcher)
       HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dpprof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 &&
       HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29534 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 ;;
+      HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_XAR_ACQ=2 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29536 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq2 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_XAR_ACQ=3 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29537 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq3 200 python bench.py --steps 200 --warmup 20 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
