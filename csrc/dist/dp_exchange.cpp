@@ -4,6 +4,8 @@
  */
 #include "dp_exchange.h"
 
+#include <stdlib.h>
+
 #include <libhpnn.h>
 #include <libhpnn/devmem.h>
 
@@ -29,9 +31,13 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
         return -2;
     }
     size_t mx = 0;
+    /* HPNN_DPX_SHARD1=1 (tests): the sharded path even on one rank (the collectives are then
+     * copies), so its kernels and ordering run on a one-GPU box */
+    const char *s1 = getenv("HPNN_DPX_SHARD1");
+    const bool one = s1 && s1[0] == '1';
     for (int l = 0; l < p_->L; l++) {
         /* rows split evenly, each rank's block whole 32-row pieces (the transposes) */
-        sharded_[l] = world_ > 1 && p_->Np[l] % world_ == 0;
+        sharded_[l] = (world_ > 1 || one) && p_->Np[l] % world_ == 0;
         if (sharded_[l]) mx = mx > (size_t)p_->Np[l] * p_->Kp[l] ? mx : (size_t)p_->Np[l] * p_->Kp[l];
     }
     if (mx && (hpnn_dev_malloc(&send16_, mx * 2) != hipSuccess ||

@@ -47,7 +47,7 @@ class DataParallel:
             raise ValueError(f"grad_comm {grad_comm!r}")
         self.grad_comm = grad_comm
         self.sharded = set()
-        if grad_comm == "bf16rs" and self.active and self.world > 1:
+        if grad_comm == "bf16rs" and self.active and (self.world > 1 or os.environ.get("HPNN_DPX_FORCE", "0") == "1"):
             if getattr(model, "W0f", None) is not None or getattr(model, "fused_mode", None) is not None:
                 raise ValueError("grad_comm='bf16rs' needs the per-layer path (fused=False)")
             self.sharded = {l for l in range(model.L) if model.Np[l] % self.world == 0}
@@ -61,7 +61,10 @@ class DataParallel:
         elif self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
             from .comm import NativeComm
             self.native = NativeComm(group, device=model.device.index)
-        if self.native is not None and self.native.h and self.world > 1:
+        # HPNN_DPX_FORCE=1 (tests): the native exchange even on one rank (with HPNN_DPX_SHARD1=1
+        # its BF16 reduce-scatter path too), so a one-GPU box runs its kernels
+        dpx_one = os.environ.get("HPNN_DPX_FORCE", "0") == "1"
+        if self.native is not None and self.native.h and (self.world > 1 or dpx_one):
             # the library's data-parallel step (csrc/dist/dp_exchange.h): per-layer exchange on
             # the communicator's side stream, overlapped with the backward; BF16 reduce-scatter
             # + sharded step + BF16 all-gather for grad_comm="bf16rs" (no per-step allocation)

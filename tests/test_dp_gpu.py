@@ -77,3 +77,46 @@ def test_native_comm_primitives_single_rank(gpu):
         c.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grad_comm", ["fp32", "bf16rs"])
+def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
+    """the library's data-parallel step (csrc/dist/dp_exchange.cpp, hpnn::DpExchange) forced
+    onto a one-rank RCCL group (HPNN_DPX_FORCE / HPNN_DPX_SHARD1): fp32 = per-layer bucket
+    all-reduce on the communicator's side stream + one update; bf16rs = per-layer BF16 cast ->
+    reduce-scatter -> row step of the FP32 masters -> in-place BF16 all-gather -> W^T rebuild.
+    Against the plain step: fp32 to summation order, bf16rs within the BF16 rounding of the
+    gradient (relative error of the weight change < 1e-2)."""
+    monkeypatch.setenv("HPNN_DPX_FORCE", "1")
+    monkeypatch.setenv("HPNN_DPX_SHARD1", "1")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        sizes, B = [300, 96, 64, 7], 2048
+        g = torch.Generator(device=dev).manual_seed(5)
+        Xr = torch.rand(B, sizes[0], device=dev, generator=g)
+        L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
+        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        w0 = [w.clone() for w in b.host_weights()]
+        dp = DataParallel(a, comm="native", grad_comm=grad_comm)
+        assert dp.dpx is not None
+        if grad_comm == "bf16rs":
+            assert dp.sharded == set(range(3))
+        Xa, Xb = a.prepare_input(Xr), b.prepare_input(Xr)
+        for _ in range(3):
+            dp.train_step(Xa, labels=L, lr=0.05, alpha=0.2)
+            b.train_step(Xb, labels=L, lr=0.05, alpha=0.2)
+        dp.gather_masters()
+        torch.cuda.synchronize()
+        for l, (wa, wb) in enumerate(zip(a.host_weights(), b.host_weights())):
+            da, db = wa - w0[l], wb - w0[l]
+            rel = ((da - db).norm() / db.norm()).item()
+            assert rel < (1e-5 if grad_comm == "fp32" else 1e-2), (l, rel)
+            # the BF16 compute copies follow the masters
+            assert torch.equal(a.Wb[l], a.W32[l].bfloat16())
+            assert torch.equal(a.Wt[l], a.W32[l].bfloat16().t().contiguous())
+        dp.check()
+    finally:
+        dist.destroy_process_group()
