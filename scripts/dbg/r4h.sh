@@ -1,2 +1,2 @@
 cd $GRAFT_REPO_ROOT
-bash scripts/gpu_r4.sh r4h "tests:tile or model or dp_exchange or dp_rccl" dpprof bench pmc trace
+bash scripts/gpu_r4.sh r4h "tests:tile or model or dp_exchange or dp_rccl" j3ab dpprof trace pmc

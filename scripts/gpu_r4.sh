@@ -64,6 +64,14 @@ for s in "$@"; do
       HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_XAR_ACQ=2 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29536 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq2 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_XAR_ACQ=3 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29537 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq3 200 python bench.py --steps 200 --warmup 20 ;;
+    j3ab)  # tile front phase A: 2 stages + B one step ahead (default) vs 3 stages, W0 3 / 4 steps ahead
+      step j3_0 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_J3=3 step j3_3 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_J3=4 step j3_4 200 python bench.py --steps 200 --warmup 20 &&
+      step j3_0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_J3=3 step j3_3b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_J3=4 step j3_4b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_J3=3 HPNN_TILE_TRACE=1 step trace_j3 200 python scripts/tile_trace.py ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
