@@ -76,6 +76,8 @@ struct TpColl {
     /* full weights for the host copy: same as all_gather, off the hot path */
     virtual bool gather_rows(const T *send, T *recv, long count, hipStream_t s) { return all_gather(send, recv, count, s); }
     virtual void abort() {}
+    /* the collectives only enqueue on the stream (no host waits): an epoch can be captured */
+    virtual bool capturable() const { return false; }
 };
 
 template <typename T>
@@ -89,6 +91,7 @@ struct RcclColl : TpColl<T> {
     bool reduce_scatter(const T *send, T *recv, long count, hipStream_t s) override {
         return hpnn_comm_reduce_scatter(c, send, recv, count, DT, HPNN_OP_SUM, s) == 0;
     }
+    bool capturable() const override { return true; }
 };
 
 /* host-thread ranks on one device: a generation barrier (abortable, so one failing rank
@@ -715,22 +718,53 @@ struct TpNetBf16 {
 };
 #undef TPK
 
-/* the epoch loop of one rank */
+/* the epoch loop of one rank; over RCCL each epoch's launches (collectives included) are
+ * captured once in a HIP graph and replayed (HPNN_GRAPH=0 or HPNN_DEBUG: eager) */
 template <class Net>
 BOOL run_rank(Net &net, UINT n, const hpnn_batched_opts *o, int B, double *ep_loss, unsigned int *ep_hits) {
     const bool mom = o->train == NN_TRAIN_BPM;
     const int n_batches = (int)((n + B - 1) / B);
-    for (UINT e = 0; e < o->epochs; e++) {
-        TPCHK(hipMemsetAsync(net.acc, 0, ACC_BYTES, net.s));
+    auto epoch = [&]() -> bool {
         for (int b = 0; b < n_batches; b++) {
             const int nv = (b == n_batches - 1) ? (int)n - b * B : B;
-            if (!net.batch_step(b, B, nv, o->lr, o->alpha, mom)) return FALSE;
+            if (!net.batch_step(b, B, nv, o->lr, o->alpha, mom)) return false;
         }
-        if (!net.read_stats(ep_loss, ep_hits)) return FALSE;
+        return true;
+    };
+    const char *ge = getenv("HPNN_GRAPH");
+    hipGraphExec_t gx = nullptr;
+    if (net.coll->capturable() && !(ge && ge[0] == '0') && !hpnn_debug_enabled() && n_batches <= 4096) {
+        hipGraph_t g = nullptr;
+        bool ok = hipStreamBeginCapture(net.s, hipStreamCaptureModeRelaxed) == hipSuccess;
+        const bool okb = ok && epoch();
+        ok = ok && hipStreamEndCapture(net.s, &g) == hipSuccess && g && okb &&
+             hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) hipGraphDestroy(g);
+        if (!ok) {
+            gx = nullptr;
+            hipGetLastError();
+            NN_DBG(stdout, "tensor-parallel rank %d: epoch not capturable, eager launches\n", net.r);
+        }
+    }
+    for (UINT e = 0; e < o->epochs; e++) {
+        TPCHK(hipMemsetAsync(net.acc, 0, ACC_BYTES, net.s));
+        if (gx) {
+            if (hipGraphLaunch(gx, net.s) != hipSuccess) {
+                hipGraphExecDestroy(gx);
+                return FALSE;
+            }
+        } else if (!epoch()) {
+            return FALSE;
+        }
+        if (!net.read_stats(ep_loss, ep_hits)) {
+            if (gx) hipGraphExecDestroy(gx);
+            return FALSE;
+        }
         if (net.r == 0 && hpnn_metrics_active())
             hpnn_metrics_epoch("gpu-tp", o->epoch0 + e + 1, *ep_loss / (double)n, *ep_hits, n, 0.0,
                                (UINT64)n * (e + 1));
     }
+    if (gx) hipGraphExecDestroy(gx);
     TPCHK(hipStreamSynchronize(net.s));
     return TRUE;
 }
@@ -892,9 +926,13 @@ BOOL train_tp(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, const hp
     const char *lb = getenv("HPNN_LOOPBACK_RANKS");
     const int lbr = lb ? atoi(lb) : 0;
     BOOL ok;
+    /* HPNN_FORCE_RCCL=1: RCCL collectives (and the epoch graphs) even for one GPU */
+    const char *fr = getenv("HPNN_FORCE_RCCL");
+    const bool rccl1 = fr && fr[0] == '1';
     if (lbr >= 2) ok = train_tp_threads<Net>(k, X, Tg, n, o, st, lbr, true);
     else if (hpnn_boot_world() > 1) ok = train_tp_mp<Net>(k, X, Tg, n, o, st);
-    else if (o->n_gpu > 1) ok = train_tp_threads<Net>(k, X, Tg, n, o, st, (int)o->n_gpu, false);
+    else if (o->n_gpu > 1 || rccl1)
+        ok = train_tp_threads<Net>(k, X, Tg, n, o, st, o->n_gpu > 1 ? (int)o->n_gpu : 1, false);
     else ok = train_tp_threads<Net>(k, X, Tg, n, o, st, 1, true);
     if (ok) hpnn_gpu_mark_host_dirty(k);
     return ok;

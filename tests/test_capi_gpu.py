@@ -221,6 +221,28 @@ def test_batched_tensor_parallel_matches_single(tmp_path, dtype, ranks, dims):
         assert rel < (1e-12 if dtype == "f64" else 1e-5), rel
 
 
+@pytest.mark.parametrize("dtype", ["f64", "bf16"])
+def test_batched_tensor_parallel_rccl_graphs(tmp_path, dtype):
+    """[parallel] tp over a real RCCL communicator (HPNN_FORCE_RCCL=1, one GPU): each epoch's
+    launches, the collectives included, are captured once in a HIP graph and replayed (eager
+    with HPNN_GRAPH=0) -- same weights either way, and the same as the loopback collectives."""
+    res = {}
+    for tag, env in (("graph", {"HPNN_FORCE_RCCL": "1"}), ("eager", {"HPNN_FORCE_RCCL": "1", "HPNN_GRAPH": "0"}),
+                     ("loopback", {})):
+        d = str(tmp_path / tag)
+        _data(os.path.join(d, "samples"), 300, 100, 7, True, seed=6)
+        formats.write_conf(os.path.join(d, "nn.conf"), name="m", type="SNN", seed=9, inputs=100, hiddens=[48, 37],
+                           outputs=7, train="BPM", sample_dir="./samples", test_dir="./samples", mode="batched",
+                           batch=128, epochs=3, lr=0.05, dtype=dtype, parallel="tp")
+        out = _run([os.path.join(BIN, "train_nn"), "-vvv", "nn.conf"], d, extra_env=env)
+        assert ("RCCL" in out) == (tag != "loopback"), out[-2000:]
+        assert "not capturable" not in out, out[-2000:]
+        res[tag] = formats.read_kernel(os.path.join(d, "kernel.opt"))["weights"]
+    for a, b, c in zip(res["graph"], res["eager"], res["loopback"]):
+        assert np.array_equal(a, b)
+        assert np.abs(a - c).max() <= (1e-12 if dtype == "f64" else 1e-6) * max(1.0, np.abs(c).max())
+
+
 @pytest.mark.parametrize("ranks,dims,batch", [(2, (100, [48, 37], 7), 128), (3, (64, [50], 9), 100),
                                                (4, (784, [128, 64], 10), 256)])
 def test_batched_tensor_parallel_bf16(tmp_path, ranks, dims, batch):
