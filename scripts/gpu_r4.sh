@@ -72,6 +72,13 @@ for s in "$@"; do
       HPNN_TILE_J3=3 step j3_3b 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_TILE_J3=4 step j3_4b 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_TILE_J3=3 HPNN_TILE_TRACE=1 step trace_j3 200 python scripts/tile_trace.py ;;
+    g0ldsab)  # first-layer gradient: direct-to-register loads (default) vs LDS-DMA staged (HPNN_G0_LDS=1)
+      step g0l_0 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_LDS=1 step g0l_1 200 python bench.py --steps 200 --warmup 20 &&
+      step g0l_0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_LDS=1 step g0l_1b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_LDS=1 HPNN_G0_FUSED=0 step g0l_1u 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_LDS=1 step rocprof_lds 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lds -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
