@@ -79,6 +79,7 @@ for s in "$@"; do
       HPNN_G0_LDS=1 step g0l_1b 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_G0_LDS=1 HPNN_G0_FUSED=0 step g0l_1u 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_G0_LDS=1 step rocprof_lds 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lds -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
+    rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
