@@ -90,6 +90,11 @@ def main():
     m = MLP(sizes, net, batch=args.batch, device=dev, momentum=True, seed=10958,
             init="reference" if args.model == "mnist" else "fast",
             splits=[int(v) for v in sp.split(",")] if sp else None)
+    if rehearse and world > 1 and hasattr(m, "plan"):
+        # ranks sharing one GPU: the fused first-layer gradient needs all its workgroups
+        # co-resident (in-kernel split-K reduction), which another rank's kernels on the same
+        # CUs can prevent -- the rehearsal takes the slab form (one GPU per rank in real runs)
+        m.plan.g0_fused = False
     dp = DataParallel(m, comm="xar" if rehearse and world > 1 else "auto",
                       grad_comm=args.grad_comm if m.fused_mode is None else "fp32")
     dp.broadcast_parameters()

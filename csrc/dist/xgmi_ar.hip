@@ -88,12 +88,9 @@ __device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world,
         }
     }
     __syncthreads();
-    if (light == 1) /* acquire: invalidate (no writeback) before reading peer data */
+    if (light) /* acquire: invalidate (no writeback) before reading peer data (agent-scope and
+                * ordering-only acquires measured no faster, profiles/r4) */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    else if (light == 2) /* agent scope: this CU's L1 only */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    else if (light == 3) /* the data lives in uncached memory no cache holds: ordering only */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     else
         __threadfence_system();
 }
@@ -325,7 +322,7 @@ struct hpnn_xar {
     bool opened[HPNN_XAR_MAX_RANKS] = {};
     unsigned long long timeout = 0;
     int mode = 0;     /* HPNN_XAR_MODE: 0 auto, 1 one-shot, 2 two-shot */
-    int light = 1;    /* HPNN_XAR_FENCE=1 -> 0: full system fences, see xbarrier; 2, 3: HPNN_XAR_ACQ */
+    int light = 1;    /* HPNN_XAR_FENCE=1 -> 0: full system fences, see xbarrier */
     int blocks = 128; /* HPNN_XAR_BLOCKS (same on every rank), <= HPNN_XAR_MAX_BLOCKS */
 };
 
@@ -355,10 +352,6 @@ extern "C" hpnn_xar *hpnn_xar_create(int rank, int world, size_t max_bytes) {
     c->mode = m ? atoi(m) : 0;
     const char *fe = getenv("HPNN_XAR_FENCE");
     c->light = !(fe && fe[0] == '1');
-    /* HPNN_XAR_ACQ (diagnostic): acquire after the barrier flags -- 1 system scope (default),
-     * 2 agent scope, 3 ordering only (the peer buffers are MTYPE UC, held by no cache) */
-    const char *aq = getenv("HPNN_XAR_ACQ");
-    if (c->light && aq && atoi(aq) >= 1 && atoi(aq) <= 3) c->light = atoi(aq);
     const char *nb = getenv("HPNN_XAR_BLOCKS");
     if (nb && atoi(nb) > 0) c->blocks = atoi(nb) < HPNN_XAR_MAX_BLOCKS ? atoi(nb) : HPNN_XAR_MAX_BLOCKS;
     c->peers.buf[rank] = (float4 *)c->buf;

@@ -20,7 +20,9 @@
  * BF16 batch; cold 26.5 us vs 34 standalone (round-2 A/B scripts, since pruned).
  * Measured (48 splits): LDS-staged TN kernel 31.2 us (its LDS-DMA
  * fill, ~27 GB/s per CU, is the bound); this kernel 23.8 us, ~5.1 TB/s of HBM reads --
- * it streams at the memory rate.  Rejected on the way: the same kernel on plain
+ * it streams at the memory rate.  Round 4, again: the same 160 x 128 tiles with the operands
+ * LDS-DMA staged (two k-steps of contiguous fragments per stage, 3-4 stages in flight, no VGPR
+ * staging) took 72.9-74.1 vs 61.3-62.0 us per MNIST step (profiles/r4).  Rejected on the way: the same kernel on plain
  * batch-contiguous (transposed row-major) operands, 51 us -- each wave load then hits
  * 16 rows x 64 B, 64 L1 tag lookups per instruction instead of 8, and the vector L1 tag
  * rate (~1 lookup per clock per CU, TCP_TOTAL_CACHE_ACCESSES) is the limit; grouping 2-4
@@ -155,156 +157,6 @@ __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nb
     }
 }
 
-/* runtime-count vmcnt wait (the count must be an immediate: one arm per value) */
-__device__ __forceinline__ void wait_vm_n(int n) {
-    switch (n) {
-#define HPNN_W(k) \
-    case k: hpnn::wait_vm<k>(); break;
-        HPNN_W(0) HPNN_W(1) HPNN_W(2) HPNN_W(3) HPNN_W(4) HPNN_W(5) HPNN_W(6) HPNN_W(7) HPNN_W(8) HPNN_W(9)
-        HPNN_W(10) HPNN_W(11) HPNN_W(12) HPNN_W(13) HPNN_W(14) HPNN_W(15)
-#undef HPNN_W
-    default: hpnn::wait_vm<0>(); break;
-    }
-}
-
-/* LDS-staged form of fm_partial for the 160 x 128 tile (WF 5, WH 4, 8 waves = two k-groups):
- * per stage the tile's operands of two consecutive k-steps -- 10 H fragments (features) and 8
- * D fragments (delta columns) each, all contiguous in the fragment-major layouts -- are copied
- * into LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no VGPR staging),
- * NST stages in flight (the direct form keeps ONE k-step in flight per wave in registers and
- * waits out most of each HBM round trip); group g computes the stage's k-step g from LDS
- * (ds_read_b64 / b128 of whole fragments: consecutive lanes, conflict-free).  One barrier per
- * stage.  On return the waves of group 0 hold the summed tile, as fm_partial. */
-template <bool HU8, int NST>
-__device__ __forceinline__ void fm_partial_lds(const __bf16 *__restrict__ Dg, int nbd, const void *__restrict__ Hg,
-                                               int nbh, int ksteps, int splits, int tiles_n, int tiles, int xcd_map,
-                                               char *lds, f32x4 (&acc)[5][4], int &tile, int &split, int &m0,
-                                               int &n0) {
-    constexpr int WF = 5, WH = 4, TMF = 160, TNH = 128;
-    constexpr int FH = HU8 ? 512 : 1024; /* bytes of one H fragment */
-    constexpr int HCH = 10 * FH / 1024;  /* 1 KiB chunks of H per k-step */
-    constexpr int CH = HCH + 8;          /* chunks per k-step */
-    constexpr int HS = CH * 1024;        /* bytes per k-step (half stage) */
-    constexpr int SS = 2 * HS;           /* bytes per stage */
-    constexpr int NCH = 2 * CH;          /* chunks per stage */
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
-    if (xcd_map) {
-        const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-        tile = j % tiles;
-        split = xcd + 8 * (j / tiles);
-    } else {
-        tile = blockIdx.x % tiles;
-        split = blockIdx.x / tiles;
-    }
-    const int mt = (tile / tiles_n) * TMF, nt = (tile % tiles_n) * TNH;
-    m0 = mt + wm * 16 * WF;
-    n0 = nt + wn * 16 * WH;
-    const int k0 = (int)((long)split * ksteps / splits), k1 = (int)((long)(split + 1) * ksteps / splits);
-    const int nk = k1 - k0, nst = (nk + 1) / 2;
-    const int my_n = (NCH - wave + 7) / 8; /* DMA instructions of this wave per stage */
-#pragma unroll
-    for (int i = 0; i < WF; i++)
-#pragma unroll
-        for (int j = 0; j < WH; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const char *hbase = (const char *)Hg + (size_t)(mt / 16) * FH + lane * 16;
-    const char *dbase = (const char *)Dg + (size_t)(nt / 16) * 1024 + lane * 16;
-    auto issue = [&](int t) {
-        char *buf = lds + (t % NST) * SS;
-        for (int c = wave; c < NCH; c += 8) {
-            const int h = c / CH, cc = c - h * CH;
-            int k = k0 + 2 * t + h;
-            k = k < k1 ? k : k1 - 1; /* past the split: re-read its last k-step (never used) */
-            const char *src = cc < HCH ? hbase + (size_t)k * nbh * FH + cc * 1024
-                                       : dbase + (size_t)k * nbd * 1024 + (cc - HCH) * 1024;
-            hpnn::glds16(src, buf + c * 1024);
-        }
-    };
-    if (nk > 0) {
-        for (int t = 0; t < NST - 1 && t < nst; t++) issue(t);
-        for (int t = 0; t < nst; t++) {
-            /* stage t landed (this wave's DMAs: the later stages may stay in flight), then every
-             * wave's: one barrier, which also retires all reads of the buffer refilled next */
-            const int later = (nst - 1 - t) < (NST - 2) ? (nst - 1 - t) : (NST - 2);
-            wait_vm_n(later * my_n);
-            hpnn::lds_barrier();
-            if (t + NST - 1 < nst) issue(t + NST - 1);
-            if (k0 + 2 * t + kg < k1) {
-                const char *buf = lds + (t % NST) * SS + kg * HS;
-                bf16x8 a[WF], b[WH];
-#pragma unroll
-                for (int i = 0; i < WF; i++) {
-                    if constexpr (HU8) {
-                        const uint2 v = *(const uint2 *)(buf + (wm * WF + i) * FH + lane * 8);
-                        a[i] = hpnn::u8x8_int_bf16(v.x, v.y);
-                    } else {
-                        a[i] = *(const bf16x8 *)(buf + (wm * WF + i) * FH + lane * 16);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < WH; j++) b[j] = *(const bf16x8 *)(buf + HCH * 1024 + (wn * WH + j) * 1024 + lane * 16);
-#pragma unroll
-                for (int i = 0; i < WF; i++)
-#pragma unroll
-                    for (int j = 0; j < WH; j++)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-            }
-        }
-    }
-    /* group 1 hands its partial tile to group 0 through the (now idle) stage memory */
-    hpnn::lds_barrier();
-    f32x4 *part = (f32x4 *)lds;
-    if (kg == 1) {
-#pragma unroll
-        for (int i = 0; i < WF; i++)
-#pragma unroll
-            for (int j = 0; j < WH; j++) part[((wave & 3) * WF * WH + i * WH + j) * 64 + lane] = acc[i][j];
-    }
-    __syncthreads();
-    if (kg == 0) {
-#pragma unroll
-        for (int i = 0; i < WF; i++)
-#pragma unroll
-            for (int j = 0; j < WH; j++) acc[i][j] += part[((wave & 3) * WF * WH + i * WH + j) * 64 + lane];
-    }
-}
-template <bool HU8>
-constexpr int g0_lds_nst() { return HU8 ? 4 : 3; }
-template <bool HU8>
-constexpr int g0_lds_bytes() { return g0_lds_nst<HU8>() * 2 * ((10 * (HU8 ? 512 : 1024) / 1024) + 8) * 1024; }
-
-/* the slab-writing G0 (gemm_fm_direct_kernel's contract) on fm_partial_lds */
-template <bool HU8>
-__global__ __launch_bounds__(512) void gemm_fm_lds_kernel(const __bf16 *__restrict__ Dg, int nbd,
-                                                          const void *__restrict__ Hg, int nbh, float hscale,
-                                                          float *__restrict__ slab, int ldg, int N, int ksteps,
-                                                          int splits, int tiles_n, int tiles, int xcd_map,
-                                                          TnTail tail) {
-    extern __shared__ __attribute__((aligned(16))) char dyn_lds[];
-    if ((int)blockIdx.x >= tiles * splits) {
-        if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - tiles * splits);
-        return;
-    }
-    f32x4 acc[5][4];
-    int tile, split, m0, n0;
-    fm_partial_lds<HU8, g0_lds_nst<HU8>()>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, dyn_lds, acc,
-                                           tile, split, m0, n0);
-    if ((threadIdx.x >> 6) >= 4) return;
-    const int lane = threadIdx.x & 63, r16 = lane & 15, q = lane >> 4;
-    float *out = slab + (size_t)split * N * ldg;
-#pragma unroll
-    for (int i = 0; i < 5; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) = HU8 ? acc[i][j] * hscale : acc[i][j];
-}
-
-bool g0_lds_on() {
-    static const bool on = [] { const char *e = getenv("HPNN_G0_LDS"); return e && e[0] == '1'; }();
-    return on;
-}
-
 template <int WF, int WH, int PD, int KW, bool HU8 = false>
 __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                                   const void *__restrict__ Hg, int nbh, float hscale,
@@ -430,7 +282,7 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
     }
 }
 
-template <int WF, int WH, int PD, int KW, bool HU8, bool LDSV = false>
+template <int WF, int WH, int PD, int KW, bool HU8>
 __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                             const void *__restrict__ Hg, int nbh, float hscale,
                                                             float *__restrict__ slab, int ldg, int N, int ksteps,
@@ -440,14 +292,8 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     __shared__ f32x4 red[NT];
     f32x4 acc[WF][WH];
     int tile, split, m0, n0;
-    if constexpr (LDSV) {
-        extern __shared__ __attribute__((aligned(16))) char dyn_lds[];
-        fm_partial_lds<HU8, g0_lds_nst<HU8>()>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, dyn_lds,
-                                               acc, tile, split, m0, n0);
-    } else {
-        fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split,
-                                        m0, n0);
-    }
+    fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
+                                    n0);
     const int t = threadIdx.x, lane = t & 63;
     /* publish this split's partial tile (write-through), then one ticket for the workgroup */
     if ((t >> 6) < 4) {
@@ -547,22 +393,6 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
 #define HPNN_FM(...)                                                                                              \
     return h_u8 ? launch_fm<__VA_ARGS__, true>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)                  \
                 : launch_fm<__VA_ARGS__, false>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)
-    if (M % 160 == 0 && N % 128 == 0 && g0_lds_on()) {
-        const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
-        const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-        auto go = [&](auto kern, int bytes) {
-            static bool attr = false;
-            if (!attr) {
-                (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-                attr = true;
-            }
-            hipLaunchKernelGGL(kern, dim3(tiles * splits + t.blocks), dim3(512), bytes, s, (const __bf16 *)Dg, N / 16,
-                               Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, xcd_map, t);
-            return hipGetLastError() == hipSuccess ? 0 : -5;
-        };
-        if (h_u8) return go(gemm_fm_lds_kernel<true>, g0_lds_bytes<true>());
-        return go(gemm_fm_lds_kernel<false>, g0_lds_bytes<false>());
-    }
     if (M % 160 == 0 && N % 128 == 0) {
         /* 8-bit H: 8 waves (two k-interleaved groups) hide the byte -> bf16 conversion
          * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves.
@@ -600,28 +430,9 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_>), dim3(tiles * splits), dim3(512), 0, stream,              \
                        (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
                        xcd_map, uu)
-#define HPNN_G0FL(U8_)                                                                                             \
-    do {                                                                                                           \
-        static bool attr_ = false;                                                                                 \
-        if (!attr_) {                                                                                              \
-            (void)hipFuncSetAttribute((const void *)g0_fused_kernel<5, 4, 1, 2, U8_, true>,                        \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, g0_lds_bytes<U8_>());            \
-            attr_ = true;                                                                                          \
-        }                                                                                                          \
-        hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_, true>), dim3(tiles * splits), dim3(512),              \
-                           g0_lds_bytes<U8_>(), stream, (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, \
-                           Bt / 32, splits, tiles_n, tiles, xcd_map, uu);                                          \
-    } while (0)
-    if (g0_lds_on()) {
-        if (h_u8) HPNN_G0FL(true);
-        else HPNN_G0FL(false);
-    } else if (h_u8) {
-        HPNN_G0F(true);
-    } else {
-        HPNN_G0F(false);
-    }
+    if (h_u8) HPNN_G0F(true);
+    else HPNN_G0F(false);
 #undef HPNN_G0F
-#undef HPNN_G0FL
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -27,8 +27,10 @@
  *     fragments straight into registers from a row-fragment-major copy -- no X^T stage, no
  *     barrier in phase A: the four neuron-group waves then pull 4x the X bytes through the
  *     vector L1; phase A 31.2K vs 27.0K ticks, the drifted waves meeting at the H1 barrier
- *     16.6K vs 4.7K, 76 vs 61 us per step.)  Loads run D k-steps ahead (register ring), one barrier per
- *     k-step.  The K loop is fully unrolled (K0 is a template parameter) so every ring
+ *     16.6K vs 4.7K, 76 vs 61 us per step.  Also measured: three X^T stages with the B
+ *     fragments read just before their MFMAs and W0 loads 3 / 4 k-steps ahead, 62.0-62.1 /
+ *     61.5-61.6 vs 61.4-61.6 us same box.)  Loads run D k-steps ahead (register ring), one
+ *     barrier per k-step.  The K loop is fully unrolled (K0 is a template parameter) so every ring
  *     index is static and the compiler's counted vmcnt waits stay exact.
  *  B  back chain, per wave on ITS OWN 32 samples (no workgroup barrier inside):
  *     H2 = f(H1 W1^T), logits, softmax / sigmoid + loss + delta3 + argmax,
@@ -76,7 +78,6 @@ constexpr int OFF_W1 = OFF_D3 + TS * NO * 2;
 constexpr int LDS_TOTAL = OFF_W1 + IMG_W1;
 static_assert(TS * H2 * 2 <= 2 * IMG_XT, "H2 aliases the X^T stages");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
-static_assert(TS * NO * 2 >= IMG_XT, "a third X^T stage fits the delta3 image");
 
 /* within-wave ordering of LDS writes before other lanes' reads (one wave's LDS
  * instructions execute in order; this keeps the compiler from moving them) */
@@ -91,8 +92,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
-template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool J3 = false, int WA = 2>
+template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -208,13 +208,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                                                       : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
             }
         };
-        /* X^T stage of k-step s, as an offset from OFF_XT: stages 0, 1 in the X^T region; J3's
-         * third stage in the delta3 image (dead in phase A: written by the chain, read by phase
-         * C, both after phase A, and the previous tile is past the tile-start barrier) */
-        auto soff = [](int s) {
-            const int st = J3 ? s % 3 : (s & 1);
-            return st < 2 ? st * IMG_XT : OFF_D3 - OFF_XT;
-        };
+        auto soff = [](int s) { return (s & 1) * IMG_XT; }; /* X^T stage of k-step s */
         auto convert = [&](int s) {
             char *img = lds + OFF_XT + soff(s);
             bf16x8 v[2];
@@ -248,39 +242,6 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         };
         /* the previous tile's chain read H2 (= the X^T stages) and H1 */
         lds_barrier();
-        if constexpr (J3) {
-            /* three stages: step s reads its B fragments from stage s % 3 just before its
-             * MFMAs and converts X(s + 2) into stage (s + 2) % 3 (last read at step s - 1, before
-             * that step's barrier): one B register set instead of two, spent on W0 loads WA
-             * k-steps ahead (L2 hits under phase A's streaming take ~2-3K clocks) */
-#pragma unroll
-            for (int t = 0; t <= D && t < KS; t++) issue(t, -1);
-#pragma unroll
-            for (int t = 0; t < WA && t < KS; t++) issue(KS, t);
-            convert(0);
-            if (KS > 1) convert(1);
-            lds_barrier();
-            mark(2);
-            bf16x8 bb[STA];
-#pragma unroll
-            for (int s = 0; s < KS; s++) {
-                issue(s + D + 1, s + WA);
-                if (ABL != 4) read_b(s, bb);
-                if (s + 2 < KS && ABL != 5) convert(s + 2);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int st = 0; st < STA; st++) {
-                    if constexpr (ABL != 3) {
-                        acc[0][st] = mfma(wr[s][0], bb[st], acc[0][st]);
-                        acc[1][st] = mfma(wr[s][1], bb[st], acc[1][st]);
-                    } else {
-                        acc[0][st] += __builtin_bit_cast(f32x4, wr[s][0]) * 0.f;
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                lds_barrier();
-            }
-        } else {
 #pragma unroll
         for (int s = 0; s <= D && s < KS; s++) issue(s, s - 2);
         convert(0);
@@ -319,7 +280,6 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             if constexpr (!EARLY)
                 if (s + 2 < KS && ABL != 5) convert(s + 2);
             lds_barrier();
-        }
         }
         mark(3);
         /* H1 tile -> LDS image [sample][neuron] */
@@ -574,10 +534,6 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
         if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)
                                : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
-        /* HPNN_TILE_J3 = 3 / 4: three X^T stages, W0 loads 3 / 4 k-steps ahead (A/B) */
-        static const int j3 = [] { const char *e = getenv("HPNN_TILE_J3"); return e ? atoi(e) : 0; }();
-        if (j3 == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true, 3>, 512);
-        if (j3 == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true, 4>, 512);
 #ifdef HPNN_ABLATIONS
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);

@@ -59,26 +59,9 @@ for s in "$@"; do
       HPNN_TILE_TRACE=1 step trace1 200 python scripts/tile_trace.py &&
       HPNN_TILE_EARLY=0 HPNN_TILE_TRACE=1 step trace0 200 python scripts/tile_trace.py ;;
     dpprof)  # kernel table of the N > 1 MNIST step path, one process (env rendezvous, no launcher)
-      HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dpprof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 &&
-      HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29534 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_XAR_ACQ=2 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29536 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq2 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_XAR_ACQ=3 HPNN_DP_FORCE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29537 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_acq3 200 python bench.py --steps 200 --warmup 20 ;;
-    j3ab)  # tile front phase A: 2 stages + B one step ahead (default) vs 3 stages, W0 3 / 4 steps ahead
-      step j3_0 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_TILE_J3=3 step j3_3 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_TILE_J3=4 step j3_4 200 python bench.py --steps 200 --warmup 20 &&
-      step j3_0b 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_TILE_J3=3 step j3_3b 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_TILE_J3=4 step j3_4b 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_TILE_J3=3 HPNN_TILE_TRACE=1 step trace_j3 200 python scripts/tile_trace.py ;;
-    g0ldsab)  # first-layer gradient: direct-to-register loads (default) vs LDS-DMA staged (HPNN_G0_LDS=1)
-      step g0l_0 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_G0_LDS=1 step g0l_1 200 python bench.py --steps 200 --warmup 20 &&
-      step g0l_0b 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_G0_LDS=1 step g0l_1b 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_G0_LDS=1 HPNN_G0_FUSED=0 step g0l_1u 200 python bench.py --steps 200 --warmup 20 &&
-      HPNN_G0_LDS=1 step rocprof_lds 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lds -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
+      HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dpprof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 &&
+      HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29534 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
