@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <libhpnn.h>
 #include <libhpnn/xar.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -46,6 +47,8 @@ struct Signal {
     unsigned int flag[2][HPNN_XAR_MAX_BLOCKS][HPNN_XAR_MAX_RANKS]; /* barriers A, B */
     unsigned int error;
 };
+
+static_assert(sizeof(unsigned int) * HPNN_XAR_ERROR_WORD == offsetof(Signal, error), "xar.h signal layout");
 
 struct XarPeers {
     float4 *buf[HPNN_XAR_MAX_RANKS];
@@ -68,10 +71,11 @@ __device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world,
      * back every dirty L2 line of the XCD (buffer_wbl2) -- measured 18.6 -> 8.5 us per
      * 437 KB call at world 1 and 36.6 -> 12.5 us at world 2 (scripts/xar_bench.py);
      * HPNN_XAR_FENCE=1 restores the full fence */
-    if (light)
+    if (light == 1)
         __builtin_amdgcn_s_waitcnt(0);
-    else
+    else if (!light)
         __threadfence_system();
+    /* light == 2: the data was stored by an earlier kernel (in-place call), nothing to order */
     __syncthreads();
     const int t = threadIdx.x;
     if (t < world) {
@@ -187,17 +191,34 @@ struct XarUpd {
 };
 
 /* float4 i of the reduced gradient = 4 consecutive k of one row n of one layer: the
- * step of sgd_tile (kernels_misc.hip) on those 4 weights */
-__device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g) {
+ * step of sgd_tile (kernels_misc.hip) on those 4 weights.  The master weights and momenta
+ * (local, independent of the peers) can be loaded before the barrier: XarPre */
+struct XarPre {
+    float4 w, v;
+};
+__device__ __forceinline__ int xar_layer(const XarUpd &u, long i, long &e) {
     int l = 0;
     while (l + 1 < u.nl && i >= u.end4[l]) l++;
-    const long e = (i - (l ? u.end4[l - 1] : 0)) * 4;
+    e = (i - (l ? u.end4[l - 1] : 0)) * 4;
+    return l;
+}
+__device__ __forceinline__ XarPre xar_pre(const XarUpd &u, long i) {
+    long e;
+    const int l = xar_layer(u, i, e);
+    XarPre p;
+    p.w = *(const float4 *)(u.W32[l] + e);
+    p.v = u.momentum ? *(const float4 *)(u.V32[l] + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return p;
+}
+__device__ __forceinline__ void xar_update4(const XarUpd &u, long i, float4 g, const XarPre *pre = nullptr) {
+    long e;
+    const int l = xar_layer(u, i, e);
     const int K = u.K[l], N = u.N[l];
     const int n = (int)(e / K), k = (int)(e % K);
-    float4 w = *(const float4 *)(u.W32[l] + e);
+    float4 w = pre ? pre->w : *(const float4 *)(u.W32[l] + e);
     float gv[4] = {g.x, g.y, g.z, g.w}, wv[4] = {w.x, w.y, w.z, w.w};
     if (u.momentum) {
-        float4 v = *(const float4 *)(u.V32[l] + e);
+        float4 v = pre ? pre->v : *(const float4 *)(u.V32[l] + e);
         float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -249,12 +270,17 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
     if constexpr (!TWO) {
         const long per = (n4 + gridDim.x - 1) / gridDim.x;
         const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
-        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
-        xbarrier(P, rank, world, b, e, 0, timeout, light);
-        for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        if (in.nseg) /* else in place: an earlier kernel wrote this call's data half */
+            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
+        const long i0 = lo + threadIdx.x;
+        XarPre pre = {};
+        if constexpr (UPD)
+            if (i0 < hi) pre = xar_pre(upd, i0); /* in flight while the barrier waits */
+        xbarrier(P, rank, world, b, e, 0, timeout, in.nseg ? light : (light ? 2 : 0));
+        for (long i = i0; i < hi; i += blockDim.x) {
             const float4 v = sum_peers(P, half4, world, i);
             out[i] = v;
-            if constexpr (UPD) xar_update4(upd, i, v);
+            if constexpr (UPD) xar_update4(upd, i, v, i == i0 ? &pre : nullptr);
         }
     } else {
         const long sh = (n4 + world - 1) / world;
@@ -265,11 +291,12 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
             hi = lo + per < s_end ? lo + per : s_end;
         };
         long lo, hi;
-        for (int s = 0; s < world; s++) {
-            range(s, lo, hi);
-            for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
-        }
-        xbarrier(P, rank, world, b, e, 0, timeout, light);
+        if (in.nseg)
+            for (int s = 0; s < world; s++) {
+                range(s, lo, hi);
+                for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = xar_load_in(in, i);
+            }
+        xbarrier(P, rank, world, b, e, 0, timeout, in.nseg ? light : (light ? 2 : 0));
         range(rank, lo, hi);
         for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
             const float4 v = sum_peers(P, half4, world, i);
@@ -459,24 +486,10 @@ extern "C" int hpnn_xar_all_reduce_slabs_f32(hpnn_xar *c, const hpnn_xar_seg *se
     return xar_launch(c, x, out, tot, stream);
 }
 
-extern "C" int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
-                                                    const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha,
-                                                    float scale, int momentum, hipStream_t stream) {
-    if (!segs || nseg < 1 || nseg > HPNN_XAR_MAX_SEGS || !layers || nl < 1 || nl > HPNN_XAR_MAX_LAYERS) return -1;
-    XarIn x = {};
-    long tot = 0;
-    for (int j = 0; j < nseg; j++) {
-        const hpnn_xar_seg &g = segs[j];
-        if (!g.src || g.S < 1 || g.count <= 0 || (g.count & 3) || (g.stride & 3) || ((uintptr_t)g.src & 15))
-            return -1;
-        x.src[j] = (const float4 *)g.src;
-        x.stride4[j] = g.stride / 4;
-        x.S[j] = g.S;
-        tot += g.count;
-        x.end4[j] = tot / 4;
-    }
-    x.nseg = nseg;
-    XarUpd u = {};
+static int xar_upd_args(const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha, float scale, int momentum,
+                        long tot, XarUpd &u) {
+    if (!layers || nl < 1 || nl > HPNN_XAR_MAX_LAYERS) return -1;
+    u = {};
     long lt = 0;
     for (int l = 0; l < nl; l++) {
         const hpnn_xar_upd_layer &L = layers[l];
@@ -501,6 +514,63 @@ extern "C" int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_
     u.alpha = alpha;
     u.scale = scale;
     u.momentum = momentum;
+    return 0;
+}
+
+extern "C" int hpnn_xar_local(hpnn_xar *c, float **buf, long *half, const unsigned int **sel) {
+    if (!c || !buf || !half || !sel) return -1;
+    *buf = (float *)c->buf;
+    *half = (long)(c->max_bytes / 4);
+    *sel = c->ep; /* every workgroup's epoch is the same after each call: word 0 stands for all */
+    return 0;
+}
+
+extern "C" int hpnn_xar_view_get(hpnn_xar *c, hpnn_xar_view *v) {
+    if (!c || !v) return -1;
+    memset(v, 0, sizeof *v);
+    for (int p = 0; p < c->world; p++) {
+        if (!c->peers.buf[p]) return -3; /* not opened */
+        v->buf[p] = (float *)c->peers.buf[p];
+        v->sig[p] = (unsigned int *)c->peers.sig[p];
+    }
+    v->half = (long)(c->max_bytes / 4);
+    v->ep = c->ep;
+    v->rank = c->rank;
+    v->world = c->world;
+    v->timeout = c->timeout;
+    return 0;
+}
+
+extern "C" int hpnn_xar_reduce_local_update_f32(hpnn_xar *c, long count, float *out, const hpnn_xar_upd_layer *layers,
+                                                int nl, float lr, float alpha, float scale, int momentum,
+                                                hipStream_t stream) {
+    XarUpd u;
+    int r;
+    if ((r = xar_upd_args(layers, nl, lr, alpha, scale, momentum, count, u))) return r;
+    XarIn x = {}; /* nseg = 0: in place */
+    return xar_launch(c, x, out, count, stream, &u);
+}
+
+extern "C" int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
+                                                    const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha,
+                                                    float scale, int momentum, hipStream_t stream) {
+    if (!segs || nseg < 1 || nseg > HPNN_XAR_MAX_SEGS || !layers || nl < 1 || nl > HPNN_XAR_MAX_LAYERS) return -1;
+    XarIn x = {};
+    long tot = 0;
+    for (int j = 0; j < nseg; j++) {
+        const hpnn_xar_seg &g = segs[j];
+        if (!g.src || g.S < 1 || g.count <= 0 || (g.count & 3) || (g.stride & 3) || ((uintptr_t)g.src & 15))
+            return -1;
+        x.src[j] = (const float4 *)g.src;
+        x.stride4[j] = g.stride / 4;
+        x.S[j] = g.S;
+        tot += g.count;
+        x.end4[j] = tot / 4;
+    }
+    x.nseg = nseg;
+    XarUpd u;
+    int r;
+    if ((r = xar_upd_args(layers, nl, lr, alpha, scale, momentum, tot, u))) return r;
     return xar_launch(c, x, out, tot, stream, &u);
 }
 

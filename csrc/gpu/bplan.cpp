@@ -358,12 +358,15 @@ int BPlan::g0_reduce(const XIn &x, hipStream_t s) {
 
 /* G0 + its split-K reduction + every layer's step in ONE launch (kernels_g0.hip); -1 when
  * the shape or the input is not covered (the caller then runs G0 + the update launch) */
-int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout) {
+int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout,
+                         const unsigned int *gsel, long galt, const hpnn_xar_view *xv) {
     const void *fm = fm_input(x);
     if (!fm || !g0cnt || !g0_fused) return -1;
     hpnn_g0_update u;
     memset(&u, 0, sizeof u);
     u.gout = gout;
+    u.gsel = gsel, u.galt = galt;
+    if (xv) u.xchg = 1, u.xv = *xv;
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
     u.cnt = g0cnt, u.err = g0cnt + 224;
     u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;
@@ -510,12 +513,28 @@ int BPlan::grads_local(const XIn &x, const int *labels, const float *T, int ldt,
     return hpnn_reduce_slabs(midtmp, mid_groups, slab_f, slab_f, gflat + goff[1], s);
 }
 
+int BPlan::xchg_step(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, float lr, float alpha,
+                     float scale, const hpnn_xar_view &xv, hipStream_t s) {
+    if (mode != 't' && mode != 'x' && mode != 'm') return -1;
+    if (!fm_input(x) || !g0cnt || !g0_fused || !hpnn_gemm_fm_direct_update_ok(Kp[0], Np[0], Kp[0], Bp, S[0]) ||
+        S[0] * ((Kp[0] / 160) * (Np[0] / 128)) > HPNN_XAR_MAX_BLOCKS || (long)goff[L] > xv.half)
+        return -1;
+    int r;
+    if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
+    r = g0_fused_step(x, lr, alpha, scale, s, nullptr, nullptr, 0, &xv);
+    return r == -1 ? -9 : r; /* covered above: a refusal now is an error, not a fallback */
+}
+
 int BPlan::grads_slabs(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, SlabSegs *segs,
-                       hipStream_t s) {
+                       hipStream_t s, float *dst, const unsigned int *sel, long alt) {
     if (mode != 't' && mode != 'x' && mode != 'm') return -1;
     int r;
     if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
-    if (g0_fused_step(x, 0.f, 0.f, 0.f, s, gflat) == 0) {
+    if (dst && g0_fused_step(x, 0.f, 0.f, 0.f, s, dst, sel, alt) == 0) {
+        segs->count = 0; /* already in the all-reduce's buffer */
+        return 0;
+    }
+    if (!dst && g0_fused_step(x, 0.f, 0.f, 0.f, s, gflat) == 0) {
         /* G0 and [G1 | G2] reduced in the G0 launch: the exchange moves ONE copy */
         segs->count = 1;
         segs->base[0] = gflat;

@@ -127,13 +127,21 @@ class BPlan {
     std::vector<std::pair<int, int>> buckets() const;
     /* fused modes: front + G0 with the gradient left in slabs (the xGMI all-reduce's copy-in
      * sums them); segs[0] = G0 slabs, segs[1] = [G1|G2] groups -- or, when the G0 launch
-     * reduces in-kernel, ONE segment: gflat itself, fully reduced */
+     * reduces in-kernel, ONE segment: gflat itself, fully reduced.  dst (with sel / alt, see
+     * hpnn_g0_update.gsel): the in-kernel reduced gradient goes there instead (the xGMI
+     * all-reduce's own buffer half) and segs->count = 0 */
     int grads_slabs(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, SlabSegs *segs,
-                    hipStream_t s);
+                    hipStream_t s, float *dst = nullptr, const unsigned int *sel = nullptr, long alt = 0);
     /* fused modes: front + every layer's gradient summed over this replica's samples into
      * gflat, with G0's split-K and [G1|G2] reductions inside the G0 launch when it applies
      * (two launches; the exchange then moves one copy) */
     int grads_local(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, hipStream_t s);
+    /* fused modes, data parallel: front, then G0 with its split-K reduction, the exchange over
+     * xv (one-shot xGMI protocol inside the launch, kernels_g0.hip) and every layer's step --
+     * the single-GPU step's two launches; scale includes 1 / world.  -1 (nothing launched)
+     * when the fused G0 does not cover the shape or the input. */
+    int xchg_step(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, float lr, float alpha,
+                  float scale, const hpnn_xar_view &xv, hipStream_t s);
     int update_flat(const float *G, float lr, float alpha, float scale, hipStream_t s);
     /* layer l's weight gradient and step run as ONE 8-phase TN launch */
     bool tn_update_ok(int l) const;
@@ -159,7 +167,8 @@ class BPlan {
     bool owns_ = false;
     int grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     int g0_reduce(const XIn &x, hipStream_t s);
-    int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout = nullptr);
+    int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout = nullptr,
+                      const unsigned int *gsel = nullptr, long galt = 0, const hpnn_xar_view *xv = nullptr);
     const void *fm_input(const XIn &x) const;
     void name_pointers();
 };

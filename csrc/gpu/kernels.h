@@ -15,6 +15,7 @@
 #ifndef HPNN_GPU_KERNELS_H
 #define HPNN_GPU_KERNELS_H
 #include <hip/hip_runtime_api.h>
+#include <libhpnn/xar.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -112,11 +113,24 @@ typedef struct {
     /* non-NULL: no step -- the fully reduced gradients are stored instead, G0 [N][M] at gout,
      * [G1 | G2] right after it (the flat layout of the plan's gradient buffer; data parallel) */
     float *gout;
+    /* non-NULL (with gout): gout + galt instead of gout when *gsel is even -- gout is then the
+     * xGMI all-reduce's own data buffer and *gsel its epoch word, so the gradient lands in the
+     * half the next call reads (hpnn_xar_local) and that call needs no copy-in */
+    const unsigned int *gsel;
+    long galt;
+    /* xchg != 0: data parallel with the exchange in this launch -- each workgroup writes its
+     * reduced G0 / [G1 | G2] elements into its half of xv's buffer, runs the one-shot flag
+     * barrier of workgroup b with every peer (include/libhpnn/xar.h hpnn_xar_view), sums the
+     * peers' copies in rank order and steps those elements (scale includes 1 / world) */
+    int xchg;
+    hpnn_xar_view xv;
     int proto; /* hand-off diagnostics (HPNN_G0_PROTO): 1 producer agent release, 2 consumer agent
                 * acquire, 4 system-scope (sc0 sc1) partial loads */
 } hpnn_g0_update;
 int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
                                int M, int Bt, int splits, const hpnn_g0_update *u, hipStream_t stream);
+/* 1 when hpnn_gemm_fm_direct_update covers the shape (launch-free check) */
+int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)

@@ -282,6 +282,67 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
     }
 }
 
+/* sum of float4 at offset o over the first `world` ranks' buffers, rank order (identical bits
+ * on every rank); every load in flight before the adds */
+__device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
+    f32x4 x[HPNN_XAR_MAX_RANKS];
+#pragma unroll
+    for (int p = 0; p < HPNN_XAR_MAX_RANKS; p++)
+        if (p < v.world) x[p] = *(const f32x4 *)(v.buf[p] + o);
+    f32x4 a = x[0];
+#pragma unroll
+    for (int p = 1; p < HPNN_XAR_MAX_RANKS; p++)
+        if (p < v.world) a += x[p];
+    return a;
+}
+
+/* data-parallel tail (u.xchg): this workgroup's reduced G0 share (float4 [e0, e1) of its
+ * tile) and [G1 | G2] share sit in its half of this rank's exchange buffer (fine-grained,
+ * uncached: no cache maintenance between ranks).  One-shot barrier of workgroup b (the
+ * protocol of xgmi_ar.hip, release = waiting for the store acknowledgements), then the
+ * rank-order sums over the peers' copies of exactly those elements and their steps: the
+ * exchange and the update need no launch of their own. */
+template <int NT>
+__device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsigned int e, int N, int ldg, int e0, int e1,
+                                              int nt0, int mt0, int TMF) {
+    const hpnn_xar_view &v = u.xv;
+    const int t = threadIdx.x, b = blockIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const long hoff = (e & 1) ? v.half : 0;
+    if (t < v.world) {
+        __hip_atomic_store(HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned int *f = HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > v.timeout) {
+                __hip_atomic_store(v.sig[v.rank] + HPNN_XAR_ERROR_WORD, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* invalidate, no writeback */
+    for (int c = e0 + t; c < e1; c += NT) {
+        const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
+        const f32x4 g = xsum_peers(v, hoff + (long)(nt0 + row) * ldg + col);
+        step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
+    }
+    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = b * nf / nb, c1 = (b + 1) * nf / nb;
+    const long n1 = (long)u.Nb[0] * u.Kb[0];
+    for (long e4 = c0 + t; e4 < c1; e4 += NT) {
+        const f32x4 g = xsum_peers(v, hoff + (long)N * ldg + e4 * 4);
+        long i = e4 * 4;
+        const int l = i < n1 ? 0 : 1;
+        if (l) i -= n1;
+        const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+        step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,
+                   u);
+    }
+}
+
 template <int WF, int WH, int PD, int KW, bool HU8>
 __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                             const void *__restrict__ Hg, int nbh, float hscale,
@@ -295,6 +356,20 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
                                     n0);
     const int t = threadIdx.x, lane = t & 63;
+    /* where the reduced gradient goes instead of a step: the plan's buffer, the xGMI
+     * all-reduce's next half (gsel), or -- exchanging here -- this workgroup's epoch's half of
+     * this rank's exchange buffer */
+    __shared__ unsigned int xe_s;
+    float *gout = u.gout && u.gsel && !(*u.gsel & 1) ? u.gout + u.galt : u.gout;
+    if (u.xchg) {
+        if (t == 0) {
+            const unsigned int e = u.xv.ep[blockIdx.x] + 1; /* only this workgroup touches it */
+            u.xv.ep[blockIdx.x] = e;
+            xe_s = e;
+        }
+        __syncthreads();
+        gout = u.xv.buf[u.xv.rank] + ((xe_s & 1) ? u.xv.half : 0);
+    }
     /* publish this split's partial tile (write-through), then one ticket for the workgroup */
     if ((t >> 6) < 4) {
         const int r16 = lane & 15, q = lane >> 4;
@@ -319,7 +394,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
     {
         const long nb = (long)tiles * splits, nf = u.n12 / 4, b = blockIdx.x;
-        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red, u.gout ? u.gout + (size_t)N * ldg : nullptr);
+        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red, gout ? gout + (size_t)N * ldg : nullptr);
     }
     if (t == 0) {
         unsigned int *cnt = u.cnt + 32 * tile;
@@ -362,13 +437,14 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
             f32x4 g = red[f];
 #pragma unroll
             for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
-            if (u.gout)
-                *(f32x4 *)(u.gout + (size_t)(nt0 + row) * ldg + col) = g;
+            if (gout)
+                *(f32x4 *)(gout + (size_t)(nt0 + row) * ldg + col) = g;
             else
                 step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
         }
         __syncthreads();
     }
+    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF);
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false>
@@ -417,11 +493,19 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     /* the 160 x 128 tile configuration of fm_dispatch (8 waves) */
     if (!on || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
     if (!u->cnt || !u->err) return -1;
-    if (u->n12 % 4 || !u->mslab || u->mrows < 1 ||
-        (!u->gout && u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
+    const bool steps = !u->gout || u->xchg;
+    if (u->n12 % 4 || !u->mslab || u->mrows < 1 || (steps && u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
         return -2;
     const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
     if (tiles > 7) return -1; /* counters 32 words apart in a 256-word block, err at word 224 */
+    if (u->xchg) {
+        /* the exchange buffer holds [G0 | G1 | G2]; one epoch / flag slot per workgroup */
+        if (tiles * splits > HPNN_XAR_MAX_BLOCKS || u->xv.world < 1 || u->xv.world > HPNN_XAR_MAX_RANKS ||
+            !u->xv.ep || (long)N * ldg + u->n12 > u->xv.half)
+            return -1;
+        for (int p = 0; p < u->xv.world; p++)
+            if (!u->xv.buf[p] || !u->xv.sig[p]) return -1;
+    }
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
     static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
     hpnn_g0_update uu = *u;
@@ -434,6 +518,12 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     else HPNN_G0F(false);
 #undef HPNN_G0F
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits) {
+    static const bool on = [] { const char *e = getenv("HPNN_G0_FUSED"); return !(e && e[0] == '0'); }();
+    return on && M % 160 == 0 && N % 128 == 0 && Bt % 32 == 0 && splits >= 1 && splits <= Bt / 32 && ldg == M &&
+           (M / 160) * (N / 128) <= 7;
 }
 
 extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,

@@ -142,15 +142,26 @@ void bind_plan(py::module_ &m) {
                        "BPlan.grads");
              })
         .def("grads_slabs",
-             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, uptr s) {
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, uptr s,
+                uptr dst, uptr sel, long alt) {
                  hpnn::SlabSegs g;
                  check(p.grads_slabs(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt, n_valid,
-                                     &g, S(s)),
+                                     &g, S(s), (float *)P(dst), (const unsigned int *)P(sel), alt),
                        "BPlan.grads_slabs");
                  py::list out; /* (address, slab stride, slabs, floats) per segment */
                  for (int i = 0; i < g.count; i++)
                      out.append(py::make_tuple((uptr)g.base[i], g.stride[i], g.cnt[i], g.n[i]));
                  return out;
+             })
+        .def("xchg_step",
+             [](BPlan &p, uptr x, uptr xg, int u8, float sc, uptr labels, uptr T, int ldt, int n_valid, float lr,
+                float alpha, float scale, uptr xar, uptr s) {
+                 hpnn_xar_view v;
+                 check(hpnn_xar_view_get((hpnn_xar *)xar, &v), "xar_view_get");
+                 const int r = p.xchg_step(xin(x, xg, u8, sc), (const int *)P(labels), (const float *)P(T), ldt,
+                                           n_valid, lr, alpha, scale, v, S(s));
+                 if (r != -1) check(r, "BPlan.xchg_step");
+                 return r == 0;
              })
         .def("update_flat",
              [](BPlan &p, uptr G, float lr, float alpha, float scale, uptr s) {
@@ -492,6 +503,24 @@ PYBIND11_MODULE(_native, m) {
                                                          L.data(), (int)L.size(), lr, alpha, scale, momentum,
                                                          S(stream)),
                     "xar_all_reduce_slabs_update_f32");
+          });
+    m.def("xar_local", [](uptr c) {
+        float *buf = nullptr;
+        long half = 0;
+        const unsigned int *sel = nullptr;
+        check(hpnn_xar_local((hpnn_xar *)c, &buf, &half, &sel), "xar_local");
+        return py::make_tuple((uptr)buf, (uptr)sel, half);
+    });
+    m.def("xar_reduce_local_update_f32",
+          [](uptr c, long count, uptr out, std::vector<std::tuple<uptr, uptr, uptr, uptr, uptr, int, int>> layers,
+             float lr, float alpha, float scale, int momentum, uptr stream) {
+              std::vector<hpnn_xar_upd_layer> L;
+              for (auto &t : layers)
+                  L.push_back({(float *)P(std::get<0>(t)), (float *)P(std::get<1>(t)), P(std::get<2>(t)),
+                               P(std::get<3>(t)), P(std::get<4>(t)), std::get<5>(t), std::get<6>(t)});
+              check(hpnn_xar_reduce_local_update_f32((hpnn_xar *)c, count, (float *)P(out), L.data(), (int)L.size(), lr,
+                                                     alpha, scale, momentum, S(stream)),
+                    "xar_reduce_local_update_f32");
           });
     m.def("xar_status", [](uptr c) { return hpnn_xar_status((hpnn_xar *)c); });
     m.def("xar_self_test", [](uptr c, uptr stream) { return hpnn_xar_self_test((hpnn_xar *)c, S(stream)); });

@@ -343,11 +343,15 @@ class MLP:
             if on_ready:
                 on_ready(l)
 
-    def grads_slabs(self, X, labels=None, T=None, n_valid=None):
+    def grads_slabs(self, X, labels=None, T=None, n_valid=None, dst=None):
         """fused modes: front + first-layer gradient with the gradient left unreduced; returns
-        [(address, slab stride, slabs, floats)] segments for the xGMI all-reduce's copy-in"""
+        [(address, slab stride, slabs, floats)] segments for the xGMI all-reduce's copy-in.
+        dst = (address, selector address, half stride in floats) -- the all-reduce's own
+        buffer (NativeComm.xar_local): when G0 reduces in-kernel the gradient goes there and
+        the result is [] (nothing to copy in)"""
         n_valid = self.Bp if n_valid is None else int(n_valid)
-        return self.plan.grads_slabs(*self._x(X), *self._tgt(labels, T), n_valid, _stream())
+        d, sel, alt = dst if dst is not None else (0, 0, 0)
+        return self.plan.grads_slabs(*self._x(X), *self._tgt(labels, T), n_valid, _stream(), d, sel, alt)
 
     def train_step(self, X, labels=None, T=None, n_valid=None, lr=0.01, alpha=0.2):
         """One minibatch fwd + bwd + update on the current stream (no host sync)."""

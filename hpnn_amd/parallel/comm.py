@@ -87,6 +87,26 @@ class NativeComm:
         """one-shot xGMI all-reduce for the small gradient buckets (include/libhpnn/xar.h):
         every rank maps every peer's buffer (hipIpc handles exchanged over the process
         group); all ranks agree before it is used, else every rank stays on RCCL"""
+        x = self._open_xar(max_bytes)
+        if not x:
+            return False
+        self.xar = x
+        self.xar_max = max_bytes
+        if self.h:
+            native().comm_set_xar(self.h, x, max_bytes)
+        return True
+
+    def attach_xar_kernel(self, max_bytes):
+        """a second xGMI communicator whose protocol runs inside a compute kernel (the fused
+        data-parallel first-layer gradient, BPlan.xchg_step); collective, like the first.
+        Returns its handle, 0 when unavailable on some rank."""
+        if not self.xar:
+            return 0
+        if not getattr(self, "xar_kernel", 0):
+            self.xar_kernel = self._open_xar(max_bytes)
+        return self.xar_kernel
+
+    def _open_xar(self, max_bytes):
         n = native()
         x = n.xar_create(self.rank, self.world, max_bytes)
         ok = bool(x)
@@ -119,12 +139,8 @@ class NativeComm:
         if int(flag.item()) != 1:
             if x:
                 n.xar_destroy(x)
-            return False
-        self.xar = x
-        self.xar_max = max_bytes
-        if self.h:
-            n.comm_set_xar(self.h, x, max_bytes)
-        return True
+            return 0
+        return x
 
     # -- collectives on the current stream ------------------------------------------
     def all_reduce(self, t, op=OP_SUM):
@@ -183,6 +199,24 @@ class NativeComm:
             float(lr), float(alpha), float(scale), int(bool(momentum)), _stream())
         return out
 
+    def xar_local(self):
+        """(buffer address, selector address, half stride in floats) of the in-place form
+        (include/libhpnn/xar.h hpnn_xar_local)"""
+        if not hasattr(self, "_xar_local"):
+            self._xar_local = native().xar_local(self.xar)
+        return self._xar_local
+
+    def reduce_local_update(self, out, layers, lr, alpha, scale, momentum):
+        """the in-place all-reduce + step: this rank's contribution already sits in the
+        buffer half xar_local() selects (written by the G0 launch)"""
+        def p(t):
+            return 0 if t is None else t.data_ptr()
+        native().xar_reduce_local_update_f32(
+            self.xar, sum(w.shape[0] * w.shape[1] for w, *_ in layers), out.data_ptr(),
+            [(p(w), p(v), p(wb), p(wt), p(wf), w.shape[0], w.shape[1]) for w, v, wb, wt, wf in layers],
+            float(lr), float(alpha), float(scale), int(bool(momentum)), _stream())
+        return out
+
     # -- failure detection ----------------------------------------------------------
     def check(self):
         """raise if the communicator saw an asynchronous error (peer died, link down) or an
@@ -208,7 +242,7 @@ class NativeComm:
 
     def xar_healthy(self):
         """False when an xGMI all-reduce barrier of this rank timed out"""
-        return not self.xar or native().xar_status(self.xar) == 0
+        return all(not x or native().xar_status(x) == 0 for x in (self.xar, getattr(self, "xar_kernel", 0)))
 
     def detach_xar(self):
         """stop using the xGMI all-reduce (every rank must call it: RCCL takes over).  The
@@ -217,11 +251,14 @@ class NativeComm:
             native().comm_set_xar(self.h, 0, 0)
         self._xar_detached = self.xar
         self.xar = 0
+        self._xar_kernel_detached = getattr(self, "xar_kernel", 0)
+        self.xar_kernel = 0
 
     def close(self):
-        if getattr(self, "_xar_detached", 0):
-            native().xar_destroy(self._xar_detached)
-            self._xar_detached = 0
+        for a in ("_xar_detached", "_xar_kernel_detached", "xar_kernel"):
+            if getattr(self, a, 0):
+                native().xar_destroy(getattr(self, a))
+                setattr(self, a, 0)
         if getattr(self, "xar", 0):
             if self.h:
                 native().comm_set_xar(self.h, 0, 0)

@@ -22,6 +22,10 @@ from .. import ops
 
 # HPNN_XAR_UPD=0: separate optimizer launch after the xGMI all-reduce (fused MNIST path)
 _XAR_UPD = os.environ.get("HPNN_XAR_UPD", "1") == "1"
+# HPNN_XAR_LOCAL=0: the G0 launch writes gflat and the all-reduce copies it in (A/B)
+_XAR_LOCAL = os.environ.get("HPNN_XAR_LOCAL", "1") == "1"
+# HPNN_XAR_G0=0: no exchange inside the first-layer gradient launch (separate all-reduce launch)
+_XAR_G0 = os.environ.get("HPNN_XAR_G0", "1") == "1"
 
 
 class DataParallel:
@@ -54,6 +58,7 @@ class DataParallel:
         self.buckets = self._plan(bucket_bytes)
         self.native = None
         self.dpx = None
+        self.xar_inplace = False  # last fused xGMI step wrote its gradient in place
         on_gpu = getattr(model, "device", torch.device("cpu")).type == "cuda"
         if self.active and on_gpu and comm == "xar":
             from .comm import NativeComm
@@ -61,6 +66,13 @@ class DataParallel:
         elif self.active and on_gpu and (comm == "native" or (comm == "auto" and dist.get_backend(group) == "nccl")):
             from .comm import NativeComm
             self.native = NativeComm(group, device=model.device.index)
+        # fused MNIST modes on the xGMI communicator: a second one whose protocol runs inside
+        # the first-layer gradient launch (BPlan.xchg_step: front + ONE launch for G0, its
+        # reduction, the exchange and every step -- the single-GPU step's launch count)
+        self.xar_k = 0
+        if (self.native is not None and self.native.xar and _XAR_G0 and getattr(model, "fused_mode", None) in ("x", "t")
+                and model.grad_flat.numel() * 4 <= self.native.xar_max):
+            self.xar_k = self.native.attach_xar_kernel(model.grad_flat.numel() * 4)
         # HPNN_DPX_FORCE=1 (tests): the native exchange even on one rank (with HPNN_DPX_SHARD1=1
         # its BF16 reduce-scatter path too), so a one-GPU box runs its kernels
         dpx_one = os.environ.get("HPNN_DPX_FORCE", "0") == "1"
@@ -136,14 +148,22 @@ class DataParallel:
         copy-in phase also sums the local split-K slabs of G0 and the [G1|G2] groups and
         which then applies every layer's update to the reduced gradients"""
         m = self.m
-        segs = m.grads_slabs(X, labels, T, n_valid)
         scale = 1.0 / (n_valid * self.world)
-        if _XAR_UPD:
+        if self.xar_k and m.plan.xchg_step(*m._x(X), *m._tgt(labels, T), int(n_valid), float(lr), float(alpha),
+                                           float(scale), self.xar_k, torch.cuda.current_stream().cuda_stream):
+            self.xar_inplace = "kernel"
+            return
+        segs = m.grads_slabs(X, labels, T, n_valid, dst=self.native.xar_local() if _XAR_UPD and _XAR_LOCAL else None)
+        layers = [(m.W32[l], m.V32[l], m.Wb[l], m.Wt[l], m.W0f if l == 0 else None) for l in range(m.L)]
+        self.xar_inplace = "buffer" if not segs else False
+        if not segs:
+            # the G0 launch wrote the reduced local gradient straight into the all-reduce's
+            # buffer: barrier, peer sums and every layer's step, no copy-in
+            self.native.reduce_local_update(m.grad_flat, layers, lr, alpha, scale, m.momentum)
+        elif _XAR_UPD:
             # exchange + every layer's optimizer step in ONE launch (the update kernel and
             # its launch gap leave the data-parallel step)
-            self.native.all_reduce_slabs_update(
-                m.grad_flat, segs, [(m.W32[l], m.V32[l], m.Wb[l], m.Wt[l], m.W0f if l == 0 else None)
-                                    for l in range(m.L)], lr, alpha, scale, m.momentum)
+            self.native.all_reduce_slabs_update(m.grad_flat, segs, layers, lr, alpha, scale, m.momentum)
         else:
             self.native.all_reduce_slabs(m.grad_flat, segs)
             m.update_all(lr, alpha, scale)

@@ -78,6 +78,33 @@ typedef struct {
 int hpnn_xar_all_reduce_slabs_update_f32(hpnn_xar *c, const hpnn_xar_seg *segs, int nseg, float *out,
                                          const hpnn_xar_upd_layer *layers, int nl, float lr, float alpha, float scale,
                                          int momentum, hipStream_t stream);
+/* in-place form: a producer kernel writes this rank's contribution to the NEXT call
+ * straight into the buffer -- at buf + half when *sel is even, at buf when odd (read *sel
+ * on the device, in stream order: graph replays stay correct) -- and
+ * hpnn_xar_reduce_local_update_f32 then runs the barrier, the peer sums and the step with
+ * no copy-in phase.  The double-buffer argument is the copy-in's: the producer runs after
+ * this rank's previous call, whose barrier no peer passes before finishing the call before. */
+int hpnn_xar_local(hpnn_xar *c, float **buf, long *half, const unsigned int **sel);
+int hpnn_xar_reduce_local_update_f32(hpnn_xar *c, long count, float *out, const hpnn_xar_upd_layer *layers, int nl,
+                                     float lr, float alpha, float scale, int momentum, hipStream_t stream);
+/* the communicator as seen by a kernel that runs the one-shot protocol itself (the fused
+ * data-parallel first-layer gradient, kernels_g0.hip): every rank's buffer (two halves of
+ * `half` floats) and signal block, this rank's per-workgroup epochs.  Workgroup b of every
+ * rank owns the same elements; the kernel advances ep[b], stores into half (ep[b] & 1) of its
+ * own buffer, waits for its stores, writes flag A of (b, rank) on every peer, waits for flag A
+ * of (b, p) from every peer, then reads the peers' halves.  An instance used this way must not
+ * also serve hpnn_xar_all_reduce* calls (their workgroups own other elements). */
+typedef struct {
+    float *buf[HPNN_XAR_MAX_RANKS];
+    unsigned int *sig[HPNN_XAR_MAX_RANKS];
+    long half;
+    unsigned int *ep;
+    int rank, world;
+    unsigned long long timeout; /* wall-clock ticks */
+} hpnn_xar_view;
+#define HPNN_XAR_FLAG_A(sig, b, r) ((sig) + (long)(b) * HPNN_XAR_MAX_RANKS + (r))
+#define HPNN_XAR_ERROR_WORD (2 * HPNN_XAR_MAX_BLOCKS * HPNN_XAR_MAX_RANKS)
+int hpnn_xar_view_get(hpnn_xar *c, hpnn_xar_view *v);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
 int hpnn_xar_status(hpnn_xar *c);
 /* collective self-test, run by every rank right after hpnn_xar_open: all-reduces known

@@ -62,6 +62,13 @@ for s in "$@"; do
       HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dpprof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 &&
       HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29534 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_XAR_UPD=0 HPNN_DP_FORCE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 step dpbench_sep 200 python bench.py --steps 200 --warmup 20 ;;
+    dpab)  # N > 1 step path on one GPU: exchange inside the G0 launch vs its own launch (HPNN_XAR_G0=0), vs single
+      step dpab_single 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_DP_FORCE=1 step dpab_local 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --steps 200 --warmup 20 &&
+      HPNN_XAR_G0=0 HPNN_DP_FORCE=1 step dpab_buffer 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 bench.py --steps 200 --warmup 20 &&
+      step dpab_singleb 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_DP_FORCE=1 step dpab_localb 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29543 bench.py --steps 200 --warmup 20 &&
+      HPNN_XAR_G0=0 HPNN_DP_FORCE=1 step dpab_bufferb 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29544 bench.py --steps 200 --warmup 20 ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;

@@ -24,9 +24,11 @@ def _data(rank, step, u8=False):
     return x, torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
 
 
-def _worker(rank, world, port, graph, q, u8=False, xar_mode=None):
+def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel"):
     try:
         os.environ["LOCAL_WORLD_SIZE"] = str(world)
+        os.environ["HPNN_XAR_G0"] = "1" if form == "kernel" else "0"
+        os.environ["HPNN_XAR_LOCAL"] = "1" if form == "buffer" else "0"
         if xar_mode is not None:  # 1 one-shot, 2 two-shot (the default from 4 ranks), unset: auto
             os.environ["HPNN_XAR_MODE"] = str(xar_mode)
         os.environ["HPNN_XAR_TIMEOUT_MS"] = "2000"
@@ -63,6 +65,9 @@ def _worker(rank, world, port, graph, q, u8=False, xar_mode=None):
                 dp.train_step(batches[step][0], labels=batches[step][1], lr=0.05, alpha=0.2)
         torch.cuda.synchronize()
         dp.check()
+        # kernel: the exchange ran inside the G0 launch; buffer: the G0 launch wrote the
+        # gradient into the all-reduce's buffer half; copy: the all-reduce copied it in
+        assert dp.xar_inplace == (form if form != "copy" else False), (dp.xar_inplace, form)
         W = torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
         q.put((rank, W))
         dist.barrier()
@@ -84,13 +89,13 @@ def _reference(u8=False, world=2):
     return torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
 
 
-def _run(world, graph, u8, xar_mode=None):
+def _run(world, graph, u8, xar_mode=None, form="kernel"):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode, form)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=110) for _ in ps)
@@ -114,6 +119,15 @@ def test_dp_step_on_xgmi_allreduce_two_processes(gpu, graph, u8):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", ["buffer", "copy"])
+def test_dp_step_separate_exchange_forms(gpu, form):
+    """HPNN_XAR_G0=0: the exchange in its own launch after the G0 launch, which writes the
+    all-reduce's buffer half (buffer) or the plan's gradient buffer for the all-reduce to
+    copy in (copy, HPNN_XAR_LOCAL=0): same weights as the in-kernel exchange"""
+    _run(2, True, False, None, form)
+
+
+@pytest.mark.gpu
 def test_dp_step_two_shot_with_fused_update(gpu):
     """the two-shot all-reduce with the optimizer step fused in (each rank updates its own
     shard in the reduce phase and the peers' shards after the gather), forced at 2 ranks in
@@ -121,4 +135,4 @@ def test_dp_step_two_shot_with_fused_update(gpu):
     front kernel needs whole CUs while the other ranks' all-reduce workgroups spin on
     theirs; the two-shot + update exchange itself runs at 3, 4 and 8 ranks in
     tests/test_xar_gpu.py.)"""
-    _run(2, True, True, 2)
+    _run(2, True, True, 2, "buffer")
