@@ -283,12 +283,16 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
 }
 
 /* sum of float4 at offset o over the first `world` ranks' buffers, rank order (identical bits
- * on every rank); every load in flight before the adds */
+ * on every rank); all loads in flight at once, system-coherent (sc0 sc1: no cache can serve a
+ * stale line, so no acquire fence -- an invalidating acquire per workgroup, while the other
+ * workgroups still stream their split sums, cost ~10 us per step) */
+static_assert(HPNN_XAR_MAX_RANKS == 8, "one ld_sc1_x8 per element");
 __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
-    f32x4 x[HPNN_XAR_MAX_RANKS];
+    const float *q[8];
 #pragma unroll
-    for (int p = 0; p < HPNN_XAR_MAX_RANKS; p++)
-        if (p < v.world) x[p] = *(const f32x4 *)(v.buf[p] + o);
+    for (int p = 0; p < 8; p++) q[p] = v.buf[p < v.world ? p : 0] + o;
+    f32x4 x[8];
+    hpnn::ld_sc1_x8<true>(x, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
     f32x4 a = x[0];
 #pragma unroll
     for (int p = 1; p < HPNN_XAR_MAX_RANKS; p++)
@@ -310,7 +314,7 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const long hoff = (e & 1) ? v.half : 0;
-    if (t < v.world) {
+    if (t < v.world && !(u.proto & 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
         __hip_atomic_store(HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         unsigned int *f = HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
         const unsigned long long t0 = wall_clock64();
@@ -324,7 +328,8 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         }
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* invalidate, no writeback */
+    if (u.proto & 8) /* diagnostics: the invalidating system acquire as well */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     for (int c = e0 + t; c < e1; c += NT) {
         const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
         const f32x4 g = xsum_peers(v, hoff + (long)(nt0 + row) * ldg + col);

@@ -69,6 +69,10 @@ for s in "$@"; do
       step dpab_singleb 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_DP_FORCE=1 step dpab_localb 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29543 bench.py --steps 200 --warmup 20 &&
       HPNN_XAR_G0=0 HPNN_DP_FORCE=1 step dpab_bufferb 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29544 bench.py --steps 200 --warmup 20 ;;
+    xchgab)  # in-kernel exchange ablations (HPNN_G0_PROTO: 8 + system acquire, 16 no barrier)
+      for pr in 0 8 16; do HPNN_G0_PROTO=$pr HPNN_DP_FORCE=1 step xchg_p$pr 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $((29550 + pr)) bench.py --steps 200 --warmup 20 || exit 1; done ;;
+    tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
+    widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
     learn) step learn 900 python scripts/learnability.py --out $O/learnability.jsonl ;;
     synthrs) step bench_synth_rs 300 python bench.py --model synth --grad-comm bf16rs --steps 20 --warmup 5 ;;
