@@ -38,6 +38,8 @@
 #include <libhpnn.h>
 #include <libhpnn/xar.h>
 #include <stddef.h>
+
+#include "../gpu/mfma_common.h"
 #include <stdlib.h>
 #include <string.h>
 
@@ -92,11 +94,18 @@ __device__ __forceinline__ void xbarrier(const XarPeers &P, int rank, int world,
         }
     }
     __syncthreads();
-    if (light) /* acquire: invalidate (no writeback) before reading peer data (agent-scope and
-                * ordering-only acquires measured no faster, profiles/r4) */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    else
-        __threadfence_system();
+    /* acquire: light modes read peer data with system-coherent loads (sc0 sc1, ld_peer*), which
+     * no cache serves stale, so no invalidating fence (in the fused MNIST exchange that fence,
+     * one per workgroup, cost ~10 us per step: profiles/r4/m_dp_exchange_ab.txt) */
+    if (!light) __threadfence_system();
+}
+
+/* system-coherent float4 load of a peer buffer (load and its wait in one asm block, see
+ * ld_sc1_x8) */
+__device__ __forceinline__ float4 ld_peer(const float4 *p) {
+    hpnn::f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return make_float4(v[0], v[1], v[2], v[3]);
 }
 
 /* the input of a call: up to HPNN_XAR_MAX_SEGS segments laid end to end in the output;
@@ -162,21 +171,18 @@ __device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
 }
 
 /* sum of element i over the first `world` data halves, rank order */
+static_assert(HPNN_XAR_MAX_RANKS == 8, "one ld_sc1_x8 per element");
 __device__ __forceinline__ float4 sum_peers(const XarPeers &P, long half4, int world, long i) {
-    float4 v[HPNN_XAR_MAX_RANKS];
+    const float *q[8];
 #pragma unroll
-    for (int p = 0; p < HPNN_XAR_MAX_RANKS; p++)
-        if (p < world) v[p] = P.buf[p][half4 + i];
-    float4 s = v[0];
+    for (int p = 0; p < 8; p++) q[p] = (const float *)(P.buf[p < world ? p : 0] + half4 + i);
+    hpnn::f32x4 v[8];
+    hpnn::ld_sc1_x8<true>(v, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
+    hpnn::f32x4 s = v[0];
 #pragma unroll
-    for (int p = 1; p < HPNN_XAR_MAX_RANKS; p++)
-        if (p < world) {
-            s.x += v[p].x;
-            s.y += v[p].y;
-            s.z += v[p].z;
-            s.w += v[p].w;
-        }
-    return s;
+    for (int p = 1; p < 8; p++)
+        if (p < world) s += v[p];
+    return make_float4(s[0], s[1], s[2], s[3]);
 }
 
 /* optimizer step fused after the exchange (hpnn_xar_all_reduce_slabs_update_f32) */
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
             range(s, lo, hi);
             const float4 *src = P.buf[s] + half4;
             for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-                const float4 v = src[i];
+                const float4 v = light ? ld_peer(src + i) : src[i];
                 out[i] = v;
                 if constexpr (UPD) xar_update4(upd, i, v);
             }

@@ -71,6 +71,10 @@ for s in "$@"; do
       HPNN_XAR_G0=0 HPNN_DP_FORCE=1 step dpab_bufferb 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29544 bench.py --steps 200 --warmup 20 ;;
     xchgab)  # in-kernel exchange ablations (HPNN_G0_PROTO: 8 + system acquire, 16 no barrier)
       for pr in 0 8 16; do HPNN_G0_PROTO=$pr HPNN_DP_FORCE=1 step xchg_p$pr 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $((29550 + pr)) bench.py --steps 200 --warmup 20 || exit 1; done ;;
+    xarb)  # all-reduce per-call protocol cost, 1 and 2 processes on this GPU
+      step xarb_w1 200 python scripts/xar_bench.py --world 1 &&
+      step xarb_w2 200 python scripts/xar_bench.py --world 2 &&
+      step xarb_w2m2 200 python scripts/xar_bench.py --world 2 --mode 2 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
