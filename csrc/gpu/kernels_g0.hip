@@ -199,11 +199,19 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
  * cuda_snn.cu:2726-3717 (GER into dW, W += dW, dW *= alpha), batched. */
 constexpr unsigned long long G0_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
+/* the master weight / momentum of the first element a thread steps, loaded right after the
+ * GEMM so the load is in flight through the publish, ticket and split-sum waits instead of
+ * in series after them (passed by value with a flag: a pointer to it would put it on the
+ * stack) */
+struct Pre4 {
+    f32x4 w, v;
+};
+
 __device__ __forceinline__ void bpm_step4(float *__restrict__ W32, float *__restrict__ V32, size_t idx, f32x4 g,
-                                          const hpnn_g0_update &u, f32x4 &w) {
-    w = *(const f32x4 *)(W32 + idx);
+                                          const hpnn_g0_update &u, f32x4 &w, bool use = false, Pre4 pre = {}) {
+    w = use ? pre.w : *(const f32x4 *)(W32 + idx);
     if (u.momentum) {
-        f32x4 v = *(const f32x4 *)(V32 + idx);
+        f32x4 v = use ? pre.v : *(const f32x4 *)(V32 + idx);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             v[r] += u.lr * (g[r] * u.scale);
@@ -220,11 +228,12 @@ __device__ __forceinline__ void bpm_step4(float *__restrict__ W32, float *__rest
 
 /* element (n, k..k+3) of a [N][K] layer: FP32 master + BF16 W / W^T (+ fragment-major Wf) */
 __device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, __bf16 *Wt, __bf16 *Wf, int N, int K,
-                                           int n, int k, f32x4 g, const hpnn_g0_update &u) {
+                                           int n, int k, f32x4 g, const hpnn_g0_update &u, bool use = false,
+                                           Pre4 pre = {}) {
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
     const size_t idx = (size_t)n * K + k;
     f32x4 w;
-    bpm_step4(W32, V32, idx, g, u, w);
+    bpm_step4(W32, V32, idx, g, u, w, use, pre);
     bf16x4 wb;
 #pragma unroll
     for (int r = 0; r < 4; r++) wb[r] = (__bf16)w[r];
@@ -237,11 +246,28 @@ __device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, _
     for (int r = 0; r < 4; r++) Wt[(size_t)(k + r) * N + n] = wb[r];
 }
 
+/* float4 e4 of [G1 | G2] -> layer l, row n, column k */
+__device__ __forceinline__ int g12_elem(const hpnn_g0_update &u, long e4, int &n, int &k) {
+    long i = e4 * 4;
+    const long n1 = (long)u.Nb[0] * u.Kb[0];
+    const int l = i < n1 ? 0 : 1;
+    if (l) i -= n1;
+    n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+    return l;
+}
+__device__ __forceinline__ Pre4 pre_load(const float *W32, const float *V32, size_t idx, int momentum) {
+    Pre4 p;
+    p.w = *(const f32x4 *)(W32 + idx);
+    p.v = momentum ? *(const f32x4 *)(V32 + idx) : f32x4{0.f, 0.f, 0.f, 0.f};
+    return p;
+}
+
 /* [G1 | G2]: float4 columns [c0, c1) of the front's block slabs summed over all mrows rows in
  * a fixed order (RG row groups of NT / 16 threads, met in LDS in order), then layers 1 / 2
  * stepped at those elements */
 template <int NT>
-__device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long c1, f32x4 *red, float *g12out) {
+__device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long c1, f32x4 *red, float *g12out,
+                                          bool use = false, Pre4 pre = {}) {
     constexpr int C4 = 16, RG = NT / C4;
     const int t = threadIdx.x, c = t % C4, rg = t / C4;
     for (long b0 = c0; b0 < c1; b0 += C4) {
@@ -271,11 +297,10 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
             if (g12out) {
                 *(f32x4 *)(g12out + i) = g;
             } else {
-                const int l = i < (long)u.Nb[0] * u.Kb[0] ? 0 : 1;
-                if (l) i -= (long)u.Nb[0] * u.Kb[0];
-                const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+                int n, k;
+                const int l = g12_elem(u, e4, n, k);
                 step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n,
-                           k, g, u);
+                           k, g, u, use && b0 == c0 /* this thread's prefetched element */, pre);
             }
         }
         __syncthreads();
@@ -308,7 +333,7 @@ __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
  * exchange and the update need no launch of their own. */
 template <int NT>
 __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsigned int e, int N, int ldg, int e0, int e1,
-                                              int nt0, int mt0, int TMF) {
+                                              int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12) {
     const hpnn_xar_view &v = u.xv;
     const int t = threadIdx.x, b = blockIdx.x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -333,18 +358,16 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
     for (int c = e0 + t; c < e1; c += NT) {
         const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
         const f32x4 g = xsum_peers(v, hoff + (long)(nt0 + row) * ldg + col);
-        step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
+        step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
+                   pf && c == e0 + t && t < 128, pg0);
     }
     const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = b * nf / nb, c1 = (b + 1) * nf / nb;
-    const long n1 = (long)u.Nb[0] * u.Kb[0];
     for (long e4 = c0 + t; e4 < c1; e4 += NT) {
         const f32x4 g = xsum_peers(v, hoff + (long)N * ldg + e4 * 4);
-        long i = e4 * 4;
-        const int l = i < n1 ? 0 : 1;
-        if (l) i -= n1;
-        const int n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+        int n, k;
+        const int l = g12_elem(u, e4, n, k);
         step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,
-                   u);
+                   u, pf && e4 == c0 + t && t < 16, pg12);
     }
 }
 
@@ -375,6 +398,24 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         __syncthreads();
         gout = u.xv.buf[u.xv.rank] + ((xe_s & 1) ? u.xv.half : 0);
     }
+    /* this split's share of the tile (float4 [e0, e1)) and of [G1 | G2] ([c0, c1)); the first
+     * element of each that this thread will step: its W / V loads go out now (HPNN_G0_PROTO
+     * bit 64 turns the prefetch off) */
+    const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
+    const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
+    const long nb = (long)tiles * splits, nf = u.n12 / 4;
+    const long c0 = blockIdx.x * nf / nb, c1 = (blockIdx.x + 1) * nf / nb;
+    const bool steps = !u.gout || u.xchg, pf = steps && !(u.proto & 64);
+    Pre4 pg0 = {}, pg12 = {};
+    if (pf && t < 128 && e0 + t < e1) {
+        const int e = e0 + t, row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
+        pg0 = pre_load(u.W32, u.V32, (size_t)(nt0 + row) * ldg + col, u.momentum);
+    }
+    if (pf && t < 16 && c0 + t < c1) {
+        int n, k;
+        const int l = g12_elem(u, c0 + t, n, k);
+        pg12 = pre_load(u.W32b[l], u.V32b[l], (size_t)n * u.Kb[l] + k, u.momentum);
+    }
     /* publish this split's partial tile (write-through), then one ticket for the workgroup */
     if ((t >> 6) < 4) {
         const int r16 = lane & 15, q = lane >> 4;
@@ -397,10 +438,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         want_s = old - old % (unsigned)splits + (unsigned)splits; /* this launch's last ticket */
     }
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
-    {
-        const long nb = (long)tiles * splits, nf = u.n12 / 4, b = blockIdx.x;
-        g12_share<NT>(u, b * nf / nb, (b + 1) * nf / nb, red, gout ? gout + (size_t)N * ldg : nullptr);
-    }
+    g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
     if (t == 0) {
         unsigned int *cnt = u.cnt + 32 * tile;
         const unsigned int want = want_s;
@@ -420,13 +458,11 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     __syncthreads();
     /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
      * float4, each summing a fixed run of splits; the runs meet in LDS in order */
-    const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
     const int f = t % 128, part = t / 128;
-    const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
     const int s0 = part * splits / PARTS, s1 = (part + 1) * splits / PARTS;
     const size_t ss = (size_t)N * ldg;
-    for (int c0 = e0; c0 < e1; c0 += 128) {
-        const int e = c0 + f;
+    for (int cc = e0; cc < e1; cc += 128) {
+        const int e = cc + f;
         const int row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
         if (e < e1) {
@@ -445,11 +481,12 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
             if (gout)
                 *(f32x4 *)(gout + (size_t)(nt0 + row) * ldg + col) = g;
             else
-                step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u);
+                step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
+                           pf && cc == e0, pg0);
         }
         __syncthreads();
     }
-    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF);
+    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12);
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false>

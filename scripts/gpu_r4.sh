@@ -75,6 +75,13 @@ for s in "$@"; do
       step xarb_w1 200 python scripts/xar_bench.py --world 1 &&
       step xarb_w2 200 python scripts/xar_bench.py --world 2 &&
       step xarb_w2m2 200 python scripts/xar_bench.py --world 2 --mode 2 ;;
+    pfab)  # fused G0: first stepped element's W / V prefetched after the GEMM (default) vs not (HPNN_G0_PROTO=64)
+      step pf1 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_PROTO=64 step pf0 200 python bench.py --steps 200 --warmup 20 &&
+      step pf1b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_PROTO=64 step pf0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_DP_FORCE=1 step pfdp1 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29561 bench.py --steps 200 --warmup 20 &&
+      HPNN_G0_PROTO=64 HPNN_DP_FORCE=1 step pfdp0 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29562 bench.py --steps 200 --warmup 20 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
