@@ -17,14 +17,14 @@ SIZES = [784, 128, 64, 10]
 B = 8192
 
 
-def _data(rank, step, u8=False):
+def _data(rank, step, u8=False, B=B):
     g = torch.Generator().manual_seed(100 * rank + step)
     x = (torch.randint(0, 256, (B, SIZES[0]), generator=g, dtype=torch.uint8) if u8
          else torch.rand(B, SIZES[0], generator=g))
     return x, torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
 
 
-def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel"):
+def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel", B=B):
     try:
         os.environ["LOCAL_WORLD_SIZE"] = str(world)
         os.environ["HPNN_XAR_G0"] = "1" if form == "kernel" else "0"
@@ -39,11 +39,13 @@ def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel")
         dev = torch.device("cuda", 0)
         m = MLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=3)
         dp = DataParallel(m, comm="xar")
+        if form == "kernel":  # the in-kernel exchange needs the fused G0 on the tile path
+            assert m.fused_mode == "t" and dp.xar_k, (m.fused_mode, dp.xar_k)
         assert dp.native is not None and dp.native.xar and m.fused_mode in ("x", "t")
         dp.broadcast_parameters()
         batches = []
         for step in range(3):
-            x, lab = _data(rank, step, u8)
+            x, lab = _data(rank, step, u8, B)
             batches.append((m.prepare_input(x.to(dev)), lab.to(dev)))
             if u8:  # 8-bit pixels: fragment-major byte copy for the first-layer gradient
                 assert m._fm_input(batches[-1][0]) is not None
@@ -77,28 +79,28 @@ def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel")
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def _reference(u8=False, world=2):
+def _reference(u8=False, world=2, B=B):
     from hpnn_amd.models import MLP
     dev = torch.device("cuda", 0)
     m = MLP(SIZES, "SNN", batch=world * B, device=dev, momentum=True, seed=3)
     for step in (0, 1, 1):
-        xs, ls = zip(*[_data(r, step, u8) for r in range(world)])
+        xs, ls = zip(*[_data(r, step, u8, B) for r in range(world)])
         X = m.prepare_input(torch.cat(xs).to(dev))
         m.train_step(X, labels=torch.cat(ls).to(dev), lr=0.05, alpha=0.2)
     torch.cuda.synchronize()
     return torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
 
 
-def _run(world, graph, u8, xar_mode=None, form="kernel"):
+def _run(world, graph, u8, xar_mode=None, form="kernel", B=B):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode, form)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode, form, B)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=110) for _ in ps)
+    res = dict(q.get(timeout=110 if world <= 2 else 250) for _ in ps)
     for p in ps:
         p.join(timeout=30)
         if p.is_alive():
@@ -107,7 +109,7 @@ def _run(world, graph, u8, xar_mode=None, form="kernel"):
         assert isinstance(res[r], torch.Tensor), res[r]
     for r in range(1, world):
         assert torch.equal(res[0], res[r])  # deterministic, identical on every rank
-    ref = _reference(u8, world)
+    ref = _reference(u8, world, B)
     err = (res[0] - ref).abs().max().item()
     assert err < 2e-6, err
 
@@ -136,3 +138,14 @@ def test_dp_step_two_shot_with_fused_update(gpu):
     theirs; the two-shot + update exchange itself runs at 3, 4 and 8 ranks in
     tests/test_xar_gpu.py.)"""
     _run(2, True, True, 2, "buffer")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,batch", [(4, 4096), (8, 2048)])
+def test_dp_step_in_kernel_exchange_many_ranks(gpu, world, batch):
+    """the in-kernel exchange (flag barrier per G0 workgroup with every peer) at 4 and 8 ranks,
+    graph-captured, 8-bit input.  The ranks share this one GPU, so the per-rank batch is cut
+    until every rank's G0 grid (5 tiles x splits, 40 / 20 workgroups) plus its front fits on
+    the CUs at once: a rank's G0 spins at its barrier until every peer's G0 arrives."""
+    _run(world, True, True, None, "kernel", batch)
