@@ -792,6 +792,15 @@ struct Batched {
         return dpx && dpx->step(at(xs, row), L, L ? nullptr : T, ldt, nv, total, lr, alpha, s) == 0;
     }
     BOOL gather_masters() { return !dpx || dpx->gather_masters(s) == 0; }
+    /* fused modes: front + G0 with the exchange over xk and every layer's step in the same
+     * launch (BPlan::xchg_step, the Python DataParallel's path); -1 = not covered */
+    int xchg_step(const XSet &xs, long row, const float *T, int ldt, int nv, float lr, float alpha, float scale,
+                  hpnn_xar *xk) {
+        hpnn_xar_view v;
+        if (hpnn_xar_view_get(xk, &v)) return -2;
+        const int *L = xs.lab ? xs.lab + row : nullptr;
+        return p.xchg_step(at(xs, row), L, L ? nullptr : T, ldt, nv, lr, alpha, scale, v, s);
+    }
     bool has_dpx() const { return (bool)dpx; }
     void detach_dpx() { dpx.reset(); }
 
@@ -1052,6 +1061,7 @@ struct BatchedFP {
 
     bool attach_dpx(hpnn_comm *, int) { return false; } /* FP32 / FP64: the generic bucket loop */
     BOOL dp_step(const XSet &, long, const T *, int, int, int, double, double) { return FALSE; }
+    int xchg_step(const XSet &, long, const T *, int, int, double, double, double, hpnn_xar *) { return -1; }
     BOOL gather_masters() { return TRUE; }
     bool has_dpx() const { return false; }
     void detach_dpx() {}
@@ -1527,33 +1537,47 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const size_t count = net.flat_count();
     /* gradient exchange: one-shot xGMI all-reduce when every rank is on this node and the
      * gradients are small, else RCCL; every rank takes the same decision */
-    hpnn_xar *xar = nullptr;
+    hpnn_xar *xar = nullptr, *xark = nullptr;
     hpnn_comm *comm = nullptr;
     const char *xe = getenv("HPNN_XAR");
     const char *lws = getenv("LOCAL_WORLD_SIZE");
     /* the xGMI all-reduce sums FP32; FP64 gradients go through RCCL */
     bool use_xar = Net::comm_dt == HPNN_DT_F32 && !(xe && xe[0] == '0') && lws && atoi(lws) == W &&
                    W <= HPNN_XAR_MAX_RANKS && count * 4 <= ((size_t)4 << 20) && !bf16rs;
-    if (use_xar) {
-        xar = hpnn_xar_create(R, W, count * 4);
+    /* collective: create, exchange the IPC handles, open, self-test on the real links; every
+     * rank agrees, else all get nullptr (-1: bootstrap failure) */
+    auto open_xar = [&](size_t bytes, hpnn_xar **out) -> int {
+        *out = nullptr;
+        hpnn_xar *x = hpnn_xar_create(R, W, bytes);
         std::vector<char> h(HPNN_XAR_HANDLE_BYTES, 0), all((size_t)W * HPNN_XAR_HANDLE_BYTES);
-        int ok = xar && hpnn_xar_handles(xar, h.data()) == 0;
-        if (hpnn_boot_allgather(h.data(), h.size(), all.data()) != 0) return FALSE;
-        if (ok) ok = hpnn_xar_open(xar, all.data()) == 0;
+        int ok = x && hpnn_xar_handles(x, h.data()) == 0;
+        if (hpnn_boot_allgather(h.data(), h.size(), all.data()) != 0) return -1;
+        if (ok) ok = hpnn_xar_open(x, all.data()) == 0;
         std::vector<int> oks(W);
-        if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return FALSE;
-        for (int v : oks) use_xar = use_xar && v;
-        if (use_xar) { /* known sums over the real links before any gradient goes through */
-            const int rc = hpnn_xar_self_test(xar, s);
+        if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return -1;
+        bool all_ok = true;
+        for (int v : oks) all_ok = all_ok && v;
+        if (all_ok) { /* known sums over the real links before any gradient goes through */
+            const int rc = hpnn_xar_self_test(x, s);
             ok = rc == 0;
             if (!ok) NN_WARN(stderr, "xGMI all-reduce self-test failed (%d) on rank %d\n", rc, R);
-            if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return FALSE;
-            for (int v : oks) use_xar = use_xar && v;
+            if (hpnn_boot_allgather(&ok, sizeof ok, oks.data()) != 0) return -1;
+            for (int v : oks) all_ok = all_ok && v;
         }
-        if (!use_xar && xar) {
-            hpnn_xar_destroy(xar);
-            xar = nullptr;
+        if (!all_ok) {
+            if (x) hpnn_xar_destroy(x);
+            return 0;
         }
+        *out = x;
+        return 0;
+    };
+    if (use_xar) {
+        if (open_xar(count * 4, &xar)) return FALSE;
+        use_xar = xar != nullptr;
+        /* fused modes: a second communicator whose protocol runs inside the G0 launch
+         * (HPNN_XAR_G0=0: the all-reduce launch instead) */
+        const char *xg = getenv("HPNN_XAR_G0");
+        if (use_xar && !(xg && xg[0] == '0') && open_xar(count * 4, &xark)) return FALSE;
     }
     if (!use_xar) {
         unsigned char id[HPNN_COMM_ID_BYTES] = {0};
@@ -1597,6 +1621,24 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                 ok = net.dp_step(Xd, start, tb, n_out, nv, total, o->lr, o->alpha);
                 continue;
             }
+            if (xark) {
+                /* the exchange and every step inside the first-layer gradient launch */
+                const int r = net.xchg_step(Xd, start, tb, n_out, nv, o->lr, o->alpha,
+                                            1.0 / (double)(total > 0 ? total : 1), xark);
+                if (r == 0) {
+                    if (e == 0 && b == 0 && R == 0)
+                        NN_OUT(stdout, "data-parallel step: exchange inside the first-layer gradient launch\n");
+                    continue;
+                }
+                if (r != -1) {
+                    NN_ERROR(stderr, "data-parallel fused step failed: %d\n", r);
+                    ok = FALSE;
+                    break;
+                }
+                /* not covered (same on every rank): the all-reduce launch from here on */
+                hpnn_xar_destroy(xark);
+                xark = nullptr;
+            }
             if (use_xar) {
                 /* small gradients: ONE latency-bound xGMI all-reduce of the whole buffer */
                 ok = net.grads(Xd, start, tb, n_out, nv);
@@ -1623,7 +1665,8 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         double l = 0.0;
         unsigned int h = 0;
         ok = net.read_stats(&l, &h);
-        if (ok) ok = use_xar ? hpnn_xar_status(xar) == 0 : hpnn_comm_check(comm) == 0;
+        if (ok) ok = use_xar ? hpnn_xar_status(xar) == 0 && (!xark || hpnn_xar_status(xark) == 0)
+                             : hpnn_comm_check(comm) == 0;
         struct {
             double loss;
             unsigned int hits, ok;
@@ -1658,6 +1701,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     Xd.release();
     if (Td) hpnn_dev_free(Td);
     if (xar) hpnn_xar_destroy(xar);
+    if (xark) hpnn_xar_destroy(xark);
     if (comm) hpnn_comm_destroy(comm);
     if (ok && k->gpu) ((GpuModel *)k->gpu)->host_newer = true;
     return ok;

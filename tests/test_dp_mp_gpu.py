@@ -45,7 +45,8 @@ def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims, dtype):
         _data(str(d / "s"), 700, n_in, n_out)
         formats.write_conf(str(d / "nn.conf"), name="mp", type="SNN", seed=4, inputs=n_in, hiddens=hid, outputs=n_out,
                            train="BPM", sample_dir="./s", test_dir="./s", dtype=dtype)
-    flags = ["-vv", "-b", "256", "-e", "2", "nn.conf"]
+    # MNIST-shaped: 256 samples per rank, the tile path (fused G0 with the in-kernel exchange)
+    flags = ["-vv", "-b", "512" if n_in == 784 else "256", "-e", "2", "nn.conf"]
     r = subprocess.run([TN] + flags, cwd=tmp_path / "one", env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     with socket.socket() as s:
@@ -69,6 +70,8 @@ def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims, dtype):
     for rc, o, e in outs:
         assert rc == 0, o[-2000:] + e[-2000:]
     assert f"2 processes (xGMI all-reduce, {dtype})" in outs[0][1]
+    if dims[0] == 784 and dtype == "bf16":  # fused tile mode: the exchange runs in the G0 launch
+        assert "exchange inside the first-layer gradient launch" in outs[0][1], outs[0][1][-2000:]
     assert outs[1][1].strip() == ""  # rank 1 prints nothing
     w1 = formats.read_kernel(str(tmp_path / "one" / "kernel.opt"))["weights"]
     w2 = formats.read_kernel(str(tmp_path / "two" / "kernel.opt"))["weights"]
