@@ -82,6 +82,12 @@ for s in "$@"; do
       HPNN_G0_PROTO=64 step pf0b 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_DP_FORCE=1 step pfdp1 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29561 bench.py --steps 200 --warmup 20 &&
       HPNN_G0_PROTO=64 HPNN_DP_FORCE=1 step pfdp0 200 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29562 bench.py --steps 200 --warmup 20 ;;
+    rruffs)  # RRUFF G0 / G1 split sweep in the step
+      step rs_def 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=8,32 step rs_8_32 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=32,32 step rs_32_32 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_SPLITS=16,16 step rs_16_16 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      step rs_defb 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
