@@ -444,6 +444,12 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
         }
         return launch_tn_big(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     }
+    /* 64 x 64 tiles when the 128 x 128 grid leaves CUs idle: RRUFF's G1 (256 x 256 over 16384
+     * rows, 32 splits) as 16 x 32 = 512 workgroups instead of 4 x 32 = 128, 145.8 / 146.1 vs
+     * 150.6 / 149.4 us per step (profiles/r4/u_rruff_t64.txt; HPNN_TN_T64=0: off) */
+    static const int t64 = [] { const char *e = getenv("HPNN_TN_T64"); return e ? atoi(e) : 1; }();
+    if (t64 && M % 64 == 0 && N % 64 == 0 && (long)(M / 128) * (N / 128) * splits < 256)
+        return launch_tn_t<64, 64>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 128 == 0) return launch_tn_m<128>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 160 == 0) return launch_tn_m<160>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);
     if (M % 96 == 0) return launch_tn_m<96>(D, ldd, H, ldh, slab, ldg, N, M, Bt, splits, stream, t);

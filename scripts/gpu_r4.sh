@@ -88,6 +88,13 @@ for s in "$@"; do
       HPNN_SPLITS=32,32 step rs_32_32 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       HPNN_SPLITS=16,16 step rs_16_16 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       step rs_defb 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
+    t64ab)  # RRUFF G1: 128 x 128 tiles (default) vs 64 x 64 (HPNN_TN_T64=1), 32 / 16 splits
+      step t64_def 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN_T64=1 step t64_32 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN_T64=1 HPNN_SPLITS=16,16 step t64_16 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN_T64=1 HPNN_SPLITS=16,8 step t64_8 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      step t64_defb 200 python bench.py --model rruff --steps 100 --warmup 10 &&
+      HPNN_TN_T64=1 step t64_32b 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
