@@ -39,8 +39,8 @@ def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel",
         dev = torch.device("cuda", 0)
         m = MLP(SIZES, "SNN", batch=B, device=dev, momentum=True, seed=3)
         dp = DataParallel(m, comm="xar")
-        if form == "kernel":  # the in-kernel exchange needs the fused G0 on the tile path
-            assert m.fused_mode == "t" and dp.xar_k, (m.fused_mode, dp.xar_k)
+        if form == "kernel":  # the in-kernel exchange needs the fused G0 (tile or fused-x path)
+            assert m.fused_mode in ("t", "x") and dp.xar_k, (m.fused_mode, dp.xar_k)
         assert dp.native is not None and dp.native.xar and m.fused_mode in ("x", "t")
         dp.broadcast_parameters()
         batches = []
@@ -149,3 +149,10 @@ def test_dp_step_in_kernel_exchange_many_ranks(gpu, world, batch):
     until every rank's G0 grid (5 tiles x splits, 40 / 20 workgroups) plus its front fits on
     the CUs at once: a rank's G0 spins at its barrier until every peer's G0 arrives."""
     _run(world, True, True, None, "kernel", batch)
+
+
+@pytest.mark.gpu
+def test_dp_step_in_kernel_exchange_fused_x_mode(gpu):
+    """a per-rank batch that is not a whole number of 256-sample tiles (8320 = 65 x 128) runs
+    the fused-x front (kernels_mlp3x.hip) before the same G0 launch with the exchange"""
+    _run(2, True, True, None, "kernel", 8320)
