@@ -95,6 +95,13 @@ for s in "$@"; do
       HPNN_TN_T64=1 HPNN_SPLITS=16,8 step t64_8 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       step t64_defb 200 python bench.py --model rruff --steps 100 --warmup 10 &&
       HPNN_TN_T64=1 step t64_32b 200 python bench.py --model rruff --steps 100 --warmup 10 ;;
+    g0s)  # MNIST fused G0 split count in the step (tiles x splits <= 256 for co-residency)
+      step g0s48 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_SPLITS=40,1,1 step g0s40 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_SPLITS=32,1,1 step g0s32 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_SPLITS=48,1,1 step g0s48x 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_SPLITS=40,1,1 step g0s40b 200 python bench.py --steps 200 --warmup 20 &&
+      step g0s48b 200 python bench.py --steps 200 --warmup 20 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
