@@ -102,6 +102,13 @@ for s in "$@"; do
       HPNN_SPLITS=48,1,1 step g0s48x 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_SPLITS=40,1,1 step g0s40b 200 python bench.py --steps 200 --warmup 20 &&
       step g0s48b 200 python bench.py --steps 200 --warmup 20 ;;
+    gsab)  # steps per HIP graph replay
+      step gs20 200 python bench.py --steps 200 --warmup 20 --graph-steps 20 &&
+      step gs50 200 python bench.py --steps 200 --warmup 20 --graph-steps 50 &&
+      step gs100 200 python bench.py --steps 200 --warmup 20 --graph-steps 100 &&
+      step gs20b 200 python bench.py --steps 200 --warmup 20 --graph-steps 20 &&
+      step gs50b 200 python bench.py --steps 200 --warmup 20 --graph-steps 50 &&
+      step gs100b 200 python bench.py --steps 200 --warmup 20 --graph-steps 100 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
