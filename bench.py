@@ -90,10 +90,11 @@ def main():
     m = MLP(sizes, net, batch=args.batch, device=dev, momentum=True, seed=10958,
             init="reference" if args.model == "mnist" else "fast",
             splits=[int(v) for v in sp.split(",")] if sp else None)
-    if rehearse and world > 1 and hasattr(m, "plan"):
+    if rehearse and world > 1 and hasattr(m, "plan") and os.environ.get("HPNN_REHEARSE_FUSED", "0") != "1":
         # ranks sharing one GPU: the fused first-layer gradient needs all its workgroups
         # co-resident (in-kernel split-K reduction), which another rank's kernels on the same
-        # CUs can prevent -- the rehearsal takes the slab form (one GPU per rank in real runs)
+        # CUs can prevent -- the rehearsal takes the slab form (one GPU per rank in real runs).
+        # HPNN_REHEARSE_FUSED=1 keeps it, for per-rank batches whose grids fit together.
         m.plan.g0_fused = False
     dp = DataParallel(m, comm="xar" if rehearse and world > 1 else "auto",
                       grad_comm=args.grad_comm if m.fused_mode is None else "fp32")
@@ -260,7 +261,9 @@ def main():
                 "grad_allreduce": ("none" if not dp.active else
                                    (("xgmi+rccl" if dp.native.h else "xgmi") if dp.native is not None and dp.native.xar else
                                     ("rccl-native" if dp.native is not None else "torch.distributed"))),
-                "grad_exchange": "bf16 reduce-scatter + sharded update + bf16 all-gather" if dp.sharded else "fp32",
+                "grad_exchange": ("bf16 reduce-scatter + sharded update + bf16 all-gather" if dp.sharded else
+                                  "fp32, inside the first-layer gradient launch"
+                                  if getattr(dp, "xar_inplace", False) == "kernel" else "fp32"),
                 "steps_per_graph": min(gsteps, args.steps) if use_graph else 0,
             },
             "train_loss_mean": loss_sum / max(1, samples // world),
