@@ -528,7 +528,8 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
     };
     /* D = 3 k-steps of loads in flight: 58.7-59.4 us per MNIST step vs 59.6-60.4 at D = 4 and
      * 59.8-60.3 at D = 2 (B reads one k-step ahead; a deeper ring costs the registers the B
-     * prefetch needs), profiles/r3/SUMMARY.md */
+     * prefetch needs), profiles/r3/SUMMARY.md; re-measured on the round-4 front (253 VGPRs):
+     * D = 2 62.4 / 62.1, D = 4 (spills) 63.0 / 63.3 vs 62.1 us (profiles/r4/dd_tile_d.txt) */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
         static const bool late = [] { const char *e = getenv("HPNN_TILE_EARLY"); return e && e[0] == '0'; }();
         if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)
