@@ -366,7 +366,12 @@ int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipSt
     memset(&u, 0, sizeof u);
     u.gout = gout;
     u.gsel = gsel, u.galt = galt;
-    if (xv) u.xchg = 1, u.xv = *xv;
+    if (xv) {
+        /* HPNN_XAR_G0_MODE: 0 auto (two-shot from 4 ranks), 1 one-shot, 2 two-shot */
+        static const int xm = [] { const char *e = getenv("HPNN_XAR_G0_MODE"); return e ? atoi(e) : 0; }();
+        u.xchg = xm == 1 ? 1 : (xm == 2 || xv->world >= 4) ? 2 : 1;
+        u.xv = *xv;
+    }
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
     u.cnt = g0cnt, u.err = g0cnt + 224;
     u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;

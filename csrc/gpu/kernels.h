@@ -122,7 +122,7 @@ typedef struct {
      * reduced G0 / [G1 | G2] elements into its half of xv's buffer, runs the one-shot flag
      * barrier of workgroup b with every peer (include/libhpnn/xar.h hpnn_xar_view), sums the
      * peers' copies in rank order and steps those elements (scale includes 1 / world) */
-    int xchg;
+    int xchg; /* 1 one-shot, 2 two-shot (each rank reduces 1 / world of every slice, then gathers) */
     hpnn_xar_view xv;
     int proto; /* hand-off diagnostics (HPNN_G0_PROTO): 1 producer agent release, 2 consumer agent
                 * acquire, 4 system-scope (sc0 sc1) partial loads */

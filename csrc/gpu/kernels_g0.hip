@@ -336,34 +336,66 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
                                               int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12) {
     const hpnn_xar_view &v = u.xv;
     const int t = threadIdx.x, b = blockIdx.x;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     const long hoff = (e & 1) ? v.half : 0;
-    if (t < v.world && !(u.proto & 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
-        __hip_atomic_store(HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        unsigned int *f = HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > v.timeout) {
-                __hip_atomic_store(v.sig[v.rank] + HPNN_XAR_ERROR_WORD, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
+    /* flag barrier `which` of workgroup b with every peer: this workgroup's stores to its buffer
+     * acknowledged first (uncached memory: no writeback needed) */
+    auto barrier = [&](int which) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t < v.world && !(u.proto & 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
+            unsigned int *const mine = which ? HPNN_XAR_FLAG_B(v.sig[v.rank], b, t) : HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
+            __hip_atomic_store(which ? HPNN_XAR_FLAG_B(v.sig[t], b, v.rank) : HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > v.timeout) {
+                    __hip_atomic_store(v.sig[v.rank] + HPNN_XAR_ERROR_WORD, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
             }
         }
+        __syncthreads();
+        if (u.proto & 8) /* diagnostics: the invalidating system acquire as well */
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    };
+    auto g0_off = [&](int c) { return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4)); };
+    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = b * nf / nb, c1 = (b + 1) * nf / nb;
+    const bool two = u.xchg == 2 && v.world > 1;
+    barrier(0);
+    if (two) {
+        /* reduce-scatter: element j of each part belongs to rank j % world, which sums it over
+         * all ranks (rank order) into its own buffer; a second barrier; every rank then reads
+         * each element from its owner -- each link carries 2 / world of the slice, not all */
+        for (int c = e0 + t; c < e1; c += NT)
+            if ((c - e0) % v.world == v.rank) {
+                const long o = hoff + g0_off(c);
+                *(f32x4 *)(v.buf[v.rank] + o) = xsum_peers(v, o);
+            }
+        for (long e4 = c0 + t; e4 < c1; e4 += NT)
+            if ((int)((e4 - c0) % v.world) == v.rank) {
+                const long o = hoff + (long)N * ldg + e4 * 4;
+                *(f32x4 *)(v.buf[v.rank] + o) = xsum_peers(v, o);
+            }
+        barrier(1);
     }
-    __syncthreads();
-    if (u.proto & 8) /* diagnostics: the invalidating system acquire as well */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    /* one-shot: the rank-order sum over every peer; two-shot: the owner's sum */
+    auto fetch = [&](long o, long j) -> f32x4 {
+        if (!two) return xsum_peers(v, o);
+        const float *q = v.buf[(int)(j % v.world)] + o;
+        f32x4 x; /* one system-coherent load and its wait in one asm block (see ld_sc1_x8) */
+        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(q) : "memory");
+        return x;
+    };
     for (int c = e0 + t; c < e1; c += NT) {
         const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
-        const f32x4 g = xsum_peers(v, hoff + (long)(nt0 + row) * ldg + col);
+        const f32x4 g = fetch(hoff + g0_off(c), c - e0);
         step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
                    pf && c == e0 + t && t < 128, pg0);
     }
-    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = b * nf / nb, c1 = (b + 1) * nf / nb;
     for (long e4 = c0 + t; e4 < c1; e4 += NT) {
-        const f32x4 g = xsum_peers(v, hoff + (long)N * ldg + e4 * 4);
+        const f32x4 g = fetch(hoff + (long)N * ldg + e4 * 4, e4 - c0);
         int n, k;
         const int l = g12_elem(u, e4, n, k);
         step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,

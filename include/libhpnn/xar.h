@@ -103,6 +103,7 @@ typedef struct {
     unsigned long long timeout; /* wall-clock ticks */
 } hpnn_xar_view;
 #define HPNN_XAR_FLAG_A(sig, b, r) ((sig) + (long)(b) * HPNN_XAR_MAX_RANKS + (r))
+#define HPNN_XAR_FLAG_B(sig, b, r) ((sig) + (long)(HPNN_XAR_MAX_BLOCKS + (b)) * HPNN_XAR_MAX_RANKS + (r))
 #define HPNN_XAR_ERROR_WORD (2 * HPNN_XAR_MAX_BLOCKS * HPNN_XAR_MAX_RANKS)
 int hpnn_xar_view_get(hpnn_xar *c, hpnn_xar_view *v);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */

@@ -24,8 +24,10 @@ def _data(rank, step, u8=False, B=B):
     return x, torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
 
 
-def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel", B=B):
+def _worker(rank, world, port, graph, q, u8=False, xar_mode=None, form="kernel", B=B, g0_mode=None):
     try:
+        if g0_mode is not None:  # in-kernel exchange: 1 one-shot, 2 two-shot (auto: two-shot from 4 ranks)
+            os.environ["HPNN_XAR_G0_MODE"] = str(g0_mode)
         os.environ["LOCAL_WORLD_SIZE"] = str(world)
         os.environ["HPNN_XAR_G0"] = "1" if form == "kernel" else "0"
         os.environ["HPNN_XAR_LOCAL"] = "1" if form == "buffer" else "0"
@@ -91,13 +93,13 @@ def _reference(u8=False, world=2, B=B):
     return torch.cat([w.flatten() for w in m.W32] + [v.flatten() for v in m.V32]).cpu()
 
 
-def _run(world, graph, u8, xar_mode=None, form="kernel", B=B):
+def _run(world, graph, u8, xar_mode=None, form="kernel", B=B, g0_mode=None):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode, form, B)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, graph, q, u8, xar_mode, form, B, g0_mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=110 if world <= 2 else 250) for _ in ps)
@@ -142,13 +144,20 @@ def test_dp_step_two_shot_with_fused_update(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,batch", [(4, 4096), (8, 2048)])
-def test_dp_step_in_kernel_exchange_many_ranks(gpu, world, batch):
-    """the in-kernel exchange (flag barrier per G0 workgroup with every peer) at 4 and 8 ranks,
-    graph-captured, 8-bit input.  The ranks share this one GPU, so the per-rank batch is cut
-    until every rank's G0 grid (5 tiles x splits, 40 / 20 workgroups) plus its front fits on
-    the CUs at once: a rank's G0 spins at its barrier until every peer's G0 arrives."""
-    _run(world, True, True, None, "kernel", batch)
+@pytest.mark.parametrize("world,batch,g0_mode", [(4, 4096, None), (8, 2048, None), (4, 4096, 1), (8, 2048, 1)])
+def test_dp_step_in_kernel_exchange_many_ranks(gpu, world, batch, g0_mode):
+    """the in-kernel exchange (flag barriers per G0 workgroup with every peer) at 4 and 8 ranks,
+    two-shot (the default from 4 ranks) and one-shot, graph-captured, 8-bit input.  The ranks
+    share this one GPU, so the per-rank batch is cut until every rank's G0 grid (5 tiles x
+    splits, 40 / 20 workgroups) plus its front fits on the CUs at once: a rank's G0 spins at
+    its barriers until every peer's G0 arrives."""
+    _run(world, True, True, None, "kernel", batch, g0_mode)
+
+
+@pytest.mark.gpu
+def test_dp_step_in_kernel_exchange_two_shot_two_ranks(gpu):
+    """the two-shot in-kernel exchange forced at 2 ranks (HPNN_XAR_G0_MODE=2)"""
+    _run(2, True, True, None, "kernel", B, 2)
 
 
 @pytest.mark.gpu
