@@ -109,6 +109,11 @@ for s in "$@"; do
       step gs20b 200 python bench.py --steps 200 --warmup 20 --graph-steps 20 &&
       step gs50b 200 python bench.py --steps 200 --warmup 20 --graph-steps 50 &&
       step gs100b 200 python bench.py --steps 200 --warmup 20 --graph-steps 100 ;;
+    synthab)  # synthetic 8 x 4096 ANN: 64 x 64 underfill tiles on (default) / off
+      step sy1 300 python bench.py --model synth --steps 20 --warmup 5 &&
+      HPNN_TN_T64=0 step sy0 300 python bench.py --model synth --steps 20 --warmup 5 &&
+      step sy1b 300 python bench.py --model synth --steps 20 --warmup 5 &&
+      HPNN_TN_T64=0 step sy0b 300 python bench.py --model synth --steps 20 --warmup 5 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
