@@ -92,7 +92,8 @@ __device__ __forceinline__ void wave_lds_fence() {
 constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
-template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true>
+template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
+          bool TRADE = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(acc[i][st][r] * xscale);
-                st_d4<TS>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i, o, lane);
+                st_d4<TS, TRADE>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i, o, lane);
             }
         lds_barrier();
 
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     bf16x4 o;
 #pragma unroll
                     for (int r = 0; r < 4; r++) o[r] = (__bf16)bipolar(a[st][ht][r]);
-                    st_d4<TS>(imgH2, lo, sw + 16 * st, 16 * ht, o, lane);
+                    st_d4<TS, TRADE>(imgH2, lo, sw + 16 * st, 16 * ht, o, lane);
                 }
         }
         mark(5);
@@ -378,11 +379,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 #pragma unroll
             for (int ht = 0; ht < 4; ht++) {
                 const f32x4 a = mfma(w2tf[ht], b, f32x4{0.f, 0.f, 0.f, 0.f});
-                const bf16x4 h = ld_d4<TS>(imgH2, lo, r0, 16 * ht, lane);
+                const bf16x4 h = ld_d4<TS, TRADE>(imgH2, lo, r0, 16 * ht, lane);
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; r++) o[r] = (__bf16)(a[r] * dbipolar((float)h[r]));
-                st_d4<TS>(imgD2, lo, r0, 16 * ht, o, lane);
+                st_d4<TS, TRADE>(imgD2, lo, r0, 16 * ht, o, lane);
             }
         }
         mark(7);
@@ -532,9 +533,16 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
      * D = 2 62.4 / 62.1, D = 4 (spills) 63.0 / 63.3 vs 62.1 us (profiles/r4/dd_tile_d.txt) */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
         static const bool late = [] { const char *e = getenv("HPNN_TILE_EARLY"); return e && e[0] == '0'; }();
+        /* HPNN_TILE_TRADE=1 (A/B): the chain's 8-byte image stores / loads with a lane-pair trade of
+         * halves -- LDS bank conflicts 18.5 % -> 5.6 % of the LDS instructions, but the shuffles
+         * cost more than the conflicts: 60.6 / 61.4 / 62.5 vs 59.9 / 59.8 / 60.0 us per step,
+         * per-workgroup span 59.4K vs 55.6K ticks (profiles/r4/tr_tile_trade_ab.txt) */
+        static const bool trade = [] { const char *e = getenv("HPNN_TILE_TRADE"); return e && e[0] == '1'; }();
+        if (trace && trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, true>, 512);
         if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)
                                : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
+        if (trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true>, 512);
 #ifdef HPNN_ABLATIONS
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);

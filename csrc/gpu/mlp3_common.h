@@ -64,8 +64,12 @@ __device__ __forceinline__ char *wr_ptr(char *img, const LaneOff &lo, int r0, in
  * same row, other 8-byte half of the same chunk (address ^ 8) -- through v_permlane16_swap,
  * so every group covers all slots.  Both lanes of a pair trade, so each byte is still
  * written / read once. */
-template <int R>
+template <int R, bool TRADE = true>
 __device__ __forceinline__ void st_d4(char *img, const LaneOff &lo, int r0, int c0, bf16x4 v, int lane) {
+    if constexpr (!TRADE) { /* plain wr_ptr store (2-way conflicts, no shuffles) */
+        *(bf16x4 *)wr_ptr<R>(img, lo, r0, c0) = v;
+        return;
+    }
     typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
     const u32x2 w = __builtin_bit_cast(u32x2, v);
     const bool trade = (lane >> 2) & 1;
@@ -78,8 +82,9 @@ __device__ __forceinline__ void st_d4(char *img, const LaneOff &lo, int r0, int 
     const int dh = trade ? (((lane >> 4) & 1) ? -8 : 8) : 0;
     *(u32x2 *)(p + dh) = trade ? o : w;
 }
-template <int R>
+template <int R, bool TRADE = true>
 __device__ __forceinline__ bf16x4 ld_d4(const char *img, const LaneOff &lo, int r0, int c0, int lane) {
+    if constexpr (!TRADE) return *(const bf16x4 *)wr_ptr<R>((char *)img, lo, r0, c0);
     typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
     const bool trade = (lane >> 2) & 1;
     const char *p = wr_ptr<R>((char *)img, lo, r0, c0);

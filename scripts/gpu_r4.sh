@@ -114,6 +114,14 @@ for s in "$@"; do
       HPNN_TN_T64=0 step sy0 300 python bench.py --model synth --steps 20 --warmup 5 &&
       step sy1b 300 python bench.py --model synth --steps 20 --warmup 5 &&
       HPNN_TN_T64=0 step sy0b 300 python bench.py --model synth --steps 20 --warmup 5 ;;
+    tradeab)  # tile front chain: lane-pair trade of 8-byte halves (HPNN_TILE_TRADE=1) vs plain stores (default)
+      HPNN_TILE_TRADE=1 step tr1 200 python bench.py --steps 200 --warmup 20 &&
+      step tr0 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_TRADE=1 step tr1b 200 python bench.py --steps 200 --warmup 20 &&
+      step tr0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_TRADE=1 step tr1c 200 python bench.py --steps 200 --warmup 20 &&
+      step tr0c 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_TRACE=1 step trace_tr0 200 python scripts/tile_trace.py ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
