@@ -93,7 +93,7 @@ constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool TRADE = false>
+          bool TRADE = false, bool XORD = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
      * 2k + e sit at bank group 4 e + g(k) (g = t32_g(2k): 0 1 0 1 2 3 2 3), so in-order
      * writes put each 8-lane ds_write_b128 group on 4 bank groups (2-way conflict); the
      * swapped order spreads it over all 8 */
-    const int xp = (xi >> 1) & 1;
+    const int xp = XORD ? (xi >> 1) & 1 : 0;
     const int xa0 = xoff[xp], xa1 = xoff[xp ^ 1];
     const char *xbase = (const char *)Xg + ((size_t)wave * NCB + xcbh) * CHUNK + (size_t)xi * XB;
 
@@ -543,6 +543,12 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
                                : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
         if (trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true>, 512);
+        /* HPNN_TILE_XORD=1 (A/B): X^T stage writes in a per-lane-pair order that spreads each
+         * 8-lane ds_write_b128 group over all 8 bank groups (LDS conflicts 60 % -> 18.5 %), but
+         * the selects cost more: 61.5 / 61.5 / 62.0 vs 60.7 / 60.3 / 61.3 us per step in row
+         * order (profiles/r4/xo_tile_xord_ab.txt) */
+        static const bool xord = [] { const char *e = getenv("HPNN_TILE_XORD"); return e && e[0] == '1'; }();
+        if (xord) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, true>, 512);
 #ifdef HPNN_ABLATIONS
         if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
         if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);

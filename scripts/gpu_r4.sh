@@ -122,6 +122,13 @@ for s in "$@"; do
       HPNN_TILE_TRADE=1 step tr1c 200 python bench.py --steps 200 --warmup 20 &&
       step tr0c 200 python bench.py --steps 200 --warmup 20 &&
       HPNN_TILE_TRACE=1 step trace_tr0 200 python scripts/tile_trace.py ;;
+    xordab)  # tile front X^T stage writes: per-lane-pair order (HPNN_TILE_XORD=1) vs row order (default)
+      HPNN_TILE_XORD=1 step xo1 200 python bench.py --steps 200 --warmup 20 &&
+      step xo0 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_XORD=1 step xo1b 200 python bench.py --steps 200 --warmup 20 &&
+      step xo0b 200 python bench.py --steps 200 --warmup 20 &&
+      HPNN_TILE_XORD=1 step xo1c 200 python bench.py --steps 200 --warmup 20 &&
+      step xo0c 200 python bench.py --steps 200 --warmup 20 ;;
     tnr) step tn_rruff 200 python scripts/tn_rruff_bench.py --splits 4,8,16,32 ;;
     widetr) HPNN_WIDE_TRACE=1 step wide_trace 200 python scripts/wide_bench.py ;;
     rehearse) step rehearse 400 bash scripts/gpu_rehearse.sh ;;
