@@ -164,7 +164,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
         const int row = 16 * xcbh + 2 * (xi & 7) + e;
         xoff[e] = wave * (XR * 64) + row * 64 + (((xg ^ t32_g(row)) & 3) << 4);
     }
-    /* write order: lanes k = xi & 7 with bit 1 set write their odd row first.  Lane k's rows
+    /* write order (XORD, HPNN_TILE_XORD=1; off by default: the selects measured slower than
+     * the conflicts): lanes k = xi & 7 with bit 1 set write their odd row first.  Lane k's rows
      * 2k + e sit at bank group 4 e + g(k) (g = t32_g(2k): 0 1 0 1 2 3 2 3), so in-order
      * writes put each 8-lane ds_write_b128 group on 4 bank groups (2-way conflict); the
      * swapped order spreads it over all 8 */

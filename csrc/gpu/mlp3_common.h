@@ -63,7 +63,9 @@ __device__ __forceinline__ char *wr_ptr(char *img, const LaneOff &lo, int r0, in
  * (same 16-byte chunk, same half).  Lanes whose row has bit 2 set trade with lane l ^ 16 --
  * same row, other 8-byte half of the same chunk (address ^ 8) -- through v_permlane16_swap,
  * so every group covers all slots.  Both lanes of a pair trade, so each byte is still
- * written / read once. */
+ * written / read once.  TRADE = false: the plain wr_ptr access -- what the tile front uses by
+ * default, since the shuffles measured slower than the conflicts they remove
+ * (profiles/r4/tr_tile_trade_ab.txt). */
 template <int R, bool TRADE = true>
 __device__ __forceinline__ void st_d4(char *img, const LaneOff &lo, int r0, int c0, bf16x4 v, int lane) {
     if constexpr (!TRADE) { /* plain wr_ptr store (2-way conflicts, no shuffles) */
