@@ -2,7 +2,9 @@
 # round-4 GPU call: steps by name, each under its own time limit; a crash / fault / timeout
 # (rc not 0 or 1) ends the call.   usage: scripts/gpu_r4.sh <tag> <step> [<step> ...]
 #   steps: tests | tests:<pytest -k expr> | smoke | bench | rruff | synth | synthrs | libbench | fpbench |
-#          learn | prof | prof_rruff
+#          learn | prof | prof0 | prof_rruff | fpsteps | pmc | pmc_rruff | trace | rehearse | dpforce |
+#          dpprof | A/B sets: mnistab rruffab rruffab2 earlyab dpab xchgab pfab xarb g0s rruffs t64ab
+#          tradeab xordab gsab synthab tnr widetr
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag=$1; shift
 O=gpurun_out/$tag; mkdir -p $O
