@@ -28,6 +28,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from hpnn_amd._lib import native  # noqa: E402
 from hpnn_amd.models import MLP  # noqa: E402
 from hpnn_amd.parallel import DataParallel, init_from_env  # noqa: E402
 
@@ -159,6 +160,13 @@ def main():
                 use_graph = bool(args.graph) and args.graph == 2
             dp.broadcast_parameters()
 
+    # the replicas must hold bitwise-identical weights after the first exchange (a sum that
+    # arrived in time but is wrong shows here, before anything is timed)
+    if dp.active and not dp.weights_consistent():
+        if rank == 0:
+            print("replica weights differ after the first step; no result reported", file=sys.stderr)
+        sys.exit(3)
+
     if use_graph:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -195,6 +203,10 @@ def main():
 
     run_steps(0, args.warmup)
     torch.cuda.synchronize()
+    if world > 1 and rank == world - 1 and native().fault_hit("weights"):
+        # test hook (HPNN_FAULT=weights:1): one replica's weights drift from the others'
+        m.W32[0].view(-1)[0] += 1.0
+        m.refresh_bf16()
     m.reset_stats()
     if world > 1:
         dist.barrier()
@@ -212,7 +224,11 @@ def main():
     # timed-region integrity: a barrier timeout inside a replayed xGMI all-reduce, or an
     # asynchronous RCCL error, leaves wrong sums behind without stopping the ranks -- every
     # rank re-checks its communicator and all must agree, else no number is reported
-    healthy = True
+    # in-kernel hand-offs (split-K tickets, tile pairs) must not have timed out: such a step
+    # used partial sums -- checked at N = 1 too
+    healthy = m.healthy()
+    if not healthy:
+        print(f"rank {rank}: an in-kernel hand-off timed out during the timed steps", file=sys.stderr)
     if dp.active:
         try:
             dp.check()
@@ -222,6 +238,9 @@ def main():
         if dp.native is not None and not dp.native.xar_healthy():
             healthy = False
         healthy = dp.all_ok(healthy)
+        if healthy and not dp.weights_consistent():
+            print(f"rank {rank}: replica weights differ after the timed steps", file=sys.stderr)
+            healthy = False
     if not healthy:
         if rank == 0:
             print("communication failed during the timed steps; no result reported", file=sys.stderr)

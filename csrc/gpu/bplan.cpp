@@ -5,6 +5,7 @@
 #include "bplan.h"
 
 #include <libhpnn.h>
+#include <libhpnn/comm.h>
 #include <libhpnn/devmem.h>
 #include <stdlib.h>
 #include <string.h>
@@ -226,6 +227,7 @@ int BPlan::bind(void *const *ptrs) {
 }
 
 BPlan::~BPlan() {
+    if (digest_) hpnn_dev_free(digest_);
     if (!owns_) return;
     for (void *p : ptr_)
         if (p) hpnn_dev_free(p);
@@ -374,6 +376,7 @@ int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipSt
     }
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
     u.cnt = g0cnt, u.err = g0cnt + 224;
+    u.fault = hpnn_fault_hit("handoff"); /* HPNN_FAULT=handoff:n: the n-th launch reports a timed-out wait */
     u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;
     u.mslab = midslab, u.mrows = mid_grid, u.mstride = slab_f, u.n12 = slab_f;
     for (int l = 0; l < 2; l++) {
@@ -588,6 +591,30 @@ int BPlan::health(hipStream_t s) {
         return -7;
     if (hipStreamSynchronize(s) != hipSuccess) return -7;
     return (e[0] || e[1] || e2) ? -9 : 0;
+}
+
+int BPlan::weights_digest(int which, unsigned long long *out, hipStream_t s) {
+    if (!digest_ && hpnn_dev_malloc((void **)&digest_, sizeof *digest_) != hipSuccess) return -7;
+    if (hipMemsetAsync(digest_, 0, sizeof *digest_, s) != hipSuccess) return -7;
+    long base = 0;
+    for (int l = 0; l < L; l++) {
+        const long n = (long)Np[l] * Kp[l];
+        int r = 0;
+        if (which & 1) {
+            if (!r) r = hpnn_hash_words(Wb[l], n * 2, base, digest_, s);
+            if (!r) r = hpnn_hash_words(Wt[l], n * 2, base + n / 2, digest_, s);
+            base += n;
+        }
+        if ((which & 2) && !r) {
+            r = hpnn_hash_words(W32[l], n * 4, base, digest_, s);
+            base += n;
+        }
+        if (r) return r;
+    }
+    if (hipMemcpyAsync(out, digest_, sizeof *out, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -7;
+    return 0;
 }
 
 int BPlan::read_stats(double *loss, unsigned int *hits, hipStream_t s) {

@@ -150,6 +150,9 @@ class BPlan {
     /* 0, or -9 when an in-kernel hand-over (wide front partials, fused G0 splits) timed out
      * since the plan was created (synchronises s) */
     int health(hipStream_t s);
+    /* 64-bit digest of the weights (bit 1: BF16 copies W / W^T of every layer, bit 2: the FP32
+     * masters); data-parallel replicas must agree on it bit for bit (synchronises s) */
+    int weights_digest(int which, unsigned long long *out, hipStream_t s);
     /* (loss sum, hits) summed over the stat slots (synchronises s) */
     int read_stats(double *loss, unsigned int *hits, hipStream_t s);
 
@@ -165,6 +168,7 @@ class BPlan {
   private:
     std::vector<void *> ptr_;
     bool owns_ = false;
+    unsigned long long *digest_ = nullptr; /* device word of weights_digest */
     int grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s);
     int g0_reduce(const XIn &x, hipStream_t s);
     int g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipStream_t s, float *gout = nullptr,

@@ -804,6 +804,24 @@ struct Batched {
     bool has_dpx() const { return (bool)dpx; }
     void detach_dpx() { dpx.reset(); }
 
+    /* FALSE when an in-kernel hand-off (fused G0 split-K tickets, fused TN tickets, the wide
+     * front's tile pair) timed out since the plan was made: that launch stepped with partial
+     * sums, so training must not go on from those weights (reference: CHK_ERR after every
+     * launch, common.h:324-335) */
+    BOOL healthy() {
+        if (p.health(s) == 0) return TRUE;
+        NN_ERROR(stderr, "batched GPU training: an in-kernel split-K / tile hand-off timed out "
+                         "(the step used partial sums); stopping\n");
+        return FALSE;
+    }
+    /* digest of the weights every data-parallel replica must hold bit for bit: the BF16 copies,
+     * plus the FP32 masters unless the BF16 reduce-scatter step keeps them sharded */
+    BOOL digest(unsigned long long *d) {
+        bool sh = false;
+        for (int l = 0; dpx && l < L; l++) sh = sh || dpx->sharded(l);
+        return p.weights_digest(sh ? 1 : 3, d, s) == 0;
+    }
+
     /* FP32 master weights (and BPM momentum, into k->dw) -> host FP64 */
     BOOL download(kernel_ann *k) {
         HIPCHK(hipStreamSynchronize(s));
@@ -893,6 +911,7 @@ struct BatchedFP {
 
     ~BatchedFP() {
         if (s) hipStreamSynchronize(s);
+        if (dig) hpnn_dev_free(dig);
         for (int l = 0; l < 16; l++) {
             hpnn_dev_free(W[l]);
             hpnn_dev_free(V[l]);
@@ -1063,6 +1082,19 @@ struct BatchedFP {
     BOOL dp_step(const XSet &, long, const T *, int, int, int, double, double) { return FALSE; }
     int xchg_step(const XSet &, long, const T *, int, int, double, double, double, hpnn_xar *) { return -1; }
     BOOL gather_masters() { return TRUE; }
+    BOOL healthy() { return TRUE; } /* no in-kernel hand-offs in the FP64 / FP32 kernels */
+    unsigned long long *dig = nullptr; /* device word of digest() */
+    BOOL digest(unsigned long long *d) {
+        if (!dig && hpnn_dev_malloc((void **)&dig, 8) != hipSuccess) return FALSE;
+        if (hipMemsetAsync(dig, 0, 8, s) != hipSuccess) return FALSE;
+        long base = 0;
+        for (int l = 0; l < L; l++) {
+            const long nb = (long)N[l] * M[l] * (long)sizeof(T);
+            if (hpnn_hash_words(W[l], nb, base, dig, s) != 0) return FALSE;
+            base += nb / 4;
+        }
+        return hipMemcpyAsync(d, dig, 8, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+    }
     bool has_dpx() const { return false; }
     void detach_dpx() {}
 
@@ -1252,6 +1284,8 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
         auto g = graphs.find(ne);
         ok = (g != graphs.end() && g->second) ? hipGraphLaunch(g->second, s) == hipSuccess : epochs(ne);
         e += ne;
+        /* hand-off health after every replay (<= ~32 steps): one 12-byte readback */
+        if (ok) ok = net.healthy();
         if (ok && (metrics || e == E)) ok = net.read_stats(&ep_loss, &ep_hits);
         if (ok && metrics)
             hpnn_metrics_epoch("gpu", o->epoch0 + e, ep_loss / (double)n, ep_hits, n,
@@ -1469,7 +1503,7 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
             hipSetDevice(dev[g]);
             double l = 0.0;
             unsigned int h = 0;
-            ok = nets[g]->read_stats(&l, &h);
+            ok = nets[g]->read_stats(&l, &h) && nets[g]->healthy();
             ep_loss += l;
             ep_hits += h;
         }
@@ -1664,22 +1698,37 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         if (!ok) break;
         double l = 0.0;
         unsigned int h = 0;
-        ok = net.read_stats(&l, &h);
+        ok = net.read_stats(&l, &h) && net.healthy();
         if (ok) ok = use_xar ? hpnn_xar_status(xar) == 0 && (!xark || hpnn_xar_status(xark) == 0)
                              : hpnn_comm_check(comm) == 0;
+        /* replicas must hold bitwise-identical weights: a wrong-but-timely exchange (a sum that
+         * arrived in time but is not every rank's) shows here, after the first epoch and the last */
+        unsigned long long dig = 0;
+        const bool check_dig = e == 0 || e + 1 == o->epochs;
+        if (ok && check_dig && !net.digest(&dig)) ok = FALSE;
+        if (ok && check_dig && R == W - 1 && hpnn_fault_hit("digest")) dig ^= 1; /* test hook */
         struct {
             double loss;
+            unsigned long long digest;
             unsigned int hits, ok;
-        } mine = {l, h, (unsigned)ok}, *every = new decltype(mine)[W];
+        } mine = {l, dig, h, (unsigned)ok}, *every = new decltype(mine)[W];
         if (hpnn_boot_allgather(&mine, sizeof mine, every) != 0) ok = FALSE;
         ep_loss = 0.0;
         ep_hits = 0;
+        bool same = true;
         for (int r = 0; r < W && ok; r++) {
             ep_loss += every[r].loss;
             ep_hits += every[r].hits;
             ok = ok && every[r].ok;
+            same = same && every[r].digest == every[0].digest;
         }
         delete[] every;
+        if (ok && check_dig && !same) {
+            if (R == 0)
+                NN_ERROR(stderr, "data-parallel training: the replicas' weights differ after epoch %u "
+                                 "(exchange error); stopping\n", e + 1);
+            ok = FALSE;
+        }
         if (ok && hpnn_metrics_active())
             hpnn_metrics_epoch("gpu-dp-mp", o->epoch0 + e + 1, ep_loss / (double)n, ep_hits, n,
                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),

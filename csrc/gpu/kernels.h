@@ -100,7 +100,7 @@ int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_u8, float h
 typedef struct {
     float *W32, *V32; /* layer 0 [N][M] FP32 master / momentum (V32 NULL for BP) */
     void *Wb, *Wt, *Wf; /* BF16 W [N][M], W^T [M][N], fragment-major copy (may be NULL) */
-    unsigned int *cnt;  /* 256 words, zeroed once: tile counters (monotonic) */
+    unsigned int *cnt;  /* 256 words, zeroed once: 64-bit tile counters, 32 words apart (monotonic) */
     unsigned int *err;  /* set when a wait for the other splits timed out */
     float lr, alpha, scale;
     int momentum;
@@ -124,13 +124,26 @@ typedef struct {
      * peers' copies in rank order and steps those elements (scale includes 1 / world) */
     int xchg; /* 1 one-shot, 2 two-shot (each rank reduces 1 / world of every slice, then gathers) */
     hpnn_xar_view xv;
-    int proto; /* hand-off diagnostics (HPNN_G0_PROTO): 1 producer agent release, 2 consumer agent
-                * acquire, 4 system-scope (sc0 sc1) partial loads */
+    int proto; /* hand-off diagnostics (HPNN_G0_PROTO, make ABLATIONS=1 builds only): 1 producer agent
+                * release, 2 consumer agent acquire, 4 system-scope (sc0 sc1) partial loads, 8 system
+                * acquire after the exchange barrier, 16 no exchange barrier, 64 no W / V prefetch */
+    int fault; /* test hook (HPNN_FAULT=handoff:n): the split-K wait of that launch reports a
+                * timeout (sets *err) as a real one would */
 } hpnn_g0_update;
 int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,
                                int M, int Bt, int splits, const hpnn_g0_update *u, hipStream_t stream);
-/* 1 when hpnn_gemm_fm_direct_update covers the shape (launch-free check) */
+/* 1 when hpnn_gemm_fm_direct_update covers the shape (launch-free check), including the
+ * residency its in-kernel hand-offs need: every workgroup of the grid co-resident */
 int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits);
+/* workgroups of `kernel` (threads per workgroup, dynamic LDS bytes) the device can hold at once:
+ * the occupancy API's blocks per CU x CUs (cached per kernel).  Kernels whose workgroups wait
+ * for each other inside one launch (split-K tickets, tile-pair hand-offs, the in-kernel DP
+ * exchange) refuse grids above it: the first wave of workgroups would spin on partners that
+ * cannot be scheduled until the wait times out. */
+int hpnn_resident_capacity(const void *kernel, int threads, size_t dyn_lds);
+/* *out += order-independent 64-bit digest of the nbytes / 4 words at p (word index offset by
+ * base, so several buffers can be folded into one digest); *out must be initialised */
+int hpnn_hash_words(const void *p, long nbytes, long base, unsigned long long *out, hipStream_t stream);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)

@@ -483,18 +483,9 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
                     }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
-            unsigned int *cnt = upd.cnt + 32 * tile;
-            const unsigned int old = atomicAdd(cnt, 1u);
-            const unsigned int want = old - old % (unsigned)splits + (unsigned)splits;
-            const unsigned long long t0 = wall_clock64();
-            while ((int)(__hip_atomic_load((hpnn::gu32 *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > TN8_TIMEOUT) {
-                    __hip_atomic_store((hpnn::gu32 *)upd.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
+        if (tid == 0) { /* 64-bit tickets (mfma_common.h): no wrap */
+            const unsigned long long want = hpnn::ticket_arrive(upd.cnt + 32 * tile, (unsigned)splits);
+            hpnn::ticket_wait(upd.cnt + 32 * tile, want, upd.err, TN8_TIMEOUT);
         }
         __syncthreads();
         constexpr int NE4 = 256 * 256 / 4;
@@ -743,13 +734,15 @@ extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int l
 
 /* the same step for a gradient over `splits` splits (>= 2), reduced inside the launch
  * (MODE 2 above): slab is the scratch the partials are published through ([splits][N][M]).
- * -1: shape not covered, or more workgroups than CUs (every split of a tile must be
- * resident at once), or HPNN_TN8_FUSED=0. */
+ * -1: shape not covered, or more workgroups than the device holds at once (every split of a
+ * tile waits for the others: hpnn_resident_capacity), or HPNN_TN8_FUSED=0. */
 extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt,
                                           int splits, float *slab, float *W32, float *V32, void *Wbf, void *Wt,
                                           float lr, float alpha, float scale, int momentum, unsigned int *cnt,
                                           unsigned int *err, hipStream_t stream) {
     static const bool on = [] { const char *e = getenv("HPNN_TN8_FUSED"); return !(e && e[0] == '0'); }();
+    /* every split of a tile waits for the others: the whole grid must be resident at once */
+    static const int cap = hpnn_resident_capacity((const void *)gemm_tn8_kernel<2>, 512, 0);
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -763,11 +756,11 @@ extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H,
     const int units = Bt / 64;
     if (units % splits || (units / splits) % 2) return -1;
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    /* tickets: 32 words apart in 1024 (a block the caller keeps for this GEMM shape: the
+    /* 64-bit tickets: 32 words apart in 1024 (a block the caller keeps for this GEMM shape: the
      * counters are monotonic, every launch must add `splits` per tile); at least min_wg workgroups (HPNN_TN8_MINWG, default
      * half the CUs: fewer splits leave the chip idle while each reduces a larger share) */
     static const int min_wg = [] { const char *e = getenv("HPNN_TN8_MINWG"); return e ? atoi(e) : 0; }();
-    if (ntiles > 31 || ntiles * splits > cus || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;
+    if (ntiles > 31 || ntiles * splits > cap || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;
     const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, cnt, err};
     hipLaunchKernelGGL(gemm_tn8_kernel<2>, dim3(ntiles * splits), dim3(512), 0, stream, (const __bf16 *)D, ldd,
                        (const __bf16 *)H, ldh, slab, M, N, units, splits, tiles_n, ntiles, hpnn::TnTail{}, u);

@@ -45,6 +45,13 @@
 
 namespace {
 
+/* HPNN_G0_PROTO hand-off diagnostics exist only in make ABLATIONS=1 builds */
+#ifdef HPNN_ABLATIONS
+#define G0_PROTO(u, bit) ((u).proto & (bit))
+#else
+#define G0_PROTO(u, bit) 0
+#endif
+
 using hpnn::bf16x8;
 using hpnn::f32x4;
 using hpnn::TnTail;
@@ -342,7 +349,7 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
     auto barrier = [&](int which) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t < v.world && !(u.proto & 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
+        if (t < v.world && !G0_PROTO(u, 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
             unsigned int *const mine = which ? HPNN_XAR_FLAG_B(v.sig[v.rank], b, t) : HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
             __hip_atomic_store(which ? HPNN_XAR_FLAG_B(v.sig[t], b, v.rank) : HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -357,7 +364,7 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
             }
         }
         __syncthreads();
-        if (u.proto & 8) /* diagnostics: the invalidating system acquire as well */
+        if (G0_PROTO(u, 8)) /* diagnostics: the invalidating system acquire as well */
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     };
     auto g0_off = [&](int c) { return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4)); };
@@ -437,7 +444,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
     const long nb = (long)tiles * splits, nf = u.n12 / 4;
     const long c0 = blockIdx.x * nf / nb, c1 = (blockIdx.x + 1) * nf / nb;
-    const bool steps = !u.gout || u.xchg, pf = steps && !(u.proto & 64);
+    const bool steps = !u.gout || u.xchg, pf = steps && !G0_PROTO(u, 64);
     Pre4 pg0 = {}, pg12 = {};
     if (pf && t < 128 && e0 + t < e1) {
         const int e = e0 + t, row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
@@ -460,29 +467,21 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    __shared__ unsigned int want_s;
+    __shared__ unsigned long long want_s;
     if (t == 0) {
-        if (u.proto & 1) {
+        if (G0_PROTO(u, 1)) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        const unsigned int old = atomicAdd(u.cnt + 32 * tile, 1u);
-        want_s = old - old % (unsigned)splits + (unsigned)splits; /* this launch's last ticket */
+        want_s = hpnn::ticket_arrive(u.cnt + 32 * tile, (unsigned)splits); /* this launch's last ticket */
     }
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
     g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
     if (t == 0) {
-        unsigned int *cnt = u.cnt + 32 * tile;
-        const unsigned int want = want_s;
-        const unsigned long long t0 = wall_clock64();
-        while ((int)(__hip_atomic_load((gu32 *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > G0_TIMEOUT) {
-                __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        if (u.proto & 2) {
+        /* fault hook: this launch reports a timed-out wait (and, like one, reduces what is there) */
+        if (u.fault) __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else hpnn::ticket_wait(u.cnt + 32 * tile, want_s, u.err, G0_TIMEOUT);
+        if (G0_PROTO(u, 2)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -499,7 +498,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
         if (e < e1) {
             const float *p = slab + (size_t)(nt0 + row) * ldg + col;
-            if (u.proto & 4)
+            if (G0_PROTO(u, 4))
                 for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8<true>(p + (size_t)s * ss, ss, s1 - s);
             else
                 for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
@@ -560,18 +559,37 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
 
 }  // namespace
 
+/* the fused G0 grid (tiles x splits workgroups of 512 threads) fits on the device at once;
+ * both instantiations checked (they differ only in the operand conversion) */
+static bool g0_fused_resident(int blocks) {
+    static const int cap = [] {
+        const int a = hpnn_resident_capacity((const void *)g0_fused_kernel<5, 4, 1, 2, true>, 512, 0);
+        const int b = hpnn_resident_capacity((const void *)g0_fused_kernel<5, 4, 1, 2, false>, 512, 0);
+        return a < b ? a : b;
+    }();
+    return blocks <= cap;
+}
+
+static bool g0_fused_on() {
+    static const bool on = [] { const char *e = getenv("HPNN_G0_FUSED"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab,
                                           int ldg, int N, int M, int Bt, int splits, const hpnn_g0_update *u,
                                           hipStream_t stream) {
-    static const bool on = [] { const char *e = getenv("HPNN_G0_FUSED"); return !(e && e[0] == '0'); }();
     /* the 160 x 128 tile configuration of fm_dispatch (8 waves) */
-    if (!on || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
+    if (!g0_fused_on() || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
     if (!u->cnt || !u->err) return -1;
     const bool steps = !u->gout || u->xchg;
     if (u->n12 % 4 || !u->mslab || u->mrows < 1 || (steps && u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
         return -2;
     const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
-    if (tiles > 7) return -1; /* counters 32 words apart in a 256-word block, err at word 224 */
+    if (tiles > 7) return -1; /* 64-bit counters 32 words apart in a 256-word block, err at word 224 */
+    /* every workgroup waits for the other splits of its tile: all must be resident at once
+     * (more splits than that, e.g. forced by HPNN_TN_SPLITS, take the slab form instead of
+     * stalling to the timeout) */
+    if (!g0_fused_resident(tiles * splits)) return -1;
     if (u->xchg) {
         /* the exchange buffer holds [G0 | G1 | G2]; one epoch / flag slot per workgroup */
         if (tiles * splits > HPNN_XAR_MAX_BLOCKS || u->xv.world < 1 || u->xv.world > HPNN_XAR_MAX_RANKS ||
@@ -581,9 +599,11 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
             if (!u->xv.buf[p] || !u->xv.sig[p]) return -1;
     }
     const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
-    static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
     hpnn_g0_update uu = *u;
+#ifdef HPNN_ABLATIONS
+    static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
     uu.proto |= proto;
+#endif
 #define HPNN_G0F(U8_)                                                                                              \
     hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_>), dim3(tiles * splits), dim3(512), 0, stream,              \
                        (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
@@ -595,9 +615,10 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
 }
 
 extern "C" int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits) {
-    static const bool on = [] { const char *e = getenv("HPNN_G0_FUSED"); return !(e && e[0] == '0'); }();
-    return on && M % 160 == 0 && N % 128 == 0 && Bt % 32 == 0 && splits >= 1 && splits <= Bt / 32 && ldg == M &&
-           (M / 160) * (N / 128) <= 7;
+    if (!(g0_fused_on() && M % 160 == 0 && N % 128 == 0 && Bt % 32 == 0 && splits >= 1 && splits <= Bt / 32 &&
+          ldg == M && (M / 160) * (N / 128) <= 7))
+        return 0;
+    return g0_fused_resident((M / 160) * (N / 128) * splits) ? 1 : 0;
 }
 
 extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,

@@ -22,6 +22,10 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "kernels.h"
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -862,6 +866,54 @@ inline int grid_for(long n, int bs) {
 static bool od_wave_mode() {
     static const bool v = [] { const char *e = getenv("HPNN_OD_WAVE"); return e && e[0] == '1'; }();
     return v;
+}
+
+/* order-independent 64-bit digest of a buffer's 4-byte words: the wrapping sum over i of a
+ * murmur3 finalizer of (word << 32 | i).  Equal buffers give equal digests on every device
+ * and run (integer adds commute); one changed bit changes it.  Used to check that data-
+ * parallel replicas hold bitwise-identical weights (bench.py, train_nn under a launcher). */
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+__global__ __launch_bounds__(256) void hash_words_kernel(const unsigned int *__restrict__ w, long n, long base,
+                                                         unsigned long long *__restrict__ out) {
+    unsigned long long h = 0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        h += mix64(((unsigned long long)w[i] << 32) ^ (unsigned long long)(i + base) ^ 0x9e3779b97f4a7c15ull);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
+}
+
+extern "C" int hpnn_hash_words(const void *p, long nbytes, long base, unsigned long long *out, hipStream_t stream) {
+    if (!p || !out || nbytes < 0 || nbytes % 4) return -1;
+    const long n = nbytes / 4;
+    if (n == 0) return 0;
+    long blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(hash_words_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const unsigned int *)p, n,
+                       base, out);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_resident_capacity(const void *kernel, int threads, size_t dyn_lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void *, int, size_t>, int> cache;
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_tuple(kernel, threads, dyn_lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, dyn_lds) != hipSuccess)
+        cus = per = 0; /* unknown: no grid counts as resident (callers take their other forms) */
+    return cache[key] = cus * per;
 }
 
 extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ldt, const int *labels, float t_hi,

@@ -560,6 +560,9 @@ int launch_wide(const hpnn_wide2_args &a, hipStream_t stream) {
         attr[ti] = true;
     }
     const int n_tiles = a.Bp / TS;
+    /* KSPLIT 2: the two workgroups of a tile wait for each other -- the grid must be resident */
+    if constexpr (KSPLIT == 2)
+        if (n_tiles * KSPLIT > hpnn_resident_capacity((const void *)kern, 512, LDS_TOTAL)) return -6;
     hipLaunchKernelGGL(kern, dim3(n_tiles * KSPLIT), dim3(512), LDS_TOTAL, stream, (const __bf16 *)a.X, a.ldx,
                        (const __bf16 *)a.W0, a.K0, (const __bf16 *)a.W1, (const __bf16 *)a.W1t, a.labels, a.T, a.ldt,
                        a.t_hi, a.t_lo, (__bf16 *)a.H0, (__bf16 *)a.D2, (__bf16 *)a.D1, (f32x4 *)a.pbuf, a.cnt,
@@ -586,8 +589,15 @@ extern "C" int hpnn_wide2_ksplit(int Bp, int K0) {
     static const int forced = [] { const char *e = getenv("HPNN_WIDE_KSPLIT"); return e ? atoi(e) : 0; }();
     if (Bp <= 0 || Bp % TS) return 0;
     if (K0 != 4096) return 0;
-    if (forced == 1 || forced == 2) return forced;
-    return 2;
+    if (forced == 1) return 1;
+    /* the tile pair's hand-off needs every workgroup of the grid resident at once: larger
+     * batches take the one-workgroup-per-tile form */
+    static const int cap = [] {
+        (void)hipFuncSetAttribute((const void *)wide2_kernel<2, true, 32, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_TOTAL);
+        return hpnn_resident_capacity((const void *)wide2_kernel<2, true, 32, 2>, 512, LDS_TOTAL);
+    }();
+    return 2 * (Bp / TS) <= cap ? 2 : 1;
 }
 
 extern "C" long hpnn_wide2_pbuf_bytes(int Bp) { return (long)(Bp / TS) * 8 * 16 * 64 * 16; }

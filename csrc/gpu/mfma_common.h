@@ -299,6 +299,39 @@ __device__ __forceinline__ f32x4 sum_sc1_x8(const float *p, size_t ss, int n) {
     return g;
 }
 
+/* Split-K arrival tickets: one monotonic 64-bit counter per output tile; every launch adds
+ * `splits` tickets to it (one per workgroup of the tile), and a workgroup waits until the last
+ * ticket of its own launch has arrived: want = old - old % splits + splits.  The counter is
+ * 64-bit because that target is only right while the counter has not wrapped: a 32-bit
+ * counter wraps after 2^32 / splits launches (89M at 48 splits, ~1.5 h of MNIST steps), and
+ * since 2^32 is not a multiple of 48 every launch after the wrap would compute a wrong target
+ * (reducing partial sums, or stalling to the timeout).  At 64 bits the wrap is ~10^10 years of
+ * steps away.  Protocol (gfx950 guide, hand-off table row 1): the workgroup's partials are
+ * stored sc1 and drained (vmcnt(0) in every storing wave, then the workgroup barrier) before
+ * ONE lane takes the ticket (agent-scope atomic add); the waiter polls with relaxed
+ * agent-scope (sc1) loads and its workgroup reads the partials with sc1 loads after a
+ * barrier.  The wait is bounded: on timeout it sets *err (read back by BPlan::health) and
+ * returns false. */
+__device__ __forceinline__ unsigned long long ticket_arrive(unsigned int *cnt32, unsigned int splits) {
+    unsigned long long *cnt = (unsigned long long *)cnt32;
+    const unsigned long long old = atomicAdd(cnt, 1ull);
+    return old - old % splits + splits;
+}
+__device__ __forceinline__ bool ticket_wait(unsigned int *cnt32, unsigned long long want, unsigned int *err,
+                                            unsigned long long timeout) {
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    gu64 *cnt = (gu64 *)cnt32;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > timeout) {
+            __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+
 /* Optional tail work of a TN launch: a grouped slab reduction (reduce_groups_kernel of
  * kernels_mlp3.hip: out[g*ostride + i] = sum of slabs [g*SG, min(S, (g+1)*SG)), float4 i)
  * run by extra workgroups appended to the GEMM grid.  The fused MNIST step reduces its

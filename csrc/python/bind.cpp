@@ -168,6 +168,12 @@ void bind_plan(py::module_ &m) {
                  check(p.update_flat((const float *)P(G), lr, alpha, scale, S(s)), "BPlan.update_flat");
              })
         .def("health", [](BPlan &p, uptr s) { return p.health(S(s)); })
+        .def("weights_digest",
+             [](BPlan &p, int which, uptr s) {
+                 unsigned long long d = 0;
+                 check(p.weights_digest(which, &d, S(s)), "weights_digest");
+                 return d;
+             })
         .def_readwrite("g0_fused", &BPlan::g0_fused)
         .def_readwrite("tn_update", &BPlan::tn_update)
         .def("tn_update_ok", &BPlan::tn_update_ok)

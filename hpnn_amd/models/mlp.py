@@ -381,6 +381,27 @@ class MLP:
         ops.output_delta(self.Z, self.n_out, self.type, self.D[-1], T=Tz, n_valid=n_valid, O=O)
         return O[:n_valid, :self.n_out]
 
+    def healthy(self):
+        """False when an in-kernel hand-off (the fused G0's split-K tickets, a fused TN
+        gradient's tickets, the wide front's tile pair) timed out since the model was made:
+        that step used partial sums (synchronises the current stream)."""
+        if not self._gpu:
+            return True
+        return self.plan.health(_stream()) == 0
+
+    def weights_digest(self, which=3):
+        """64-bit digest of the weights (1: BF16 copies, 2: FP32 masters, 3: both); data-
+        parallel replicas hold bitwise-identical weights, so equal digests (synchronises)."""
+        if self._gpu:
+            return int(self.plan.weights_digest(int(which), _stream()))
+        h = 0
+        for l in range(self.L):
+            ts = ([self.Wb[l], self.Wt[l]] if which & 1 else []) + ([self.W32[l]] if which & 2 else [])
+            for t in ts:
+                h = (h * 1000003 + hash(t.contiguous().view(-1).view(torch.int16 if t.element_size() == 2
+                                                                    else torch.int32).cpu().numpy().tobytes())) % (1 << 64)
+        return h
+
     def reset_stats(self):
         self.stats.zero_()
 

@@ -135,6 +135,19 @@ class DataParallel:
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return bool(t.item())
 
+    def weights_consistent(self):
+        """True when every replica holds bitwise-identical weights (digest all-gathered):
+        catches an exchange that completed in time but summed the wrong data.  BF16 copies
+        only when the sharded optimizer keeps the FP32 masters split over the ranks."""
+        d = self.m.weights_digest(1 if self.sharded else 3)
+        if not self.active or self.world == 1:
+            return True
+        dev = self.m.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        mine = torch.tensor([d & 0xFFFFFFFF, d >> 32], dtype=torch.int64, device=dev)
+        every = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(every, mine, group=self.group)
+        return all(torch.equal(e, every[0]) for e in every)
+
     def _bucket_view(self, layers):
         lo, hi = min(layers), max(layers)
         m = self.m

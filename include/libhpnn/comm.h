@@ -102,7 +102,9 @@ void hpnn_comm_abort(hpnn_comm *c);
 int hpnn_comm_all_ok(hpnn_comm *c, int ok, hipStream_t stream);
 
 /* fault injection for tests: HPNN_FAULT=<site>:<n>[,<site>:<n>] makes the n-th
- * (1-based) event at `site` fail (sites: comm, sample, load, nan, stop); returns 1
+ * (1-based) event at `site` fail (sites: comm, sample, load, nan, stop; handoff: a fused
+ * split-K launch reports a timed-out wait; digest / weights: one replica's weight digest /
+ * weights differ, in train_nn / bench.py); returns 1
  * when it fires */
 int hpnn_fault_hit(const char *site);
 

@@ -18,14 +18,15 @@ NAMES = ["W1 DMA issue", "prologue (X(0), W0 ring)", "phase A (25 k-steps)", "H1
 
 def main():
     assert os.environ.get("HPNN_TILE_TRACE") == "1"
+    nd = int(sys.argv[1]) if len(sys.argv) > 1 else 4  # distinct batches cycled (1: X stays in the Infinity Cache)
     dev = torch.device("cuda")
     m = MLP([784, 128, 64, 10], "SNN", batch=65536, momentum=True, fused="t")
-    Xs = [m.prepare_input(torch.randint(0, 256, (m.Bp, 784), dtype=torch.uint8, device=dev)) for _ in range(4)]
+    Xs = [m.prepare_input(torch.randint(0, 256, (m.Bp, 784), dtype=torch.uint8, device=dev)) for _ in range(nd)]
     lab = torch.randint(0, 10, (m.Bp,), device=dev, dtype=torch.int32)
     for i in range(12):
-        m.train_step(Xs[i % 4], labels=lab)
+        m.train_step(Xs[i % nd], labels=lab)
     torch.cuda.synchronize()
-    m._fused_front(Xs[1], labels=lab, T=None, n_valid=m.Bp)
+    m._fused_front(Xs[1 % nd], labels=lab, T=None, n_valid=m.Bp)
     torch.cuda.synchronize()
     G = m.midslab.shape[0]
     t = torch.tensor(native().mlp3_tile_trace(), dtype=torch.float64).view(1024, 12)[:G]
