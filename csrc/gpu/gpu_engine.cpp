@@ -1170,8 +1170,12 @@ extern "C" BOOL hpnn_gpu_train_batched(kernel_ann *k, const DOUBLE *X, const DOU
         if (dt == NN_DTYPE_F32) return train_dp<BatchedFP<float>>(k, X, T, n, o, st, lbr, true);
         return train_dp<BatchedFP<double>>(k, X, T, n, o, st, lbr, true);
     }
-    /* one process per GPU under a launcher (torchrun --no-python bin/train_nn ...) */
-    if (hpnn_boot_world() > 1 && !(nd && nd[0] == '0')) {
+    /* one process per GPU under a launcher (torchrun --no-python bin/train_nn ...);
+     * HPNN_DP_FORCE=1: the same path with ONE rank under a launcher (its step structure and
+     * exchange kernels timed on a single GPU, as bench.py's HPNN_DP_FORCE) */
+    const char *dpf = getenv("HPNN_DP_FORCE");
+    const bool dp_one = dpf && dpf[0] == '1' && getenv("LOCAL_WORLD_SIZE") && hpnn_boot_world() == 1;
+    if ((hpnn_boot_world() > 1 || dp_one) && !(nd && nd[0] == '0')) {
         if (dt == NN_DTYPE_BF16) return train_dp_mp<Batched>(k, X, T, n, o, st);
         if (dt == NN_DTYPE_F32) return train_dp_mp<BatchedFP<float>>(k, X, T, n, o, st);
         return train_dp_mp<BatchedFP<double>>(k, X, T, n, o, st);
@@ -1551,7 +1555,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                  hpnn_batched_stats *st) {
     typedef typename Net::target_t TT;
     const int W = hpnn_boot_world(), R = hpnn_boot_rank();
-    if (k->n_hiddens + 1 > 16 || W < 2 || W > 64) return FALSE;
+    if (k->n_hiddens + 1 > 16 || W < 1 || W > 64) return FALSE;
     hpnn_gpu_sync_host(k);
     const int dev = hpnn_rt_device(0);
     HIPCHK(hipSetDevice(dev));
@@ -1642,9 +1646,12 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
-    for (UINT e = 0; e < o->epochs && ok; e++) {
-        ok = hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) == hipSuccess;
-        for (int b = 0; b < n_batches && ok; b++) {
+    /* one epoch's steps: the same launches on every rank, every epoch (the minibatch order is
+     * fixed), so from the second epoch on they replay as ONE HIP graph per epoch -- the
+     * launches bench.py times (the first epoch runs eagerly: it settles the exchange form) */
+    auto epoch_steps = [&](UINT e) -> bool {
+        if (hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess) return false;
+        for (int b = 0; b < n_batches; b++) {
             const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
             const int start = b * B + R * Bg;
             int nv = end - start;
@@ -1652,7 +1659,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             const TT *tb = Td + (size_t)start * n_out;
             const int total = end - b * B;
             if (net.has_dpx()) {
-                ok = net.dp_step(Xd, start, tb, n_out, nv, total, o->lr, o->alpha);
+                if (!net.dp_step(Xd, start, tb, n_out, nv, total, o->lr, o->alpha)) return false;
                 continue;
             }
             if (xark) {
@@ -1666,18 +1673,17 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                 }
                 if (r != -1) {
                     NN_ERROR(stderr, "data-parallel fused step failed: %d\n", r);
-                    ok = FALSE;
-                    break;
+                    return false;
                 }
                 /* not covered (same on every rank): the all-reduce launch from here on */
                 hpnn_xar_destroy(xark);
                 xark = nullptr;
             }
+            bool okb;
             if (use_xar) {
                 /* small gradients: ONE latency-bound xGMI all-reduce of the whole buffer */
-                ok = net.grads(Xd, start, tb, n_out, nv);
-                if (!ok) break;
-                ok = hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s) == 0;
+                okb = net.grads(Xd, start, tb, n_out, nv) &&
+                      hpnn_xar_all_reduce_f32(xar, (float *)net.gflat, (float *)net.gflat, (long)count, s) == 0;
             } else {
                 /* RCCL: one bucket per layer on the side stream as soon as it is final
                  * (overlapping the backward of the layers below); the update joins them */
@@ -1688,13 +1694,33 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                     return hpnn_comm_all_reduce_async(comm, net.gflat + net.goff[lo],
                                                       (long)(net.goff[hi + 1] - net.goff[lo]), Net::comm_dt, s) == 0;
                 };
-                ok = net.grads(Xd, start, tb, n_out, nv, ready);
+                okb = net.grads(Xd, start, tb, n_out, nv, ready);
                 for (size_t i = issued; i < seq.size(); i++) ready(seq[i].first, seq[i].second);
-                ok = (hpnn_comm_join(comm, s) == 0) && ok;
+                okb = (hpnn_comm_join(comm, s) == 0) && okb;
             }
-            if (ok) ok = net.update_flat(net.gflat, o->lr, o->alpha, 1.0 / (double)(total > 0 ? total : 1),
-                                         mom);
+            if (!okb || !net.update_flat(net.gflat, o->lr, o->alpha, 1.0 / (double)(total > 0 ? total : 1), mom))
+                return false;
         }
+        return true;
+    };
+    hipGraphExec_t gx = nullptr;
+    for (UINT e = 0; e < o->epochs && ok; e++) {
+        if (e == 1 && graphs_enabled() && n_batches <= 4096) {
+            /* every rank captures; all replay only if all captured (a failed capture ran
+             * nothing, so eager epochs stay in step) */
+            int cap = capture_epoch(s, [&]() { return epoch_steps(e); }, &gx) ? 1 : 0;
+            std::vector<int> caps(W);
+            if (hpnn_boot_allgather(&cap, sizeof cap, caps.data()) != 0) ok = FALSE;
+            for (int v : caps) cap = cap && v;
+            if (!cap && gx) {
+                hipGraphExecDestroy(gx);
+                gx = nullptr;
+            }
+            if (ok && R == 0)
+                NN_OUT(stdout, "data-parallel epochs: %s\n", gx ? "HIP graph replays" : "eager launches (capture failed)");
+        }
+        if (!ok) break;
+        ok = gx ? hipGraphLaunch(gx, s) == hipSuccess : epoch_steps(e);
         if (!ok) break;
         double l = 0.0;
         unsigned int h = 0;
@@ -1735,6 +1761,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
                                (UINT64)n * (e + 1));
     }
     auto t1 = std::chrono::steady_clock::now();
+    if (gx) hipGraphExecDestroy(gx);
     if (ok) ok = net.gather_masters(); /* bf16rs: every rank's rows of the FP32 masters */
     if (ok) ok = net.download(k);
     if (ok && st) {

@@ -14,7 +14,7 @@
 #   prof / prof_rruff     rocprofv3 kernel table (--graph 0)
 #   pmc / pmc_rruff       PMC passes of the step (scripts/pmc_step.sh)
 #   rehearse              2 ranks sharing the GPU (scripts/rehearse.sh)
-#   libbench              train_nn vs bench.py (scripts/lib_vs_bench.py)
+#   libbench / libbench_dp   train_nn vs bench.py (scripts/lib_vs_bench.py; _dp: the N > 1 path, one rank)
 #   learn                 scripts/learnability.py
 #   cache                 headline with 4 vs 8 cycled batches (Infinity-Cache sensitivity)
 #   py:<script args>      python scripts/<script> <args> (spaces as ',')
@@ -64,6 +64,7 @@ for spec in "$@"; do
     pmc_rruff) PMC_TAG=_${tag}_rruff step pmc_rruff 600 bash scripts/pmc_step.sh --model rruff ;;
     rehearse) step rehearse 600 bash scripts/gpu_rehearse.sh ;;
     libbench) step libbench 900 python scripts/lib_vs_bench.py --out $O/lib_vs_bench.jsonl ;;
+    libbench_dp) step libbench_dp 900 python scripts/lib_vs_bench.py --dpforce --configs mnist --out $O/lib_vs_bench_dp.jsonl ;;
     learn) step learn 600 python scripts/learnability.py --out $O/learnability.jsonl ;;
     cache) step cache_d1 300 python bench.py --steps 200 --warmup 20 --datasets 1 &&
            step cache_d4 300 python bench.py --steps 200 --warmup 20 --datasets 4 &&

@@ -28,7 +28,7 @@ CONFIGS = {"mnist": ((784, [128, 64], 10), 65536, True), "rruff": ((4096, [230],
            "wide": ((4096, [4096, 4096], 10), 4096, False)}
 
 
-def run_train_nn(name, batches, epochs, work, dtype="bf16"):
+def run_train_nn(name, batches, epochs, work, dtype="bf16", dpforce=False):
     (n_in, hid, n_out), B, pixels = CONFIGS[name]
     n = B * batches
     rng = np.random.default_rng(3)
@@ -45,21 +45,31 @@ def run_train_nn(name, batches, epochs, work, dtype="bf16"):
                        mode="batched", batch=B, epochs=epochs, dtype=dtype, lr=0.01)
     env = dict(os.environ)
     env.pop("HPNN_FORCE_CPU", None)
+    if dpforce:  # the N > 1 path (train_dp_mp) with one rank, as under `torchrun --no-python`
+        env.update(HPNN_DP_FORCE="1", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
+                   HPNN_BOOT_DIR=os.path.join(work, "boot"))
     r = subprocess.run([os.path.join(ROOT, "bin", "train_nn"), "-vvv", "nn.conf"], cwd=d, env=env,
                        capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         raise SystemExit(r.stdout[-3000:] + r.stderr[-3000:])
     m = re.search(r"BATCHED TRAINING: (\d+) samples in ([0-9.]+) s", r.stdout)
     mode = re.search(r"batched plan: mode (\S)", r.stdout)
+    if dpforce and "data-parallel epochs: HIP graph replays" not in r.stdout:
+        raise SystemExit("train_nn did not replay HIP graphs on the data-parallel path:\n" + r.stdout[-3000:])
     samples, secs = int(m.group(1)), float(m.group(2))
     steps = epochs * batches
     return {"us_per_step": secs / steps * 1e6, "steps": steps, "samples": samples, "seconds": secs,
             "plan_mode": mode.group(1) if mode else None}
 
 
-def run_bench(name, steps):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", name, "--steps", str(steps),
-                        "--warmup", "10"], capture_output=True, text=True, timeout=900)
+def run_bench(name, steps, dpforce=False):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", name, "--steps", str(steps), "--warmup", "10"]
+    env = dict(os.environ)
+    if dpforce:
+        env["HPNN_DP_FORCE"] = "1"
+        cmd[1:1] = ["-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1", "--master-addr",
+                    "127.0.0.1", "--master-port", "29677"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     if r.returncode != 0:
         raise SystemExit(r.stdout[-3000:] + r.stderr[-3000:])
     j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -73,13 +83,16 @@ def main():
     ap.add_argument("--epochs", type=int, default=50)
     ap.add_argument("--dtype", default="bf16", help="bf16 (compared with bench.py) | f32 | f64 (train_nn only)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--dpforce", action="store_true",
+                    help="both on the N > 1 path with one rank (HPNN_DP_FORCE=1 under a launcher)")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as work:
         for name in a.configs.split(","):
-            lib = run_train_nn(name, a.batches, a.epochs, work, a.dtype)
-            rec = {"config": name, "dtype": a.dtype, "batch": CONFIGS[name][1], "train_nn": lib}
+            lib = run_train_nn(name, a.batches, a.epochs, work, a.dtype, a.dpforce)
+            rec = {"config": name, "dtype": a.dtype, "batch": CONFIGS[name][1], "train_nn": lib,
+                   "path": "dp (one rank)" if a.dpforce else "single"}
             if a.dtype == "bf16":
-                b = run_bench(name, 200)
+                b = run_bench(name, 200, a.dpforce)
                 rec.update(bench=b, ratio=round(lib["us_per_step"] / b["us_per_step"], 4))
             else:
                 (n_in, hid, n_out), B, _ = CONFIGS[name]

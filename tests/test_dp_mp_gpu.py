@@ -70,6 +70,7 @@ def test_train_nn_two_processes_equals_one(gpu, tmp_path, dims, dtype):
     for rc, o, e in outs:
         assert rc == 0, o[-2000:] + e[-2000:]
     assert f"2 processes (xGMI all-reduce, {dtype})" in outs[0][1]
+    assert "data-parallel epochs: HIP graph replays" in outs[0][1], outs[0][1][-2000:]
     if dims[0] == 784 and dtype == "bf16":  # fused tile mode: the exchange runs in the G0 launch
         assert "exchange inside the first-layer gradient launch" in outs[0][1], outs[0][1][-2000:]
     assert outs[1][1].strip() == ""  # rank 1 prints nothing
