@@ -248,6 +248,8 @@ int hpnn_mlp3_tile(const void *Xg, int xu8, float xscale, int K0, const void *W0
 int hpnn_mlp3_tile_grid(int Bp, int grid);
 /* profiling (HPNN_TILE_TRACE=1): per-workgroup s_memtime stamps [1024][12] */
 int hpnn_mlp3_tile_trace(unsigned long long *out);
+/* HPNN_G0_TRACE=1 phase stamps of the fused G0 launch: out[512][8] */
+int hpnn_g0_trace(unsigned long long *out);
 /* ---- wide-input one-hidden-layer front (kernels_wide.hip): K0 (4096) -> 256 -> 256 ----
  * X [Bp][ldx] bf16 row-major, W0 [256][K0], W1 / W1t [256][256] bf16; outputs H0, D2 (delta
  * of the output layer), D1 (delta of the hidden layer), all [Bp][256] bf16 row-major; labels

@@ -410,18 +410,31 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
     }
 }
 
-template <int WF, int WH, int PD, int KW, bool HU8>
+/* HPNN_G0_TRACE=1 (profiling only): s_memtime stamps of every workgroup's thread 0 at the
+ * phase boundaries, [block][mark]; read back with hpnn_g0_trace */
+constexpr int G0TR_BLOCKS = 512, G0TR_MARKS = 8;
+__device__ unsigned long long g_g0_trace[G0TR_BLOCKS][G0TR_MARKS];
+
+template <int WF, int WH, int PD, int KW, bool HU8, bool TRACE = false>
 __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                             const void *__restrict__ Hg, int nbh, float hscale,
                                                             float *__restrict__ slab, int ldg, int N, int ksteps,
                                                             int splits, int tiles_n, int tiles, int xcd_map,
                                                             hpnn_g0_update u) {
     constexpr int NT = 256 * KW, TMF = 32 * WF, TNH = 32 * WH, NE4 = TMF * TNH / 4, PARTS = NT / 128;
+    auto mark = [&](int i) {
+        if constexpr (TRACE) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            if (threadIdx.x == 0 && blockIdx.x < G0TR_BLOCKS) g_g0_trace[blockIdx.x][i] = tt;
+        }
+    };
+    mark(0);
     __shared__ f32x4 red[NT];
     f32x4 acc[WF][WH];
     int tile, split, m0, n0;
     fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
                                     n0);
+    mark(1);
     const int t = threadIdx.x, lane = t & 63;
     /* where the reduced gradient goes instead of a step: the plan's buffer, the xGMI
      * all-reduce's next half (gsel), or -- exchanging here -- this workgroup's epoch's half of
@@ -475,8 +488,10 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         }
         want_s = hpnn::ticket_arrive(u.cnt + 32 * tile, (unsigned)splits); /* this launch's last ticket */
     }
+    mark(2);
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
     g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
+    mark(3);
     if (t == 0) {
         /* fault hook: this launch reports a timed-out wait (and, like one, reduces what is there) */
         if (u.fault) __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -487,6 +502,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         }
     }
     __syncthreads();
+    mark(4);
     /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
      * float4, each summing a fixed run of splits; the runs meet in LDS in order */
     const int f = t % 128, part = t / 128;
@@ -517,6 +533,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         }
         __syncthreads();
     }
+    mark(5);
     if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12);
 }
 
@@ -604,12 +621,14 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
     uu.proto |= proto;
 #endif
-#define HPNN_G0F(U8_)                                                                                              \
-    hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_>), dim3(tiles * splits), dim3(512), 0, stream,              \
+    static const bool trace = [] { const char *e = getenv("HPNN_G0_TRACE"); return e && e[0] == '1'; }();
+#define HPNN_G0F(U8_, TR_)                                                                                         \
+    hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_, TR_>), dim3(tiles * splits), dim3(512), 0, stream,         \
                        (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
                        xcd_map, uu)
-    if (h_u8) HPNN_G0F(true);
-    else HPNN_G0F(false);
+    if (h_u8 && trace) HPNN_G0F(true, true);
+    else if (h_u8) HPNN_G0F(true, false);
+    else HPNN_G0F(false, false);
 #undef HPNN_G0F
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -635,4 +654,9 @@ extern "C" int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_
     const int bx = (int)((n4 + 255) / 256);
     const TnTail t = {rslab, rout, rstride, n4, rn, rS, (rS + rgroups - 1) / rgroups, bx, bx * rgroups};
     return fm_dispatch(Dg, Hg, h_u8, hscale, slab, ldg, N, M, Bt, splits, stream, t);
+}
+
+/* HPNN_G0_TRACE=1 stamps: out[512][8] shader-clock ticks (thread 0 of each workgroup) */
+extern "C" int hpnn_g0_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_g0_trace), sizeof(g_g0_trace)) == hipSuccess ? 0 : -5;
 }

@@ -96,7 +96,7 @@ constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool TRADE = false, bool XORD = false, bool PP = false, int PL = 4>
+          bool TRADE = false, bool XORD = false, bool PP = false, int PL = 4, bool STG = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             }
         };
         /* X^T stage of k-step s: two alternating stages, or the ping-pong's ring of three */
-        auto soff = [](int s) { return PP ? (s % PP_STAGES) * IMG_XT : (s & 1) * IMG_XT; };
+        auto soff = [](int s) { return (PP || STG) ? (s % PP_STAGES) * IMG_XT : (s & 1) * IMG_XT; };
         auto convert = [&](int s) {
             char *img = lds + OFF_XT + soff(s);
             bf16x8 v[2];
@@ -261,7 +261,64 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     st_d4<TS, TRADE>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i, o, lane);
                 }
         };
-        if constexpr (PP) {
+        if constexpr (STG) {
+            /* ================= phase A, staggered (STG) =================
+             * One barrier per k-step as in the lockstep form, but the second wave group
+             * (waves 4-7, sh = 1, the SIMD partners of waves 0-3) runs its MFMAs one k-step
+             * late: between two barriers a group-0 wave does its memory work (loads, the X(s+2)
+             * conversion, the B reads of step s + 1) and then its 16 MFMAs of step s, while its
+             * partner first issues its 16 MFMAs of step s - 1 and then its memory work (B reads
+             * of step s).  Each SIMD then pairs one wave's matrix work with the other's LDS /
+             * VALU work inside every interval, instead of both waves doing the same thing at the
+             * same time.  Group 1's B reads of step s come from stage s while group 0 converts
+             * X(s + 2): three X^T stages.  Group 1's last MFMAs run after the loop, beside group
+             * 0's H1 epilogue. */
+            const bool g1 = sh != 0;
+            bf16x8 bb[2][STA];
+            lds_barrier(); /* the previous tile's chain read H2 / D2 (= the X^T ring) and H1 */
+#pragma unroll
+            for (int s = 0; s <= D && s < KS; s++) issue(s, s - 2);
+            convert(0);
+            if (KS > 1) convert(1);
+            lds_barrier();
+            if (!g1) read_b(0, bb[0]);
+            mark(2);
+            auto mma = [&](int s) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int st = 0; st < STA; st++) {
+                    acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
+                    acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            if (g1) {
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    issue(s + D + 1, s + D - 1);
+                    if (s > 0) mma(s - 1);
+                    if (s + 2 < KS) convert(s + 2);
+                    read_b(s, bb[s & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    lds_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                mma(KS - 1);
+            } else {
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    issue(s + D + 1, s + D - 1);
+                    if (s + 2 < KS) convert(s + 2);
+                    if (s + 1 < KS) read_b(s + 1, bb[(s + 1) & 1]);
+                    mma(s);
+                    __builtin_amdgcn_sched_barrier(0);
+                    lds_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            mark(3);
+            h1_epilogue();
+        } else if constexpr (PP) {
             /* ================= phase A, ping-pong (PP) =================
              * The two wave groups sh = 0 (waves 0-3) and sh = 1 (waves 4-7) share the SIMDs
              * pairwise (wave w and w + 4 on one SIMD) and own disjoint sample halves: each
@@ -367,8 +424,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                  * the conversion and its LDS writes overlap the MFMAs and the barrier only waits
                  * for them; otherwise after the MFMAs, in series with them */
                 if constexpr (EARLY)
-                    if (s + 2 < KS && ABL != 5) convert(s + 2);
-                if (s + 1 < KS && ABL != 4) read_b(s + 1, bb[(s + 1) & 1]);
+                    if (s + 2 < KS && ABL != 5 && ABL != 8 && ABL != 9) convert(s + 2);
+                if (s + 1 < KS && ABL != 4 && ABL != 8 && ABL != 9) read_b(s + 1, bb[(s + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int st = 0; st < STA; st++) {
@@ -382,7 +439,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (!EARLY)
                     if (s + 2 < KS && ABL != 5) convert(s + 2);
-                if constexpr (ABL == 6) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* no barrier */
+                if constexpr (ABL == 6 || ABL == 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* no barrier */
                 else lds_barrier();
             }
             mark(3);
@@ -627,6 +684,10 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
      * prefetch needs), profiles/r3/SUMMARY.md; re-measured on the round-4 front (253 VGPRs):
      * D = 2 62.4 / 62.1, D = 4 (spills) 63.0 / 63.3 vs 62.1 us (profiles/r4/dd_tile_d.txt) */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
+        /* HPNN_TILE_STG=1 (A/B): the staggered phase A */
+        static const bool stg = [] { const char *e = getenv("HPNN_TILE_STG"); return e && e[0] == '1'; }();
+        if (stg) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2, true, 0, true, false, false, false, 4, true>, 512)
+                              : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2, false, 0, true, false, false, false, 4, true>, 512);
         /* HPNN_TILE_PP=<PL> (A/B): the ping-pong phase A with loads PL k-steps ahead */
         static const int pp = [] { const char *e = getenv("HPNN_TILE_PP"); return e ? atoi(e) : 0; }();
         if (pp == 3) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, true, 3>, 512)
@@ -648,6 +709,8 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
         if (trace && tabl == 5) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 5>, 512);
         if (trace && tabl == 6) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 6>, 512);
         if (trace && tabl == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 7>, 512);
+        if (trace && tabl == 8) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 8>, 512);
+        if (trace && tabl == 9) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 9>, 512);
         static const bool trade = [] { const char *e = getenv("HPNN_TILE_TRADE"); return e && e[0] == '1'; }();
         if (trace && trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, true>, 512);
         if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)

@@ -366,6 +366,11 @@ PYBIND11_MODULE(_native, m) {
         check(hpnn_mlp3_tile_trace(v.data()), "mlp3_tile_trace");
         return v;
     });
+    m.def("g0_trace", []() {
+        std::vector<unsigned long long> v(512 * 8);
+        check(hpnn_g0_trace(v.data()), "g0_trace");
+        return v;
+    });
     m.def("mlp3_fused_grid", [](int Bp, int grid) { return hpnn_mlp3_fused_grid(Bp, grid); });
     m.def("gemm_fm_direct", [](uptr Dg, uptr Hg, int h_u8, float hscale, uptr slab, int ldg, int N, int M, int Bt,
                                int splits, uptr stream) {

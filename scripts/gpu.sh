@@ -57,6 +57,7 @@ for spec in "$@"; do
     dpforce_synth1k) HPNN_DP_FORCE=1 step dpforce_synth1k 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --model synth --batch 1024 --steps 50 --warmup 10 ;;
     trace) HPNN_TILE_TRACE=1 step tile_trace 200 python scripts/tile_trace.py ;;
     trace1) HPNN_TILE_TRACE=1 step tile_trace_d1 200 python scripts/tile_trace.py 1 ;;
+    g0trace) HPNN_G0_TRACE=1 step g0_trace 200 python scripts/g0_trace.py ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
     prof_synth1k) step rocprof_synth1k 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_synth1k -o run -- python3 bench.py --model synth --batch 1024 --steps 20 --warmup 5 --graph 0 ;;
