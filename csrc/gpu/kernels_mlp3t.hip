@@ -78,9 +78,6 @@ constexpr int OFF_W1 = OFF_D3 + TS * NO * 2;
 constexpr int LDS_TOTAL = OFF_W1 + IMG_W1;
 static_assert(TS * H2 * 2 <= 2 * IMG_XT, "H2 aliases the X^T stages");
 static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
-/* ping-pong phase A: a ring of 3 X^T stages (the third one in the D2 image, dead until the chain) */
-constexpr int PP_STAGES = 3;
-static_assert(OFF_XT + PP_STAGES * IMG_XT <= OFF_D3, "the X^T ring fits below the D3 image");
 
 /* within-wave ordering of LDS writes before other lanes' reads (one wave's LDS
  * instructions execute in order; this keeps the compiler from moving them) */
@@ -96,7 +93,7 @@ constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool TRADE = false, bool XORD = false, bool PP = false, int PL = 4, bool STG = false>
+          bool TRADE = false, bool XORD = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -216,8 +213,8 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                                     : *(const bf16x8 *)(wbase + z + ((size_t)i * KS + sw) * 512);
             }
         };
-        /* X^T stage of k-step s: two alternating stages, or the ping-pong's ring of three */
-        auto soff = [](int s) { return (PP || STG) ? (s % PP_STAGES) * IMG_XT : (s & 1) * IMG_XT; };
+        /* X^T stage of k-step s: two alternating stages */
+        auto soff = [](int s) { return (s & 1) * IMG_XT; };
         auto convert = [&](int s) {
             char *img = lds + OFF_XT + soff(s);
             bf16x8 v[2];
@@ -261,145 +258,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     st_d4<TS, TRADE>(imgH1, lo, SPA * sh + 16 * st, 32 * ng + 16 * i, o, lane);
                 }
         };
-        if constexpr (STG) {
-            /* ================= phase A, staggered (STG) =================
-             * One barrier per k-step as in the lockstep form, but the second wave group
-             * (waves 4-7, sh = 1, the SIMD partners of waves 0-3) runs its MFMAs one k-step
-             * late: between two barriers a group-0 wave does its memory work (loads, the X(s+2)
-             * conversion, the B reads of step s + 1) and then its 16 MFMAs of step s, while its
-             * partner first issues its 16 MFMAs of step s - 1 and then its memory work (B reads
-             * of step s).  Each SIMD then pairs one wave's matrix work with the other's LDS /
-             * VALU work inside every interval, instead of both waves doing the same thing at the
-             * same time.  Group 1's B reads of step s come from stage s while group 0 converts
-             * X(s + 2): three X^T stages.  Group 1's last MFMAs run after the loop, beside group
-             * 0's H1 epilogue. */
-            const bool g1 = sh != 0;
-            bf16x8 bb[2][STA];
-            lds_barrier(); /* the previous tile's chain read H2 / D2 (= the X^T ring) and H1 */
-#pragma unroll
-            for (int s = 0; s <= D && s < KS; s++) issue(s, s - 2);
-            convert(0);
-            if (KS > 1) convert(1);
-            lds_barrier();
-            if (!g1) read_b(0, bb[0]);
-            mark(2);
-            auto mma = [&](int s) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int st = 0; st < STA; st++) {
-                    acc[0][st] = mfma(wr[s][0], bb[s & 1][st], acc[0][st]);
-                    acc[1][st] = mfma(wr[s][1], bb[s & 1][st], acc[1][st]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            if (g1) {
-#pragma unroll
-                for (int s = 0; s < KS; s++) {
-                    issue(s + D + 1, s + D - 1);
-                    if (s > 0) mma(s - 1);
-                    if (s + 2 < KS) convert(s + 2);
-                    read_b(s, bb[s & 1]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    lds_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                mma(KS - 1);
-            } else {
-#pragma unroll
-                for (int s = 0; s < KS; s++) {
-                    issue(s + D + 1, s + D - 1);
-                    if (s + 2 < KS) convert(s + 2);
-                    if (s + 1 < KS) read_b(s + 1, bb[(s + 1) & 1]);
-                    mma(s);
-                    __builtin_amdgcn_sched_barrier(0);
-                    lds_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            mark(3);
-            h1_epilogue();
-        } else if constexpr (PP) {
-            /* ================= phase A, ping-pong (PP) =================
-             * The two wave groups sh = 0 (waves 0-3) and sh = 1 (waves 4-7) share the SIMDs
-             * pairwise (wave w and w + 4 on one SIMD) and own disjoint sample halves: each
-             * group converts, reads and multiplies only its own 128 samples.  Every k-step is
-             * two segments between barriers; in each, one group issues its 16 MFMAs while the
-             * other does its memory work (loads, the X(s + 2) conversion, the B reads of its
-             * next MFMA segment), so the matrix pipe of a SIMD never waits for that work:
-             *   segment 1: group 0 MFMAs(s)       | group 1 memory(s), B(s)
-             *   segment 2: group 0 memory(s), B(s+1) | group 1 MFMAs(s)
-             * (the lockstep form runs both groups' memory work, then both groups' MFMAs: about
-             * half of each k-step without matrix work).  Three X^T stages: stage (s + 2) % 3
-             * is refilled one barrier after the last read of X(s - 1) in either group.  Loads
-             * run PL k-steps ahead (register ring).  Group 0 writes its H1 rows in the last
-             * segment, under group 1's last MFMAs. */
-            auto issue_x = [&](int k) {
-                if (k >= KS) return;
-                unsigned int z = 0;
-                asm volatile("" : "+s"(z));
-#pragma unroll
-                for (int n = 0; n < XV; n++) xr[k][n] = *(const u32x4 *)(xtile + z + (size_t)(2 * k) * CHUNK + 16 * n);
-            };
-            auto issue_w = [&](int k) {
-                if (k >= KS) return;
-                unsigned int z = 0;
-                asm volatile("" : "+s"(z));
-#pragma unroll
-                for (int i = 0; i < 2; i++) wr[k][i] = *(const bf16x8 *)(wbase + z + ((size_t)i * KS + k) * 512);
-            };
-            auto run = [&](auto g1c) {
-                constexpr bool G1 = decltype(g1c)::value;
-                bf16x8 bb[STA];
-                /* the previous tile's chain read H2 / D2 (= the X^T ring) and H1 */
-                lds_barrier();
-#pragma unroll
-                for (int k = 0; k < PL + 2; k++) issue_x(k);
-#pragma unroll
-                for (int k = 0; k < PL + (G1 ? 0 : 1); k++) issue_w(k);
-                convert(0);
-                if (KS > 1) convert(1);
-                lds_barrier();
-                if constexpr (!G1) read_b(0, bb);
-                mark(2);
-                /* memory segment: loads PL k-steps ahead, X(s + 2) -> its stage, B(sb) */
-                auto mem = [&](int s, int sb) {
-                    issue_x(s + 2 + PL);
-                    issue_w(sb + PL);
-                    if (s + 2 < KS) convert(s + 2);
-                    read_b(sb, bb);
-                };
-                auto comp = [&](int s) {
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int st = 0; st < STA; st++) {
-                        acc[0][st] = mfma(wr[s][0], bb[st], acc[0][st]);
-                        acc[1][st] = mfma(wr[s][1], bb[st], acc[1][st]);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                };
-#pragma unroll
-                for (int s = 0; s < KS; s++) {
-                    if constexpr (G1) mem(s, s);
-                    else comp(s);
-                    __builtin_amdgcn_sched_barrier(0);
-                    lds_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (G1) {
-                        comp(s);
-                    } else {
-                        if (s + 1 < KS) mem(s, s + 1);
-                        else h1_epilogue();
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    lds_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                mark(3);
-                if constexpr (G1) h1_epilogue();
-            };
-            if (sh) run(std::true_type{});
-            else run(std::false_type{});
-        } else {
+        {
             /* the previous tile's chain read H2 (= the X^T stages) and H1 */
             lds_barrier();
 #pragma unroll
@@ -656,9 +515,9 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
 
 int g_tile_cus = 0;
 #ifdef HPNN_ABLATIONS
-/* HPNN_TILE_ABL (make ABLATIONS=1 builds only; profiling, wrong results): 1 = half the W0
- * loads, 2 = no X loads, 3 = no phase-A MFMAs, 4 = no phase-A B reads, 5 = no X^T
- * conversion writes */
+/* HPNN_TILE_ABL (make ABLATIONS=1 builds only; profiling, wrong results): 1 = no W0 loads,
+ * 2 = no X loads, 7 = neither (a register pattern instead), 3 = no phase-A MFMAs, 4 = no
+ * phase-A B reads, 5 = no X^T conversion, 6 = no per-k-step barrier, 8 = 4 + 5 + 6, 9 = 4 + 5 */
 const int g_tile_abl = [] { const char *e = getenv("HPNN_TILE_ABL"); return e ? atoi(e) : 0; }();
 #endif
 
@@ -684,52 +543,30 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
      * prefetch needs), profiles/r3/SUMMARY.md; re-measured on the round-4 front (253 VGPRs):
      * D = 2 62.4 / 62.1, D = 4 (spills) 63.0 / 63.3 vs 62.1 us (profiles/r4/dd_tile_d.txt) */
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
-        /* HPNN_TILE_STG=1 (A/B): the staggered phase A */
-        static const bool stg = [] { const char *e = getenv("HPNN_TILE_STG"); return e && e[0] == '1'; }();
-        if (stg) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2, true, 0, true, false, false, false, 4, true>, 512)
-                              : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 2, false, 0, true, false, false, false, 4, true>, 512);
-        /* HPNN_TILE_PP=<PL> (A/B): the ping-pong phase A with loads PL k-steps ahead */
-        static const int pp = [] { const char *e = getenv("HPNN_TILE_PP"); return e ? atoi(e) : 0; }();
-        if (pp == 3) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, true, 3>, 512)
-                                  : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, false, true, 3>, 512);
-        if (pp == 4) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, true, 4>, 512)
-                                  : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, false, true, 4>, 512);
-        if (pp == 5) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, true, 5>, 512)
-                                  : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, false, true, 5>, 512);
+#ifdef HPNN_ABLATIONS
+        /* A/B variants that measured slower (make ABLATIONS=1 builds only):
+         * HPNN_TILE_EARLY=0: X(s + 2) converted after the MFMAs of step s (equal within noise);
+         * HPNN_TILE_TRADE=1: the chain's 8-byte image stores / loads with a lane-pair trade of
+         *   halves -- LDS bank conflicts 18.5 % -> 5.6 %, but 60.6 / 61.4 / 62.5 vs 59.9 / 59.8 /
+         *   60.0 us per step (profiles/r4/tr_tile_trade_ab.txt);
+         * HPNN_TILE_XORD=1: X^T stage writes in a per-lane-pair order (conflicts 60 % -> 18.5 %):
+         *   61.5 / 61.5 / 62.0 vs 60.7 / 60.3 / 61.3 us (profiles/r4/xo_tile_xord_ab.txt);
+         * HPNN_TILE_ABL=n: phase-A ablations (wrong results), traced with HPNN_TILE_TRACE=1
+         *   (profiles/r5/a_tile_phaseA_ablations.txt) */
         static const bool late = [] { const char *e = getenv("HPNN_TILE_EARLY"); return e && e[0] == '0'; }();
-        /* HPNN_TILE_TRADE=1 (A/B): the chain's 8-byte image stores / loads with a lane-pair trade of
-         * halves -- LDS bank conflicts 18.5 % -> 5.6 % of the LDS instructions, but the shuffles
-         * cost more than the conflicts: 60.6 / 61.4 / 62.5 vs 59.9 / 59.8 / 60.0 us per step,
-         * per-workgroup span 59.4K vs 55.6K ticks (profiles/r4/tr_tile_trade_ab.txt) */
-        static const int tabl = [] { const char *e = getenv("HPNN_TILE_TABL"); return e ? atoi(e) : 0; }();
-        if (trace && tabl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 1>, 512);
-        if (trace && tabl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 2>, 512);
-        if (trace && tabl == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 3>, 512);
-        if (trace && tabl == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 4>, 512);
-        if (trace && tabl == 5) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 5>, 512);
-        if (trace && tabl == 6) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 6>, 512);
-        if (trace && tabl == 7) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 7>, 512);
-        if (trace && tabl == 8) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 8>, 512);
-        if (trace && tabl == 9) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 9>, 512);
         static const bool trade = [] { const char *e = getenv("HPNN_TILE_TRADE"); return e && e[0] == '1'; }();
-        if (trace && trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, true>, 512);
-        if (trace) return late ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, false>, 512)
-                               : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
+        static const bool xord = [] { const char *e = getenv("HPNN_TILE_XORD"); return e && e[0] == '1'; }();
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
         if (trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true>, 512);
-        /* HPNN_TILE_XORD=1 (A/B): X^T stage writes in a per-lane-pair order that spreads each
-         * 8-lane ds_write_b128 group over all 8 bank groups (LDS conflicts 60 % -> 18.5 %), but
-         * the selects cost more: 61.5 / 61.5 / 62.0 vs 60.7 / 60.3 / 61.3 us per step in row
-         * order (profiles/r4/xo_tile_xord_ab.txt) */
-        static const bool xord = [] { const char *e = getenv("HPNN_TILE_XORD"); return e && e[0] == '1'; }();
         if (xord) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, true>, 512);
-#ifdef HPNN_ABLATIONS
-        if (g_tile_abl == 1) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 1>, 512);
-        if (g_tile_abl == 2) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 2>, 512);
-        if (g_tile_abl == 3) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 3>, 512);
-        if (g_tile_abl == 4) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 4>, 512);
-        if (g_tile_abl == 5) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 5>, 512);
+#define HPNN_TABL(N_)                                                                                               \
+        if (g_tile_abl == N_) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, N_>, 512)          \
+                                           : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, N_>, 512);
+        HPNN_TABL(1) HPNN_TABL(2) HPNN_TABL(3) HPNN_TABL(4) HPNN_TABL(5) HPNN_TABL(6) HPNN_TABL(7) HPNN_TABL(8)
+        HPNN_TABL(9)
+#undef HPNN_TABL
 #endif
+        if (trace) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true>, 512);
     }
     return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3>, 512);
 }
