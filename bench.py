@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--input", choices=["u8", "float"], default="u8",
                     help="synthetic images as 8-bit pixels (MNIST's format; the net sees pixel/255 in BF16) "
                          "or as uniform floats in [0, 1)")
-    ap.add_argument("--grad-comm", choices=["fp32", "bf16rs"], default="fp32",
+    ap.add_argument("--grad-comm", choices=["auto", "fp32", "bf16rs"], default="auto",
                     help="data-parallel gradient exchange: FP32 all-reduce, or BF16 reduce-scatter + sharded "
                          "optimizer step + BF16 weight all-gather (half the bytes; per-layer models only)")
     args = ap.parse_args()

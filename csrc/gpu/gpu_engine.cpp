@@ -1565,9 +1565,27 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     const bool mom = o->train == NN_TRAIN_BPM;
     const int n_out = (int)k->n_outputs;
     /* HPNN_GRAD_COMM=bf16rs: BF16 reduce-scatter + sharded step + BF16 all-gather (RCCL,
-     * per-layer plan); every rank reads the same environment */
+     * per-layer plan); fp32: the FP32 all-reduce; auto (default): bf16rs for the BF16 engine
+     * when the net takes the per-layer plan and its FP32 gradients exceed 4 MB (bandwidth-
+     * bound exchange: half the bytes, each rank steps 1 / world of the rows), else fp32.
+     * Every rank reads the same environment and net, so all decide alike. */
     const char *gce = getenv("HPNN_GRAD_COMM");
-    const bool bf16rs = gce && !strcmp(gce, "bf16rs");
+    bool bf16rs = gce && !strcmp(gce, "bf16rs");
+    if (!gce || !strcmp(gce, "auto")) {
+        double gbytes = 0.0;
+        const int nl = (int)k->n_hiddens + 1;
+        std::vector<int> sizes(nl + 1);
+        sizes[0] = (int)k->n_inputs;
+        for (int l = 0; l < nl; l++) {
+            sizes[l + 1] = (int)layer_of(k, l)->n_neurons;
+            gbytes += 4.0 * sizes[l] * sizes[l + 1];
+        }
+        hpnn::BPlan probe; /* host-only configuration: which step structure the net gets */
+        const int ty = o->type == NN_TYPE_ANN ? 0 : (o->type == NN_TYPE_LNN ? 1 : 2);
+        const bool per_layer =
+            probe.configure(sizes.data(), nl, ty, Bg, mom, -1, nullptr, 512, false) == 0 && probe.mode == 0;
+        bf16rs = W > 1 && !strcmp(Net::name(), "bf16") && per_layer && gbytes > (double)(4 << 20);
+    }
     Net net;
     if (!net.init(k, Bg, o->type, mom, s, B % 32 == 0 && Bg % 32 == 0, bf16rs ? 0 : -1) || !net.alloc_flat())
         return FALSE;

@@ -33,7 +33,10 @@ class DataParallel:
     group runs on the nccl backend, else torch.distributed), "native", "torch", or "xar"
     (xGMI all-reduce only, no RCCL: several ranks on one GPU in tests).
 
-    grad_comm: "fp32" (default): the FP32 gradient buckets are all-reduced, every rank
+    grad_comm: "auto" (default): "bf16rs" with more than one rank when the model takes the
+    per-layer path and its FP32 gradients exceed 4 MB (the exchange is bandwidth-bound there:
+    half the bytes, and each rank steps 1/world of the rows), else "fp32".
+    "fp32": the FP32 gradient buckets are all-reduced, every rank
     applies the whole update.  "bf16rs": for layers whose rows split evenly over the ranks,
     the gradient is reduce-scattered in BF16, each rank steps ITS rows of the FP32 master
     weights / momentum (a sharded optimizer), and the BF16 weight rows are all-gathered:
@@ -41,14 +44,21 @@ class DataParallel:
     2 (W-1)/W x P x 4 -- half (the 8 x 4096 synthetic config: 470 vs 940 MB).  The FP32
     masters then live sharded: gather_masters() assembles them (checkpoints, tests)."""
 
-    def __init__(self, model, group=None, bucket_bytes=256 * 1024, comm="auto", grad_comm="fp32"):
+    BF16RS_MIN_BYTES = 4 << 20
+
+    def __init__(self, model, group=None, bucket_bytes=256 * 1024, comm="auto", grad_comm="auto"):
         self.m = model
         self.group = group
         self.active = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.active else 1
         self.rank = dist.get_rank(group) if self.active else 0
-        if grad_comm not in ("fp32", "bf16rs"):
+        if grad_comm not in ("auto", "fp32", "bf16rs"):
             raise ValueError(f"grad_comm {grad_comm!r}")
+        if grad_comm == "auto":
+            per_layer = getattr(model, "fused_mode", None) is None and getattr(model, "W0f", None) is None
+            big = model.grad_flat.numel() * 4 > self.BF16RS_MIN_BYTES
+            force = os.environ.get("HPNN_DPX_FORCE", "0") == "1"  # the N > 1 path on one rank (tests)
+            grad_comm = "bf16rs" if (self.active and (self.world > 1 or force) and per_layer and big) else "fp32"
         self.grad_comm = grad_comm
         self.sharded = set()
         if grad_comm == "bf16rs" and self.active and (self.world > 1 or os.environ.get("HPNN_DPX_FORCE", "0") == "1"):

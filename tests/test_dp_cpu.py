@@ -141,3 +141,41 @@ def test_dp_bf16_reduce_scatter_sharded_update():
         da, db = a - w0, b - w0
         rel = (da - db).norm() / (db.norm() + 1e-30)
         assert rel < 2e-2, rel.item()
+
+
+def _worker_auto(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for name, sizes, fused in (("big", [1100, 1024, 10], False), ("small", [24, 64, 32, 5], False),
+                               ("mnist", [784, 128, 64, 10], None)):
+        m = MLP(sizes, "SNN", batch=128, device="cpu", seed=11, fused=fused)
+        dp = DataParallel(m)  # grad_comm="auto"
+        out[name] = (dp.grad_comm, sorted(dp.sharded))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_grad_comm_auto():
+    """grad_comm="auto" (the default): the BF16 reduce-scatter + sharded update for per-layer
+    models whose FP32 gradients exceed 4 MB at world > 1; the FP32 all-reduce otherwise
+    (small gradients are latency-bound, and the fused MNIST-shape step exchanges in-kernel)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_auto, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert got[r]["big"] == ("bf16rs", [0, 1])
+        assert got[r]["small"] == ("fp32", [])
+        assert got[r]["mnist"] == ("fp32", [])
+    # one rank: nothing to exchange, the plain path
+    m = MLP([1100, 1024, 10], "SNN", batch=128, device="cpu", fused=False)
+    assert DataParallel(m).grad_comm == "fp32"

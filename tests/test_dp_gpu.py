@@ -120,3 +120,39 @@ def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
         dp.check()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes,expect", [([2048, 1024, 10], "bf16rs"), ([300, 96, 64, 7], "fp32")])
+def test_native_dp_exchange_auto_default(gpu, monkeypatch, sizes, expect):
+    """grad_comm defaults to "auto": a per-layer net with more than 4 MB of FP32 gradients takes
+    the BF16 reduce-scatter + sharded step on the N > 1 path (here one rank, HPNN_DPX_FORCE);
+    small ones the FP32 all-reduce.  Both train like the plain step (bf16rs within the BF16
+    rounding of the gradient)."""
+    monkeypatch.setenv("HPNN_DPX_FORCE", "1")
+    monkeypatch.setenv("HPNN_DPX_SHARD1", "1")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        B = 1024
+        g = torch.Generator(device=dev).manual_seed(5)
+        Xr = torch.rand(B, sizes[0], device=dev, generator=g)
+        L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
+        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        w0 = [w.clone() for w in b.host_weights()]
+        dp = DataParallel(a, comm="native")
+        assert dp.grad_comm == expect and bool(dp.sharded) == (expect == "bf16rs")
+        Xa, Xb = a.prepare_input(Xr), b.prepare_input(Xr)
+        for _ in range(2):
+            dp.train_step(Xa, labels=L, lr=0.05, alpha=0.2)
+            b.train_step(Xb, labels=L, lr=0.05, alpha=0.2)
+        dp.gather_masters()
+        torch.cuda.synchronize()
+        for l, (wa, wb) in enumerate(zip(a.host_weights(), b.host_weights())):
+            da, db = wa - w0[l], wb - w0[l]
+            rel = ((da - db).norm() / db.norm()).item()
+            assert rel < (1e-5 if expect == "fp32" else 1e-2), (l, rel)
+        dp.check()
+    finally:
+        dist.destroy_process_group()
