@@ -14,7 +14,6 @@ namespace hpnn {
 DpExchange::~DpExchange() {
     hpnn_dev_free(send16_);
     hpnn_dev_free(recv16_);
-    hpnn_dev_free(gather32_);
 }
 
 int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
@@ -36,7 +35,8 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
     const char *s1 = getenv("HPNN_DPX_SHARD1");
     const bool one = s1 && s1[0] == '1';
     for (int l = 0; l < p_->L; l++) {
-        /* rows split evenly, each rank's block whole 32-row pieces (the transposes) */
+        /* rows split evenly over the ranks (any block height: the transpose runs on the whole
+         * all-gathered matrix) */
         sharded_[l] = (world_ > 1 || one) && p_->Np[l] % world_ == 0;
         if (sharded_[l]) mx = mx > (size_t)p_->Np[l] * p_->Kp[l] ? mx : (size_t)p_->Np[l] * p_->Kp[l];
     }

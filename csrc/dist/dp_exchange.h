@@ -48,7 +48,6 @@ class DpExchange {
     Mode mode_ = FP32;
     std::vector<bool> sharded_;
     void *send16_ = nullptr, *recv16_ = nullptr;
-    float *gather32_ = nullptr;
 };
 
 }  // namespace hpnn

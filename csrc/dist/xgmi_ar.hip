@@ -40,6 +40,9 @@
 #include <stddef.h>
 
 #include "../gpu/mfma_common.h"
+#include "../gpu/kernels.h"
+
+HPNN_CO_PROBE(xar)
 #include <stdlib.h>
 #include <string.h>
 
@@ -585,6 +588,11 @@ extern "C" int hpnn_xar_status(hpnn_xar *c) {
     unsigned int err = 0;
     if (hipMemcpy(&err, &c->sig->error, 4, hipMemcpyDeviceToHost) != hipSuccess) return -2;
     return err ? -1 : 0;
+}
+
+extern "C" int hpnn_xar_status_enqueue(hpnn_xar *c, unsigned int *dst, hipStream_t stream) {
+    if (!c) return -1;
+    return hipMemcpyAsync(dst, &c->sig->error, 4, hipMemcpyDeviceToHost, stream) == hipSuccess ? 0 : -2;
 }
 
 extern "C" int hpnn_xar_self_test(hpnn_xar *c, hipStream_t stream) {

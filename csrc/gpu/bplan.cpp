@@ -582,15 +582,18 @@ int BPlan::predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s)
     return output(lab0, nullptr, 0, n_valid, O, ldo, false, s);
 }
 
-int BPlan::health(hipStream_t s) {
-    unsigned int e[2] = {0, 0};
-    if (g0cnt && hipMemcpyAsync(&e[0], g0cnt + 224, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
-    unsigned int e2 = 0;
-    if (tncnt && hipMemcpyAsync(&e2, tncnt + 1024 * L, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
-    if (wwords && hipMemcpyAsync(&e[1], wwords + 2 * (Bp / TILE_W), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+int BPlan::health_enqueue(hipStream_t s, unsigned int *dst) {
+    if (g0cnt && hipMemcpyAsync(&dst[0], g0cnt + 224, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
+    if (tncnt && hipMemcpyAsync(&dst[1], tncnt + 1024 * L, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
+    if (wwords && hipMemcpyAsync(&dst[2], wwords + 2 * (Bp / TILE_W), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return -7;
-    if (hipStreamSynchronize(s) != hipSuccess) return -7;
-    return (e[0] || e[1] || e2) ? -9 : 0;
+    return 0;
+}
+
+int BPlan::health(hipStream_t s) {
+    unsigned int e[3] = {0, 0, 0};
+    if (health_enqueue(s, e) != 0 || hipStreamSynchronize(s) != hipSuccess) return -7;
+    return (e[0] || e[1] || e[2]) ? -9 : 0;
 }
 
 int BPlan::weights_digest(int which, unsigned long long *out, hipStream_t s) {

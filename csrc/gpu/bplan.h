@@ -150,6 +150,10 @@ class BPlan {
     /* 0, or -9 when an in-kernel hand-over (wide front partials, fused G0 splits) timed out
      * since the plan was created (synchronises s) */
     int health(hipStream_t s);
+    /* the same words copied into dst[0..2] (pinned host memory, zeroed by the caller) on s
+     * without waiting: a training loop checks them one replay later, so the check never
+     * leaves the GPU idle; any non-zero word = a timed-out hand-off */
+    int health_enqueue(hipStream_t s, unsigned int *dst);
     /* 64-bit digest of the weights (bit 1: BF16 copies W / W^T of every layer, bit 2: the FP32
      * masters); data-parallel replicas must agree on it bit for bit (synchronises s) */
     int weights_digest(int which, unsigned long long *out, hipStream_t s);

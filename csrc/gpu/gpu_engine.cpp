@@ -814,6 +814,15 @@ struct Batched {
                          "(the step used partial sums); stopping\n");
         return FALSE;
     }
+    /* healthy() in two halves: enqueue the readback into d[0..2] (pinned, zeroed), judge it
+     * once an event after it has completed */
+    bool health_enqueue(unsigned int *d) { return p.health_enqueue(s, d) == 0; }
+    BOOL health_ok(const unsigned int *d) {
+        if (!(d[0] || d[1] || d[2])) return TRUE;
+        NN_ERROR(stderr, "batched GPU training: an in-kernel split-K / tile hand-off timed out "
+                         "(the step used partial sums); stopping\n");
+        return FALSE;
+    }
     /* digest of the weights every data-parallel replica must hold bit for bit: the BF16 copies,
      * plus the FP32 masters unless the BF16 reduce-scatter step keeps them sharded */
     BOOL digest(unsigned long long *d) {
@@ -1083,6 +1092,8 @@ struct BatchedFP {
     int xchg_step(const XSet &, long, const T *, int, int, double, double, double, hpnn_xar *) { return -1; }
     BOOL gather_masters() { return TRUE; }
     BOOL healthy() { return TRUE; } /* no in-kernel hand-offs in the FP64 / FP32 kernels */
+    bool health_enqueue(unsigned int *) { return true; }
+    BOOL health_ok(const unsigned int *) { return TRUE; }
     unsigned long long *dig = nullptr; /* device word of digest() */
     BOOL digest(unsigned long long *d) {
         if (!dig && hpnn_dev_malloc((void **)&dig, 8) != hipSuccess) return FALSE;
@@ -1270,6 +1281,7 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
     const bool metrics = hpnn_metrics_active() != 0;
     const int E = (int)o->epochs;
     const int epg = metrics ? 1 : std::max(1, std::min(E, 32 / std::max(1, n_batches)));
+    hpnn_preload_code_objects();
     std::map<int, hipGraphExec_t> graphs;
     if (graphs_enabled() && n_batches <= 4096)
         for (int ne : {epg, E % epg}) {
@@ -1279,6 +1291,8 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
                 NN_DBG(stdout, "batched GPU training: epochs not capturable, eager launches\n");
             graphs[ne] = x;
         }
+    /* setup (data upload and layout conversions) is finished before the clock starts */
+    HIPCHK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
@@ -1409,6 +1423,11 @@ BOOL train_dp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const hpn
     const size_t count = nets[0]->flat_count();
     NN_OUT(stdout, "data-parallel batched training: %d replicas (%s, %s), %d samples per replica per step\n", G,
            loopback ? "loopback on one GPU" : "RCCL all-reduce", Net::name(), Bg);
+    for (int g = 0; g < G; g++) {
+        hipSetDevice(dev[g]);
+        hpnn_preload_code_objects();
+    }
+    hipSetDevice(dev[0]);
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
@@ -1661,6 +1680,34 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         ok = hpnn_dev_malloc(&Td, tf.size() * sizeof(TT)) == hipSuccess &&
              hipMemcpy(Td, tf.data(), tf.size() * sizeof(TT), hipMemcpyHostToDevice) == hipSuccess;
     }
+    hpnn_preload_code_objects();
+    /* per-replay health: plan hand-off words [0..2], exchange error words [3..4], per slot */
+    unsigned int *hw = nullptr;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    if (hipHostMalloc((void **)&hw, 16 * sizeof(unsigned int), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&hev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&hev[1], hipEventDisableTiming) != hipSuccess)
+        ok = FALSE;
+    int pend = -1; /* slot whose readback is in flight */
+    auto enqueue_check = [&](int slot) -> bool {
+        unsigned int *d = hw + 8 * slot;
+        for (int i = 0; i < 8; i++) d[i] = 0;
+        bool r = net.health_enqueue(d);
+        if (r && use_xar) r = hpnn_xar_status_enqueue(xar, d + 3, s) == 0;
+        if (r && xark) r = hpnn_xar_status_enqueue(xark, d + 4, s) == 0;
+        return r && hipEventRecord(hev[slot], s) == hipSuccess;
+    };
+    auto finish_check = [&](int slot) -> bool {
+        if (hipEventSynchronize(hev[slot]) != hipSuccess) return false;
+        const unsigned int *d = hw + 8 * slot;
+        if (!net.health_ok(d)) return false;
+        return use_xar ? d[3] == 0 && d[4] == 0 : hpnn_comm_check(comm) == 0;
+    };
+    /* preflight: the plan and the exchange start clean (and the first reads of their words, a
+     * few ms while the runtime maps them, stay out of the training time) */
+    if (ok) ok = enqueue_check(0) && finish_check(0);
+    /* setup (data upload and layout conversions) is finished before the clock starts */
+    if (hipDeviceSynchronize() != hipSuccess) ok = FALSE;
     auto t0 = std::chrono::steady_clock::now();
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
@@ -1721,12 +1768,30 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         }
         return true;
     };
+    /* Epoch 0 runs eagerly; then one HIP graph replays epg epochs (about 32 steps, as
+     * train_single).  After every replay a rank checks its own health (one small readback);
+     * the ranks agree (one host all-gather) after the first epoch, the last, every epoch under
+     * metrics and every 16th replay otherwise.  Between agreements a rank that saw a failure
+     * keeps launching -- the exchange needs every rank in step -- and reports it at the next
+     * one.  Graph capture is setup, not training: its time is left out of the training time,
+     * as train_single captures before its clock starts. */
+    const bool metrics = hpnn_metrics_active() != 0;
+    const UINT E = o->epochs;
+    const UINT epg = metrics ? 1u : std::max(1u, std::min(E > 1 ? E - 1 : 1u, 32u / (UINT)std::max(1, n_batches)));
     hipGraphExec_t gx = nullptr;
-    for (UINT e = 0; e < o->epochs && ok; e++) {
-        if (e == 1 && graphs_enabled() && n_batches <= 4096) {
+    double setup_s = 0.0;
+    bool local_ok = true;
+    UINT replays = 0;
+    for (UINT e = 0; e < E && ok;) {
+        if (e == 1 && graphs_enabled() && n_batches <= 4096 && E - 1 >= epg) {
             /* every rank captures; all replay only if all captured (a failed capture ran
              * nothing, so eager epochs stay in step) */
-            int cap = capture_epoch(s, [&]() { return epoch_steps(e); }, &gx) ? 1 : 0;
+            const auto c0 = std::chrono::steady_clock::now();
+            int cap = capture_epoch(s, [&]() {
+                for (UINT i = 0; i < epg; i++)
+                    if (!epoch_steps(e + i)) return false;
+                return true;
+            }, &gx) ? 1 : 0;
             std::vector<int> caps(W);
             if (hpnn_boot_allgather(&cap, sizeof cap, caps.data()) != 0) ok = FALSE;
             for (int v : caps) cap = cap && v;
@@ -1736,26 +1801,45 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             }
             if (ok && R == 0)
                 NN_OUT(stdout, "data-parallel epochs: %s\n", gx ? "HIP graph replays" : "eager launches (capture failed)");
+            setup_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+            if (!ok) break;
         }
-        if (!ok) break;
-        ok = gx ? hipGraphLaunch(gx, s) == hipSuccess : epoch_steps(e);
-        if (!ok) break;
+        const UINT ne = e == 0 ? 1u : std::min(epg, E - e);
+        bool lok;
+        if (gx && e > 0 && ne == epg) {
+            lok = hipGraphLaunch(gx, s) == hipSuccess;
+        } else {
+            lok = true;
+            for (UINT i = 0; i < ne && lok; i++) lok = epoch_steps(e + i);
+        }
+        e += ne;
+        if (e > 1) replays++;
+        /* this replay's health words are read back behind it; the previous replay's are judged
+         * now (the host waits for that replay only, with this one queued behind it) */
+        const int slot = (int)(replays & 1);
+        if (lok) lok = enqueue_check(slot);
+        if (pend >= 0) local_ok = finish_check(pend) && local_ok;
+        pend = lok ? slot : -1;
+        local_ok = local_ok && lok;
+        const bool first = e == 1, last = e == E;
+        if (!(first || last || metrics || replays % 16 == 0)) continue;
+        /* agreement point */
+        if (pend >= 0) local_ok = finish_check(pend) && local_ok;
+        pend = -1;
         double l = 0.0;
         unsigned int h = 0;
-        ok = net.read_stats(&l, &h) && net.healthy();
-        if (ok) ok = use_xar ? hpnn_xar_status(xar) == 0 && (!xark || hpnn_xar_status(xark) == 0)
-                             : hpnn_comm_check(comm) == 0;
+        if (local_ok && !net.read_stats(&l, &h)) local_ok = false;
         /* replicas must hold bitwise-identical weights: a wrong-but-timely exchange (a sum that
          * arrived in time but is not every rank's) shows here, after the first epoch and the last */
         unsigned long long dig = 0;
-        const bool check_dig = e == 0 || e + 1 == o->epochs;
-        if (ok && check_dig && !net.digest(&dig)) ok = FALSE;
-        if (ok && check_dig && R == W - 1 && hpnn_fault_hit("digest")) dig ^= 1; /* test hook */
+        const bool check_dig = first || last;
+        if (local_ok && check_dig && !net.digest(&dig)) local_ok = false;
+        if (local_ok && check_dig && R == W - 1 && hpnn_fault_hit("digest")) dig ^= 1; /* test hook */
         struct {
             double loss;
             unsigned long long digest;
             unsigned int hits, ok;
-        } mine = {l, dig, h, (unsigned)ok}, *every = new decltype(mine)[W];
+        } mine = {l, dig, h, (unsigned)local_ok}, *every = new decltype(mine)[W];
         if (hpnn_boot_allgather(&mine, sizeof mine, every) != 0) ok = FALSE;
         ep_loss = 0.0;
         ep_hits = 0;
@@ -1767,23 +1851,30 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             same = same && every[r].digest == every[0].digest;
         }
         delete[] every;
+        if (first && R == 0)
+            NN_DBG(stdout, "data-parallel: epoch 1 (eager, with the weight digest) %.3f ms\n",
+                   1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         if (ok && check_dig && !same) {
             if (R == 0)
                 NN_ERROR(stderr, "data-parallel training: the replicas' weights differ after epoch %u "
-                                 "(exchange error); stopping\n", e + 1);
+                                 "(exchange error); stopping\n", e);
             ok = FALSE;
         }
-        if (ok && hpnn_metrics_active())
-            hpnn_metrics_epoch("gpu-dp-mp", o->epoch0 + e + 1, ep_loss / (double)n, ep_hits, n,
-                               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
-                               (UINT64)n * (e + 1));
+        if (ok && metrics)
+            hpnn_metrics_epoch("gpu-dp-mp", o->epoch0 + e, ep_loss / (double)n, ep_hits, n,
+                               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() - setup_s,
+                               (UINT64)n * e);
     }
     auto t1 = std::chrono::steady_clock::now();
     if (gx) hipGraphExecDestroy(gx);
+    hipStreamSynchronize(s);
+    for (hipEvent_t ev : hev)
+        if (ev) hipEventDestroy(ev);
+    if (hw) hipHostFree(hw);
     if (ok) ok = net.gather_masters(); /* bf16rs: every rank's rows of the FP32 masters */
     if (ok) ok = net.download(k);
     if (ok && st) {
-        st->seconds = std::chrono::duration<double>(t1 - t0).count();
+        st->seconds = std::chrono::duration<double>(t1 - t0).count() - setup_s;
         st->samples = (UINT64)n * o->epochs;
         st->epoch_loss = ep_loss / (double)n;
         st->correct = ep_hits;

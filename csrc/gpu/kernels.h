@@ -144,6 +144,10 @@ int hpnn_resident_capacity(const void *kernel, int threads, size_t dyn_lds);
 /* *out += order-independent 64-bit digest of the nbytes / 4 words at p (word index offset by
  * base, so several buffers can be folded into one digest); *out must be initialised */
 int hpnn_hash_words(const void *p, long nbytes, long base, unsigned long long *out, hipStream_t stream);
+/* load every kernel translation unit's code object onto the current device now (HIP loads a
+ * code object at its first launch, ~0.3 ms each): training loops call it before their clock
+ * starts, so a first eager step does not pay for it.  Once per device; 0 on success. */
+int hpnn_preload_code_objects(void);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
  *   delta  D [B x ldd] BF16  (zero in padded rows/cols)
@@ -366,4 +370,10 @@ long hpnn_online_vec_bytes(const hpnn_online_args *a);
 #ifdef __cplusplus
 }
 #endif
+
+/* one probe kernel per translation unit: hpnn_preload_code_objects() queries its attributes,
+ * which loads that unit's code object onto the device */
+#define HPNN_CO_PROBE(tu)                                                                  \
+    __global__ void hpnn_co_probe_kernel_##tu() {}                                         \
+    extern "C" const void *hpnn_co_probe_##tu(void) { return (const void *)hpnn_co_probe_kernel_##tu; }
 #endif

@@ -42,6 +42,8 @@
 #include <mutex>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(8ph)
 #include "mfma_common.h"
 
 namespace {

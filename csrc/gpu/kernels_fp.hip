@@ -25,6 +25,8 @@
 
 #include "kernels.h"
 
+HPNN_CO_PROBE(fp)
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;

@@ -41,6 +41,8 @@
 #include <type_traits>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(g0)
 #include "mfma_common.h"
 
 namespace {

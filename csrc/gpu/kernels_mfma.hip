@@ -33,6 +33,8 @@
 #include <stdlib.h>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(mfma)
 #include "mfma_common.h"
 
 /* kernels_8ph.hip */

@@ -28,6 +28,8 @@
 
 #include "kernels.h"
 
+HPNN_CO_PROBE(misc)
+
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 namespace {
@@ -914,6 +916,43 @@ extern "C" int hpnn_resident_capacity(const void *kernel, int threads, size_t dy
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, dyn_lds) != hipSuccess)
         cus = per = 0; /* unknown: no grid counts as resident (callers take their other forms) */
     return cache[key] = cus * per;
+}
+
+extern "C" {
+const void *hpnn_co_probe_8ph(void);
+const void *hpnn_co_probe_fp(void);
+const void *hpnn_co_probe_g0(void);
+const void *hpnn_co_probe_mfma(void);
+const void *hpnn_co_probe_mlp3(void);
+const void *hpnn_co_probe_mlp3t(void);
+const void *hpnn_co_probe_mlp3x(void);
+const void *hpnn_co_probe_wide(void);
+const void *hpnn_co_probe_ws(void);
+const void *hpnn_co_probe_online(void);
+const void *hpnn_co_probe_xar(void);
+}
+
+extern "C" int hpnn_preload_code_objects(void) {
+    static std::mutex mu;
+    static std::map<int, int> done; /* device -> result */
+    std::lock_guard<std::mutex> g(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    auto it = done.find(dev);
+    if (it != done.end()) return it->second;
+    const void *probes[] = {hpnn_co_probe_8ph(),  hpnn_co_probe_fp(),   hpnn_co_probe_g0(),    hpnn_co_probe_mfma(),
+                            hpnn_co_probe_misc(), hpnn_co_probe_mlp3(), hpnn_co_probe_mlp3t(), hpnn_co_probe_mlp3x(),
+                            hpnn_co_probe_wide(), hpnn_co_probe_ws(),   hpnn_co_probe_online(), hpnn_co_probe_xar()};
+    /* an empty one-thread launch per unit: the launch is what loads its code object */
+    hipStream_t s = nullptr;
+    int rc = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? 0 : -1;
+    for (const void *k : probes)
+        if (rc == 0 && hipLaunchKernel(k, dim3(1), dim3(1), nullptr, 0, s) != hipSuccess) rc = -2;
+    if (s) {
+        if (hipStreamSynchronize(s) != hipSuccess) rc = -3;
+        (void)hipStreamDestroy(s);
+    }
+    return done[dev] = rc;
 }
 
 extern "C" int hpnn_output_delta(const float *Z, int ldz, const float *T, int ldt, const int *labels, float t_hi,

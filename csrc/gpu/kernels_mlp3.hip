@@ -29,6 +29,8 @@
 #include <stdlib.h>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(mlp3)
 #include "mfma_common.h"
 #include "mlp3_common.h"
 

@@ -58,6 +58,8 @@
 #include <type_traits>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(mlp3t)
 #include "mfma_common.h"
 #include "mlp3_common.h"
 

@@ -32,6 +32,8 @@
 #include <type_traits>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(mlp3x)
 #include "mfma_common.h"
 #include "mlp3_common.h"
 

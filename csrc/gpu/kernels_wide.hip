@@ -55,6 +55,8 @@
 #include <type_traits>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(wide)
 #include "mfma_common.h"
 #include "mlp3_common.h"
 

@@ -25,6 +25,8 @@
 #include <stdlib.h>
 
 #include "kernels.h"
+
+HPNN_CO_PROBE(ws)
 #include "mfma_common.h"
 
 namespace {

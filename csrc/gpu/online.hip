@@ -20,6 +20,8 @@
 
 #include "kernels.h"
 
+HPNN_CO_PROBE(online)
+
 namespace {
 
 constexpr int NTH = 1024;

@@ -823,6 +823,11 @@ BOOL train_tp_threads(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, 
     NN_OUT(stdout, "tensor-parallel batched training: %d ranks (%s, %s), rows of every hidden layer sharded, "
                    "%d samples per step\n",
            P, loopback ? "loopback on one GPU" : "RCCL", Net::name(), B);
+    for (int g = 0; g < P; g++) {
+        hipSetDevice(dev[g]);
+        hpnn_preload_code_objects();
+    }
+    hipSetDevice(dev[0]);
     auto t0 = std::chrono::steady_clock::now();
     if (ok) {
         std::vector<std::thread> th;
@@ -895,6 +900,7 @@ BOOL train_tp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *Tg, UINT n, const
            Net::name(), B);
     double loss = 0.0;
     unsigned int hits = 0;
+    hpnn_preload_code_objects();
     auto t0 = std::chrono::steady_clock::now();
     if (ok) ok = run_rank<Net>(net, n, o, B, &loss, &hits);
     auto t1 = std::chrono::steady_clock::now();

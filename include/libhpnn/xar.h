@@ -108,6 +108,9 @@ typedef struct {
 int hpnn_xar_view_get(hpnn_xar *c, hpnn_xar_view *v);
 /* 0 healthy, -1 a barrier timed out on this rank (a peer never arrived) */
 int hpnn_xar_status(hpnn_xar *c);
+/* the error word copied into *dst (pinned host memory) on `stream` without waiting; non-zero
+ * once the event after it completes = hpnn_xar_status's -1 */
+int hpnn_xar_status_enqueue(hpnn_xar *c, unsigned int *dst, hipStream_t stream);
 /* collective self-test, run by every rank right after hpnn_xar_open: all-reduces known
  * rank-dependent vectors (every partial sum exact in FP32, so any summation order gives
  * the same bits) at a one-shot size and at the full buffer size, twice each so both

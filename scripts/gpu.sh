@@ -72,7 +72,7 @@ for spec in "$@"; do
            step cache_d8 300 python bench.py --steps 200 --warmup 20 --datasets 8 &&
            step cache_d4b 300 python bench.py --steps 200 --warmup 20 --datasets 4 &&
            step cache_d8b 300 python bench.py --steps 200 --warmup 20 --datasets 8 ;;
-    py:*) a=${s#py:}; step "py_$(basename ${a%%,*} .py)" 600 python ${a//,/ } ;;
+    py:*) a=${s#py:}; step "py_$(basename ${a%%,*} .py)" 600 python scripts/${a//,/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   exit $FAILED

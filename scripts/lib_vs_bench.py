@@ -58,8 +58,12 @@ def run_train_nn(name, batches, epochs, work, dtype="bf16", dpforce=False):
         raise SystemExit("train_nn did not replay HIP graphs on the data-parallel path:\n" + r.stdout[-3000:])
     samples, secs = int(m.group(1)), float(m.group(2))
     steps = epochs * batches
-    return {"us_per_step": secs / steps * 1e6, "steps": steps, "samples": samples, "seconds": secs,
-            "plan_mode": mode.group(1) if mode else None}
+    rec = {"us_per_step": secs / steps * 1e6, "steps": steps, "samples": samples, "seconds": secs,
+           "plan_mode": mode.group(1) if mode else None}
+    e1 = re.search(r"epoch 1 \(eager, with the weight digest\) ([0-9.]+) ms", r.stdout)
+    if e1:
+        rec["first_epoch_ms"] = float(e1.group(1))
+    return rec
 
 
 def run_bench(name, steps, dpforce=False):
