@@ -23,7 +23,10 @@
  *     8 KiB of pixels) is loaded once per workgroup, one 16-byte load per lane,
  *     converted in registers and written as the transposed image X^T [32 feat][256
  *     samples] into one of two LDS stages; MFMA B operands are read from it with
- *     ds_read_b64_tr_b16.  (Measured and not kept, round 4: every wave loading its X
+ *     ds_read_b64_tr_b16.  The k-step's MFMAs are interleaved with its conversion VALU and B
+ *     reads (sched_group_barrier: MFMA, LDS read, VALU, ...): an MFMA holds the SIMD's vector
+ *     issue for 8 of its 16 cycles, so that work issues in the other 8 instead of in series
+ *     (phase A 24.0K vs 26.0K ticks).  (Measured and not kept, round 4: every wave loading its X
  *     fragments straight into registers from a row-fragment-major copy -- no X^T stage, no
  *     barrier in phase A: the four neuron-group waves then pull 4x the X bytes through the
  *     vector L1; phase A 31.2K vs 27.0K ticks, the drifted waves meeting at the H1 barrier
@@ -95,7 +98,7 @@ constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool TRADE = false, bool XORD = false>
+          bool TRADE = false, bool XORD = false, int IL = 1>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                 if constexpr (EARLY)
                     if (s + 2 < KS && ABL != 5 && ABL != 8 && ABL != 9) convert(s + 2);
                 if (s + 1 < KS && ABL != 4 && ABL != 8 && ABL != 9) read_b(s + 1, bb[(s + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (IL == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int st = 0; st < STA; st++) {
                     if constexpr (ABL != 3) {
@@ -296,6 +299,18 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
                     } else {
                         acc[0][st] += __builtin_bit_cast(f32x4, wr[s][0]) * 0.f;
                     }
+                }
+                if constexpr (IL > 0) {
+                    /* IL: the k-step's MFMAs interleaved with its conversion VALU and LDS traffic
+                     * (one MFMA, one LDS read, IL VALU ops, ...), so the wave issues them in the
+                     * shadow of its own MFMA pipe instead of in series with it */
+#pragma unroll
+                    for (int i = 0; i < 2 * STA; i++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, IL, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (!EARLY)
@@ -547,6 +562,9 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
     if constexpr (TYPE == 2 && LABELS && KS == 25 && XU8) {
 #ifdef HPNN_ABLATIONS
         /* A/B variants that measured slower (make ABLATIONS=1 builds only):
+         * HPNN_TILE_IL=0: the round-4 k-step schedule (conversion, B reads, then the 16 MFMAs as
+         *   one block): phase A 26.0K vs 24.0K ticks, 58.9 / 59.0 vs 58.6 / 58.3 us per step
+         *   (profiles/r5/SUMMARY.md);
          * HPNN_TILE_EARLY=0: X(s + 2) converted after the MFMAs of step s (equal within noise);
          * HPNN_TILE_TRADE=1: the chain's 8-byte image stores / loads with a lane-pair trade of
          *   halves -- LDS bank conflicts 18.5 % -> 5.6 %, but 60.6 / 61.4 / 62.5 vs 59.9 / 59.8 /
@@ -558,6 +576,9 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
         static const bool late = [] { const char *e = getenv("HPNN_TILE_EARLY"); return e && e[0] == '0'; }();
         static const bool trade = [] { const char *e = getenv("HPNN_TILE_TRADE"); return e && e[0] == '1'; }();
         static const bool xord = [] { const char *e = getenv("HPNN_TILE_XORD"); return e && e[0] == '1'; }();
+        static const bool il0 = [] { const char *e = getenv("HPNN_TILE_IL"); return e && e[0] == '0'; }();
+        if (il0) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, 0>, 512)
+                              : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, false, 0>, 512);
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
         if (trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true>, 512);
         if (xord) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, true>, 512);
