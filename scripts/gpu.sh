@@ -12,7 +12,7 @@
 #   dpforce               the N > 1 MNIST path with one rank under torchrun
 #   trace                 tile-front phase trace (HPNN_TILE_TRACE=1)
 #   prof / prof_rruff     rocprofv3 kernel table (--graph 0)
-#   pmc / pmc_rruff       PMC passes of the step (scripts/pmc_step.sh)
+#   pmc / pmc_rruff       PMC passes of the step (scripts/pmc_step.sh); pmc_d8: 8 cycled batches
 #   rehearse              2 ranks sharing the GPU (scripts/rehearse.sh)
 #   libbench / libbench_dp   train_nn vs bench.py (scripts/lib_vs_bench.py; _dp: the N > 1 path, one rank)
 #   learn                 scripts/learnability.py
@@ -63,6 +63,7 @@ for spec in "$@"; do
     prof_synth1k) step rocprof_synth1k 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_synth1k -o run -- python3 bench.py --model synth --batch 1024 --steps 20 --warmup 5 --graph 0 ;;
     pmc) PMC_TAG=_$tag step pmc 600 bash scripts/pmc_step.sh ;;
     pmc_rruff) PMC_TAG=_${tag}_rruff step pmc_rruff 600 bash scripts/pmc_step.sh --model rruff ;;
+    pmc_d8) PMC_TAG=_${tag}_d8 step pmc_d8 600 bash scripts/pmc_step.sh --datasets 8 ;;
     rehearse) step rehearse 600 bash scripts/gpu_rehearse.sh ;;
     libbench) step libbench 900 python scripts/lib_vs_bench.py --out $O/lib_vs_bench.jsonl ;;
     libbench_dp) step libbench_dp 900 python scripts/lib_vs_bench.py --dpforce --configs mnist --out $O/lib_vs_bench_dp.jsonl ;;
