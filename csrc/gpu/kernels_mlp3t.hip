@@ -11,8 +11,11 @@
  * ops.to_fragment_major), either 8-bit pixels (the exact integers in BF16, the pixel scale
  * xscale applied to the FP32 accumulator: H1 = f(xscale * X W0^T)) or BF16 (xscale 1).
  * It is the SAME buffer the first-layer gradient kernel (kernels_g0.hip,
- * gemm_fm_direct) streams right after this one, so a step reads the batch from HBM
- * once; the second read is served by the 256 MB Infinity Cache.
+ * gemm_fm_direct) streams right after this one, so the second read of a step finds it in
+ * the 256 MB Infinity Cache.  Where the front's read comes from depends on the data: with
+ * bench.py's 4 cycled 52 MB batches part of it is still cached from 4 steps before, with 8
+ * (past the cache) the step is 3.5 % slower (profiles/r5/SUMMARY.md; the L2-side counters
+ * cannot separate Infinity-Cache hits from HBM reads).
  *
  * One 512-thread workgroup (8 waves) per CU; per 256-sample tile:
  *
