@@ -384,6 +384,20 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
 #define HPNN_NT(BN_)                                                                                  \
     return k64 ? launch_nt_bn<BN_, 64, EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s)      \
                : launch_nt_bn<BN_, 32, EPI, CF32>(A, lda, B, ldb, C, ldc, aux, ldaux, M, N, K, s)
+    /* grids of fewer than two 128 x 128 tiles per CU (the 8 x 4096 net at its 8-GPU shard,
+     * M = 1024: 256 tiles): 8 waves (2 x 4, 64 x 32 wave tiles) and a 3-stage ring, one
+     * workgroup per CU with two waves per SIMD, instead of the 4-wave tile's one.  Synthetic
+     * 8 x 4096 step at batch 1024: 1.60 / 1.60 vs 1.68 / 1.67 ms; 2 stages 1.65, 4 stages
+     * 1.59, 5 stages 1.57-1.59, 128 x 64 tiles (two 4-wave workgroups per CU) 1.70
+     * (profiles/r5/SUMMARY.md).  HPNN_NT_SMALL=0: the 4-wave tile. */
+    static const bool small_off = [] { const char *e = getenv("HPNN_NT_SMALL"); return e && e[0] == '0'; }();
+    if (!small_off && k64 && M % 128 == 0 && N % 128 == 0 && (long)(M / 128) * (N / 128) < 512) {
+        const int tiles_n = N / 128, tiles_m = M / 128;
+        hipLaunchKernelGGL((gemm_nt_pipe_kernel<128, 128, 64, 2, 4, 3, EPI, CF32>), dim3(tiles_m * tiles_n), dim3(512),
+                           0, s, (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux,
+                           K, tiles_n);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     if (N % 128 == 0 && N >= 128) { HPNN_NT(128); }
     if (N % 64 == 0) { HPNN_NT(64); }
     HPNN_NT(32);
