@@ -12,6 +12,9 @@
 namespace hpnn {
 
 DpExchange::~DpExchange() {
+    if (p_)
+        for (int l = 0; l < p_->L; l++) p_->g16[l] = nullptr;
+    hpnn_dev_free(grad16_);
     hpnn_dev_free(send16_);
     hpnn_dev_free(recv16_);
 }
@@ -43,6 +46,18 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
     if (mx && (hpnn_dev_malloc(&send16_, mx * 2) != hipSuccess ||
                hpnn_dev_malloc(&recv16_, mx * 2 / world_ + 64) != hipSuccess))
         return -7;
+    /* one BF16 gradient buffer per sharded layer: the plan's TN GEMM writes it directly (no
+     * FP32 round trip and cast), the side stream reduce-scatters it while the next layer's
+     * gradient goes into its own buffer */
+    size_t tot = 0;
+    for (int l = 0; l < p_->L; l++)
+        if (sharded_[l]) tot += (size_t)p_->Np[l] * p_->Kp[l];
+    if (tot && hpnn_dev_malloc(&grad16_, tot * 2) != hipSuccess) return -7;
+    for (size_t l = 0, o = 0; l < (size_t)p_->L; l++)
+        if (sharded_[l]) {
+            p_->g16[l] = (char *)grad16_ + o * 2;
+            o += (size_t)p_->Np[l] * p_->Kp[l];
+        }
     return 0;
 }
 
@@ -57,8 +72,11 @@ int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, i
         if (!side) return -2;
         const int N = p_->Np[l], K = p_->Kp[l], rp = N / world_;
         const long cnt = (long)rp * K, off = (long)rank_ * cnt;
-        int r = hpnn_cast_f32_bf16(p_->gflat + p_->goff[l], send16_, (long)N * K, side);
-        if (!r) r = hpnn_comm_reduce_scatter(c_, send16_, recv16_, cnt, HPNN_DT_BF16, HPNN_OP_SUM, side);
+        const void *src = send16_;
+        int r = 0;
+        if (p_->g16[l] && p_->g16_used[l]) src = p_->g16[l]; /* the GEMM wrote BF16 already */
+        else r = hpnn_cast_f32_bf16(p_->gflat + p_->goff[l], send16_, (long)N * K, side);
+        if (!r) r = hpnn_comm_reduce_scatter(c_, src, recv16_, cnt, HPNN_DT_BF16, HPNN_OP_SUM, side);
         if (!r)
             r = hpnn_sgd_update_rows_bf16g(p_->W32[l] + off, p_->V32[l] ? p_->V32[l] + off : nullptr, recv16_, cnt, lr,
                                            alpha, scale, mom, (char *)p_->Wb[l] + off * 2, side);

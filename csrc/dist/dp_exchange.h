@@ -48,6 +48,7 @@ class DpExchange {
     Mode mode_ = FP32;
     std::vector<bool> sharded_;
     void *send16_ = nullptr, *recv16_ = nullptr;
+    void *grad16_ = nullptr; /* per-layer BF16 gradients written by the plan's TN GEMM (sharded layers) */
 };
 
 }  // namespace hpnn

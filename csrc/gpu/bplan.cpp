@@ -292,6 +292,12 @@ int BPlan::grad_layer(int l, const XIn &x, bool reduce, hipStream_t s) {
     } else {
         if (l == 0 && mode == 't') return -2; /* the tile path's input is fragment-major only */
         const void *Hin = l ? H[l - 1] : x.x;
+        g16_used[l] = false;
+        if (reduce && S[l] == 1 && g16[l] &&
+            hpnn_gemm_tn8_bf16out(D[l], Np[l], Hin, Kp[l], g16[l], Kp[l], Np[l], Kp[l], Bp, s) == 0) {
+            g16_used[l] = true; /* BF16 straight into the exchange's send buffer */
+            return 0;
+        }
         if (reduce && S[l] == 1) /* one split: the GEMM writes the all-reduce bucket itself */
             return hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], gflat + goff[l], Kp[l], Np[l], Kp[l], Bp, 1, s);
         r = hpnn_gemm_tn_bf16(D[l], Np[l], Hin, Kp[l], slab[l], Kp[l], Np[l], Kp[l], Bp, S[l], s);

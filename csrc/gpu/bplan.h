@@ -168,6 +168,11 @@ class BPlan {
     float *wpbuf = nullptr;
     unsigned int *wwords = nullptr, *g0cnt = nullptr, *tncnt = nullptr;
     int *lab0 = nullptr;
+    /* data-parallel BF16 exchange (csrc/dist/dp_exchange.cpp): where grad_layer(reduce) may
+     * write layer l's gradient as BF16 instead of FP32 into gflat (NULL: FP32), and whether the
+     * last call did (shapes the 8-phase kernel does not cover stay FP32) */
+    void *g16[16] = {0};
+    bool g16_used[16] = {0};
 
   private:
     std::vector<void *> ptr_;

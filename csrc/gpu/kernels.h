@@ -53,6 +53,9 @@ int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, vo
 /* weight gradient of one layer over the whole batch with the optimizer step fused into the
  * 8-phase TN kernel's epilogue (no gradient in memory): the step of hpnn_sgd_update with one
  * slab.  N % 256 == 0, M % 256 == 0, Bt % 128 == 0, else -1. */
+/* G = D^T H (one split) rounded to BF16 into G16 [N][ldg] (8-phase kernel); -1: shape not covered */
+int hpnn_gemm_tn8_bf16out(const void *D, int ldd, const void *H, int ldh, void *G16, int ldg, int N, int M, int Bt,
+                          hipStream_t stream);
 int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
                          void *Wbf, void *Wt, float lr, float alpha, float scale, int momentum, hipStream_t stream);
 /* the same with the gradient over `splits` (>= 2) split-K slabs reduced inside the launch (each

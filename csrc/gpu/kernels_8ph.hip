@@ -287,7 +287,9 @@ struct Tn8Upd {
 
 constexpr unsigned long long TN8_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
-/* MODE 0: split-K slabs; 1: one split, the optimizer step in the epilogue; 2: several splits,
+/* MODE 0: split-K slabs; 3: one split, the product rounded to BF16 into upd.Wb [N][ldg] (the
+ * data-parallel exchange's send buffer: no FP32 gradient round trip); 1: one split, the
+ * optimizer step in the epilogue; 2: several splits,
  * each publishes its partial tile write-through and takes a ticket, then -- once every split
  * of the tile has arrived -- reduces 1/splits of the tile over the splits in a fixed order
  * and applies the step there (the split-K reduction and the update launch of the RRUFF-shaped
@@ -590,6 +592,22 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
             const int e = t * 64 + lane, ml = e >> 3, nc = (e & 7) * 8;
             *(bf16x8 *)(Wt + (size_t)(m0 + wm * 128 + ml) * N + n0 + wn * 64 + nc) = *(const bf16x8 *)(tw + ml * 64 + nc);
         }
+    } else if constexpr (MODE == 3) {
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
+                        const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                        bf16x4 gb;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) gb[r] = (__bf16)acc[mi][ni][i][j][r];
+                        *(bf16x4 *)(upd.Wb + (size_t)n * ldg + m) = gb;
+                    }
     } else {
 #pragma unroll
         for (int mi = 0; mi < 2; mi++)
@@ -712,6 +730,22 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     hipLaunchKernelGGL(gemm_tn8_kernel<0>, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream,
                        (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles,
                        tail, Tn8Upd{});
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* G = D^T H over the whole batch (one split), rounded to BF16 into G16 [N][ldg]: -1 when the
+ * shape does not fit the 8-phase kernel */
+extern "C" int hpnn_gemm_tn8_bf16out(const void *D, int ldd, const void *H, int ldh, void *G16, int ldg, int N, int M,
+                                     int Bt, hipStream_t stream) {
+    if (N % 256 || M % 256 || Bt % 128 || ldd % 8 || ldh % 8 || ldg % 4 || ((uintptr_t)G16 & 7)) return -1;
+    const int units = Bt / 64;
+    if (units % 2) return -1;
+    if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
+    const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
+    Tn8Upd u{};
+    u.Wb = (__bf16 *)G16;
+    hipLaunchKernelGGL(gemm_tn8_kernel<3>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
+                       (const __bf16 *)H, ldh, nullptr, ldg, N, units, 1, tiles_n, ntiles, hpnn::TnTail{}, u);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
