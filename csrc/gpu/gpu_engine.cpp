@@ -1270,10 +1270,10 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
         }
         return true;
     };
-    /* ne epochs back to back, each from zeroed statistics (so the last one's remain) */
+    /* ne epochs back to back; the statistics are zeroed before the last (the only one read) */
     auto epochs = [&](int ne) -> bool {
         for (int i = 0; i < ne; i++)
-            if (hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess || !epoch()) return false;
+            if ((i + 1 == ne && hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess) || !epoch()) return false;
         return true;
     };
     /* one graph replays epg epochs (about 32 steps: the host launches once per replay); with
@@ -1706,6 +1706,14 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     /* preflight: the plan and the exchange start clean (and the first reads of their words, a
      * few ms while the runtime maps them, stay out of the training time) */
     if (ok) ok = enqueue_check(0) && finish_check(0);
+    {
+        /* ... and every other readback of the agreement points once (statistics, digest):
+         * their first calls set up host staging and copy paths (ms) */
+        double l0 = 0.0;
+        unsigned int h0 = 0;
+        unsigned long long d0 = 0;
+        if (ok) ok = net.read_stats(&l0, &h0) && net.digest(&d0);
+    }
     /* setup (data upload and layout conversions) is finished before the clock starts */
     if (hipDeviceSynchronize() != hipSuccess) ok = FALSE;
     auto t0 = std::chrono::steady_clock::now();
@@ -1714,8 +1722,9 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     /* one epoch's steps: the same launches on every rank, every epoch (the minibatch order is
      * fixed), so from the second epoch on they replay as ONE HIP graph per epoch -- the
      * launches bench.py times (the first epoch runs eagerly: it settles the exchange form) */
-    auto epoch_steps = [&](UINT e) -> bool {
-        if (hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess) return false;
+    /* reset: zero the statistics first (only the last epoch of a replay group is ever read) */
+    auto epoch_steps = [&](UINT e, bool reset = true) -> bool {
+        if (reset && hipMemsetAsync(net.acc, 0, Net::ACC_BYTES, s) != hipSuccess) return false;
         for (int b = 0; b < n_batches; b++) {
             const int end = (b * B + B < (int)n) ? b * B + B : (int)n;
             const int start = b * B + R * Bg;
@@ -1789,7 +1798,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             const auto c0 = std::chrono::steady_clock::now();
             int cap = capture_epoch(s, [&]() {
                 for (UINT i = 0; i < epg; i++)
-                    if (!epoch_steps(e + i)) return false;
+                    if (!epoch_steps(e + i, i + 1 == epg)) return false;
                 return true;
             }, &gx) ? 1 : 0;
             std::vector<int> caps(W);
@@ -1810,7 +1819,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
             lok = hipGraphLaunch(gx, s) == hipSuccess;
         } else {
             lok = true;
-            for (UINT i = 0; i < ne && lok; i++) lok = epoch_steps(e + i);
+            for (UINT i = 0; i < ne && lok; i++) lok = epoch_steps(e + i, i + 1 == ne);
         }
         e += ne;
         if (e > 1) replays++;
