@@ -62,6 +62,7 @@ for spec in "$@"; do
     g0trace) HPNN_G0_TRACE=1 step g0_trace 200 python scripts/g0_trace.py ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 50 --warmup 10 --graph 0 ;;
     prof_rruff) step rocprof_rruff 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rruff -o run -- python3 bench.py --model rruff --steps 30 --warmup 5 --graph 0 ;;
+    prof_synth1k_noupd) HPNN_TN_UPD=0 step rocprof_synth1k_noupd 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_synth1k_noupd -o run -- python3 bench.py --model synth --batch 1024 --steps 20 --warmup 5 --graph 0 ;;
     prof_synth1k) step rocprof_synth1k 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_synth1k -o run -- python3 bench.py --model synth --batch 1024 --steps 20 --warmup 5 --graph 0 ;;
     pmc) PMC_TAG=_$tag step pmc 600 bash scripts/pmc_step.sh ;;
     pmc_rruff) PMC_TAG=_${tag}_rruff step pmc_rruff 600 bash scripts/pmc_step.sh --model rruff ;;
