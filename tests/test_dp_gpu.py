@@ -123,12 +123,14 @@ def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sizes,expect", [([2048, 1024, 10], "bf16rs"), ([300, 96, 64, 7], "fp32")])
+@pytest.mark.parametrize("sizes,expect", [([2048, 1024, 10], "bf16rs"), ([300, 96, 64, 7], "fp32"),
+                                          ([4096, 4096, 32], "bf16rs")])
 def test_native_dp_exchange_auto_default(gpu, monkeypatch, sizes, expect):
     """grad_comm defaults to "auto": a per-layer net with more than 4 MB of FP32 gradients takes
     the BF16 reduce-scatter + sharded step on the N > 1 path (here one rank, HPNN_DPX_FORCE);
     small ones the FP32 all-reduce.  Both train like the plain step (bf16rs within the BF16
-    rounding of the gradient)."""
+    rounding of the gradient).  4096 x 4096 at batch 1024 is one 8-phase TN split: its GEMM
+    writes the BF16 gradient the exchange sends (gemm_tn8_kernel<3>, BPlan::g16)."""
     monkeypatch.setenv("HPNN_DPX_FORCE", "1")
     monkeypatch.setenv("HPNN_DPX_SHARD1", "1")
     dev = torch.device("cuda", 0)
