@@ -140,8 +140,9 @@ def test_native_dp_exchange_auto_default(gpu, monkeypatch, sizes, expect):
         g = torch.Generator(device=dev).manual_seed(5)
         Xr = torch.rand(B, sizes[0], device=dev, generator=g)
         L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
-        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
-        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        init = "fast" if sizes[0] * sizes[1] > 1 << 22 else "reference"
+        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False, init=init)
+        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False, init=init)
         w0 = [w.clone() for w in b.host_weights()]
         dp = DataParallel(a, comm="native")
         assert dp.grad_comm == expect and bool(dp.sharded) == (expect == "bf16rs")
