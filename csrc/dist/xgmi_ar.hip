@@ -173,12 +173,15 @@ __device__ __forceinline__ float4 xar_load_in(const XarIn &in, long i) {
     return xar_load_in_u<8>(p, in.stride4[j], S);
 }
 
-/* sum of element i over the first `world` data halves, rank order */
+/* sum of element i over the first `world` data halves, rank order.  The 8 loads go out in
+ * one block; slots past `world` re-read this rank's OWN half (local memory) and are dropped --
+ * re-reading rank 0's instead would put world - 1 .. 7 extra reads per element on the xGMI
+ * link of every other rank (6 extra at world 2). */
 static_assert(HPNN_XAR_MAX_RANKS == 8, "one ld_sc1_x8 per element");
-__device__ __forceinline__ float4 sum_peers(const XarPeers &P, long half4, int world, long i) {
+__device__ __forceinline__ float4 sum_peers(const XarPeers &P, long half4, int world, int rank, long i) {
     const float *q[8];
 #pragma unroll
-    for (int p = 0; p < 8; p++) q[p] = (const float *)(P.buf[p < world ? p : 0] + half4 + i);
+    for (int p = 0; p < 8; p++) q[p] = (const float *)(P.buf[p < world ? p : rank] + half4 + i);
     hpnn::f32x4 v[8];
     hpnn::ld_sc1_x8<true>(v, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
     hpnn::f32x4 s = v[0];
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
             if (i0 < hi) pre = xar_pre(upd, i0); /* in flight while the barrier waits */
         xbarrier(P, rank, world, b, e, 0, timeout, in.nseg ? light : (light ? 2 : 0));
         for (long i = i0; i < hi; i += blockDim.x) {
-            const float4 v = sum_peers(P, half4, world, i);
+            const float4 v = sum_peers(P, half4, world, rank, i);
             out[i] = v;
             if constexpr (UPD) xar_update4(upd, i, v, i == i0 ? &pre : nullptr);
         }
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(256) void xar_kernel(XarPeers P, int rank, int worl
         xbarrier(P, rank, world, b, e, 0, timeout, in.nseg ? light : (light ? 2 : 0));
         range(rank, lo, hi);
         for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-            const float4 v = sum_peers(P, half4, world, i);
+            const float4 v = sum_peers(P, half4, world, rank, i);
             mine[i] = v;
             out[i] = v;
             if constexpr (UPD) xar_update4(upd, i, v);

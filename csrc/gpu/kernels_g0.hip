@@ -324,7 +324,7 @@ static_assert(HPNN_XAR_MAX_RANKS == 8, "one ld_sc1_x8 per element");
 __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
     const float *q[8];
 #pragma unroll
-    for (int p = 0; p < 8; p++) q[p] = v.buf[p < v.world ? p : 0] + o;
+    for (int p = 0; p < 8; p++) q[p] = v.buf[p < v.world ? p : v.rank] + o; /* spare slots: local */
     f32x4 x[8];
     hpnn::ld_sc1_x8<true>(x, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
     f32x4 a = x[0];
