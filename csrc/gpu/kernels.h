@@ -148,8 +148,8 @@ int hpnn_resident_capacity(const void *kernel, int threads, size_t dyn_lds);
  * base, so several buffers can be folded into one digest); *out must be initialised */
 int hpnn_hash_words(const void *p, long nbytes, long base, unsigned long long *out, hipStream_t stream);
 /* load every kernel translation unit's code object onto the current device now (HIP loads a
- * code object at its first launch, ~0.3 ms each): training loops call it before their clock
- * starts, so a first eager step does not pay for it.  Once per device; 0 on success. */
+ * code object at its first launch): training loops call it before their clock starts, so a
+ * first eager step does not pay for it.  Once per device; 0 on success. */
 int hpnn_preload_code_objects(void);
 
 /* output layer: logits Z [B x ldz] FP32 (n_out valid columns) ->
