@@ -126,7 +126,8 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
          * row reads conflict-free).  Stage s: 48 one-KiB pieces, 6 per wave.  In the middle of
          * stage s each wave waits (counted vmcnt) for its own pieces of stage s + 1 and passes
          * one barrier (every wave's pieces landed; every wave's reads of stage s retired), then
-         * refills stage s's slot with stage s + RING; fragment reads run one 32-feature half
+         * refills stage s's slot with stage s + RING (waves 4-7 after the stage's second MFMA
+         * block); fragment reads run one 32-feature half
          * ahead of their 16 MFMAs.  All vmcnt waits are the kernel's own: no compiler-visible
          * loads in the loop. */
         constexpr int SX = TS * 128, STG2 = SX + HW * 128, RING = 3, PW = (TS / 8 + HW / 8) / 8;
@@ -181,10 +182,15 @@ __global__ __launch_bounds__(512) void wide2_kernel(const __bf16 *__restrict__ X
                 const int last = st + RING - 1 < NS - 1 ? st + RING - 1 : NS - 1; /* last stage issued */
                 wait_stages(last - (st + 1));
                 lds_barrier(); /* stage st + 1 landed everywhere; every read of stage st retired */
-                if (st + RING < NS) issue(st + RING);
+                if (st + RING < NS && wave < 4) issue(st + RING);
                 read(st + 1, 0);
             }
             mma(1);
+            /* waves 4-7 (the SIMD partners of 0-3) refill after their second MFMA block, so the
+             * two waves of a SIMD do not issue their LDS-DMA pieces (~60 issue cycles each)
+             * together: phase A 75.9K vs 77.4K ticks, 66.2-68.1 vs 68.5-70.8 us per launch
+             * (profiles/r5/SUMMARY.md).  Same count of pieces before every counted wait. */
+            if (wave >= 4 && st + 1 < NS && st + RING < NS) issue(st + RING);
         }
         }
     }
