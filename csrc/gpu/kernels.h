@@ -129,7 +129,8 @@ typedef struct {
     hpnn_xar_view xv;
     int proto; /* hand-off diagnostics (HPNN_G0_PROTO, make ABLATIONS=1 builds only): 1 producer agent
                 * release, 2 consumer agent acquire, 4 system-scope (sc0 sc1) partial loads, 8 system
-                * acquire after the exchange barrier, 16 no exchange barrier, 64 no W / V prefetch */
+                * acquire after the exchange barrier, 16 no exchange barrier, 32 one exchange load
+                * block per element (not one for both), 64 no W / V prefetch */
     int fault; /* test hook (HPNN_FAULT=handoff:n): the split-K wait of that launch reports a
                 * timeout (sets *err) as a real one would */
 } hpnn_g0_update;

@@ -389,6 +389,52 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
             }
         barrier(1);
     }
+    /* at most one G0 and one [G1 | G2] element per thread (the MNIST grid: ~107 and ~11 float4
+     * per workgroup): both elements' remote loads go out in ONE block and one wait -- over xGMI
+     * each wait is a link round trip, so two in series would cost the step a second one */
+    if (e1 - e0 <= NT && c1 - c0 <= NT && (two || v.world <= 4) && !G0_PROTO(u, 32)) { /* 32: ablation */
+        const bool h0 = e0 + t < e1, h12 = c0 + t < c1;
+        const long oa = h0 ? hoff + g0_off(e0 + t) : hoff, ob = h12 ? hoff + (long)N * ldg + (c0 + t) * 4 : hoff;
+        f32x4 ga, gb;
+        if (two) { /* the owners' sums (owner of element j = t: rank t % world) */
+            const float *qa = v.buf[h0 ? t % v.world : v.rank] + oa, *qb = v.buf[h12 ? t % v.world : v.rank] + ob;
+            asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+                         "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+                         "s_waitcnt vmcnt(0)"
+                         : "=&v"(ga), "=&v"(gb)
+                         : "v"(qa), "v"(qb)
+                         : "memory");
+        } else { /* one-shot, world <= 4: rank-order sums of both, 4 slots each (spares local) */
+            f32x4 x[8];
+            const float *q[8];
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                q[p] = v.buf[p < v.world ? p : v.rank] + oa;
+                q[4 + p] = v.buf[p < v.world ? p : v.rank] + ob;
+            }
+            hpnn::ld_sc1_x8<true>(x, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
+            ga = x[0];
+            gb = x[4];
+#pragma unroll
+            for (int p = 1; p < 4; p++)
+                if (p < v.world) {
+                    ga += x[p];
+                    gb += x[4 + p];
+                }
+        }
+        if (h0) {
+            const int c = e0 + t, row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
+            step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, ga, u,
+                       pf && t < 128, pg0);
+        }
+        if (h12) {
+            int n, k;
+            const int l = g12_elem(u, c0 + t, n, k);
+            step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k,
+                       gb, u, pf && t < 16, pg12);
+        }
+        return;
+    }
     /* one-shot: the rank-order sum over every peer; two-shot: the owner's sum */
     auto fetch = [&](long o, long j) -> f32x4 {
         if (!two) return xsum_peers(v, o);
