@@ -18,6 +18,7 @@ Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -69,6 +70,12 @@ def main():
     ap.add_argument("--grad-comm", choices=["auto", "fp32", "bf16rs"], default="auto",
                     help="data-parallel gradient exchange: FP32 all-reduce, or BF16 reduce-scatter + sharded "
                          "optimizer step + BF16 weight all-gather (half the bytes; per-layer models only)")
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed steps for about this long before the warmup, so the timed steps see the GPU at "
+                         "its steady clock (the first ~20 ms of steps after idle run 10-20%% slower; "
+                         "profiles/r5/SUMMARY.md); 0: off")
+    ap.add_argument("--replay-trace", default="",
+                    help="diagnostics: write the GPU time of every timed graph replay (ms) to this JSON file")
     args = ap.parse_args()
 
     # HPNN_BENCH_REHEARSE=1: rehearse the N > 1 path with several ranks on ONE GPU -- gloo
@@ -191,16 +198,35 @@ def main():
             graphs.clear()
             use_graph = False
 
-    def run_steps(first, n):
+    marks = []  # --replay-trace: one event after each timed replay
+
+    def run_steps(first, n, trace=False):
         if use_graph:
             for _ in range(n // gsteps):
                 graphs[gsteps].replay()
+                if trace:
+                    marks.append(torch.cuda.Event(enable_timing=True))
+                    marks[-1].record()
             if n % gsteps:
                 graphs[n % gsteps].replay()
         else:
             for i in range(first, first + n):
                 step(i)
 
+    # settle: whole steps for ~settle_ms (the same count on every rank: the steps hold
+    # collectives), then the W warmup steps, then the K timed steps
+    settle = 0
+    if args.settle_ms > 0:
+        t_a = time.perf_counter()
+        run_steps(0, gsteps)
+        torch.cuda.synchronize()
+        est = torch.tensor([(time.perf_counter() - t_a) / gsteps], dtype=torch.float64,
+                           device="cpu" if rehearse else dev)
+        if world > 1:
+            dist.all_reduce(est, op=dist.ReduceOp.MAX)
+        settle = gsteps * max(0, math.ceil(args.settle_ms * 1e-3 / max(float(est.item()), 1e-6) / gsteps) - 1)
+        run_steps(gsteps, settle)
+        settle += gsteps
     run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if world > 1 and rank == world - 1 and native().fault_hit("weights"):
@@ -212,11 +238,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(args.warmup, args.steps)
+    if args.replay_trace:
+        marks.append(torch.cuda.Event(enable_timing=True))
+        marks[-1].record()
+    run_steps(args.warmup, args.steps, bool(args.replay_trace))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    if args.replay_trace and rank == 0:
+        with open(args.replay_trace, "w") as f:
+            json.dump({"steps_per_replay": gsteps,
+                       "replay_ms": [a.elapsed_time(b) for a, b in zip(marks, marks[1:])]}, f)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cpu" if rehearse else dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -259,6 +292,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": scaling,

@@ -76,10 +76,19 @@ __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nb
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
-    if (xcd_map) { /* the tiles of one batch slice on one XCD: its Dt slice is fetched once into that L2 */
-        const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-        tile = j % tiles;
-        split = xcd + 8 * (j / tiles);
+    if (xcd_map) {
+        /* the tiles of one batch slice on one XCD (workgroup b runs on XCD b % 8): its Dt slice
+         * is fetched once into that L2.  8 * (splits / 8) splits map that way; the rest (splits
+         * not a multiple of 8) take the last workgroups in plain order */
+        const int b = blockIdx.x, main = (splits / 8) * 8 * tiles;
+        if (b < main) {
+            const int xcd = b & 7, j = b >> 3;
+            tile = j % tiles;
+            split = xcd + 8 * (j / tiles);
+        } else {
+            tile = (b - main) % tiles;
+            split = (splits / 8) * 8 + (b - main) / tiles;
+        }
     } else {
         tile = blockIdx.x % tiles;
         split = blockIdx.x / tiles;
@@ -590,7 +599,7 @@ int launch_fm(const void *Dg, const void *Hg, float hscale, float *slab, int ldg
               hipStream_t s, const TnTail &tail) {
     constexpr int TMF = 32 * WF, TNH = 32 * WH;
     const int tiles_n = N / TNH, tiles = (M / TMF) * tiles_n;
-    const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+    const int xcd_map = (splits >= 8 && tiles > 1) ? 1 : 0;
     hipLaunchKernelGGL((gemm_fm_direct_kernel<WF, WH, PD, KW, HU8>), dim3(tiles * splits + tail.blocks),
                        dim3(256 * KW), 0, s, (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32,
                        splits, tiles_n, tiles, xcd_map, tail);
@@ -663,7 +672,7 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
         for (int p = 0; p < u->xv.world; p++)
             if (!u->xv.buf[p] || !u->xv.sig[p]) return -1;
     }
-    const int xcd_map = (splits % 8 == 0 && tiles > 1) ? 1 : 0;
+    const int xcd_map = (splits >= 8 && tiles > 1) ? 1 : 0;
     hpnn_g0_update uu = *u;
 #ifdef HPNN_ABLATIONS
     static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();

@@ -16,8 +16,9 @@ def _bf(*shape, scale=1.0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Bt,N,M,S", [(65536, 128, 800, 48), (4096, 128, 800, 5), (2048, 64, 64, 7),
-                                      (1024, 32, 96, 3), (8192, 128, 832, 16)])
+@pytest.mark.parametrize("Bt,N,M,S", [(65536, 128, 800, 48), (65536, 128, 800, 51), (4096, 128, 800, 5),
+                                      (2048, 64, 64, 7), (1024, 32, 96, 3), (8192, 128, 832, 16),
+                                      (8192, 128, 832, 12)])
 def test_gemm_fm_direct_matches_fp32(gpu, Bt, N, M, S):
     torch.manual_seed(Bt + N + M)
     D, H = _bf(Bt, N, scale=0.25), _bf(Bt, M)
@@ -27,12 +28,13 @@ def test_gemm_fm_direct_matches_fp32(gpu, Bt, N, M, S):
     got = slab.sum(0)
     err = (got - ref).abs().max().item()
     assert err < 1e-5 * Bt ** 0.5 * 4 + 1e-4, err
-    # per-split slabs: split s covers batch rows [s*U/S, (s+1)*U/S) of 32-row units
+    # per-split slabs: split s covers batch rows [s*U/S, (s+1)*U/S) of 32-row units (every
+    # split: the XCD-aware block order maps 8 * (S // 8) of them by XCD, the rest in order)
     U = Bt // 32
-    s = S - 1
-    a, b = 32 * (s * U // S), 32 * ((s + 1) * U // S)
-    ref_s = D[a:b].float().t() @ H[a:b].float()
-    assert (slab[s] - ref_s).abs().max().item() < 1e-3
+    for s in range(S):
+        a, b = 32 * (s * U // S), 32 * ((s + 1) * U // S)
+        ref_s = D[a:b].float().t() @ H[a:b].float()
+        assert (slab[s] - ref_s).abs().max().item() < 1e-3, s
 
 
 @pytest.mark.gpu
