@@ -67,7 +67,9 @@ def run_train_nn(name, batches, epochs, work, dtype="bf16", dpforce=False):
 
 
 def run_bench(name, steps, dpforce=False):
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", name, "--steps", str(steps), "--warmup", "10"]
+    # no settle phase: train_nn's timed epochs start from an idle GPU too (the same clock ramp)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", name, "--steps", str(steps), "--warmup", "10",
+           "--settle-ms", "0"]
     env = dict(os.environ)
     if dpforce:
         env["HPNN_DP_FORCE"] = "1"
