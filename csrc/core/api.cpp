@@ -230,7 +230,8 @@ extern "C" nn_def *_NN(load, conf)(const CHAR *filename) {
             for (auto &ch : u) ch = (char)tolower(ch);
             if (u == "bf16") conf->dtype = NN_DTYPE_BF16;
             else if (u == "f32" || u == "fp32" || u == "float") conf->dtype = NN_DTYPE_F32;
-            else conf->dtype = NN_DTYPE_F64;
+            else if (u == "f64" || u == "fp64" || u == "double") conf->dtype = NN_DTYPE_F64;
+            else CONF_FAIL("[dtype] unknown: %s (f64 | f32 | bf16)\n", v.c_str()); /* docs/PARITY.md */
         } else if (is("device")) {
             std::string u = v;
             for (auto &ch : u) ch = (char)tolower(ch);

@@ -19,6 +19,7 @@ per-layer step in the PyTorch emulation of the kernels (hpnn_amd.ops), whatever 
 """
 import ctypes
 import ctypes.util
+import hashlib
 import math
 import os
 
@@ -394,13 +395,15 @@ class MLP:
         parallel replicas hold bitwise-identical weights, so equal digests (synchronises)."""
         if self._gpu:
             return int(self.plan.weights_digest(int(which), _stream()))
-        h = 0
+        # a keyless, process-independent hash (Python's hash() of bytes is salted per process,
+        # so replicas in different processes would never agree)
+        h = hashlib.blake2b(digest_size=8)
         for l in range(self.L):
             ts = ([self.Wb[l], self.Wt[l]] if which & 1 else []) + ([self.W32[l]] if which & 2 else [])
             for t in ts:
-                h = (h * 1000003 + hash(t.contiguous().view(-1).view(torch.int16 if t.element_size() == 2
-                                                                    else torch.int32).cpu().numpy().tobytes())) % (1 << 64)
-        return h
+                h.update(t.contiguous().view(-1).view(torch.int16 if t.element_size() == 2
+                                                      else torch.int32).cpu().numpy().tobytes())
+        return int.from_bytes(h.digest(), "little")
 
     def reset_stats(self):
         self.stats.zero_()

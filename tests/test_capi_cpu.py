@@ -135,6 +135,24 @@ def test_run_nn_and_conf_errors(tmp_path):
     assert r.returncode != 0 and "hidden" in (r.stdout + r.stderr)
 
 
+@pytest.mark.parametrize("dtype,ok", [("bf61", False), ("f16", False), ("bf16", True), ("F32", True),
+                                      ("fp64", True)])
+def test_conf_dtype_strict(tmp_path, dtype, ok):
+    """an unknown [dtype] fails nn_load_conf (docs/PARITY.md) instead of training in FP64"""
+    os.environ["HPNN_FORCE_CPU"] = "1"
+    from hpnn_amd import capi
+    capi.init(0)
+    conf = os.path.join(str(tmp_path), "nn.conf")
+    with open(conf, "w") as f:
+        f.write(f"[type] SNN\n[init] generate\n[seed] 3\n[input] 4\n[hidden] 5\n[output] 3\n[train] BP\n"
+                f"[mode] batched\n[dtype] {dtype}\n")
+    if ok:
+        capi.Network(conf).close()
+    else:
+        with pytest.raises(Exception):
+            capi.Network(conf)
+
+
 def test_dry_run_writes_nothing(tmp_path):
     d = str(tmp_path)
     _make_dataset(os.path.join(d, "samples"), 2, 4, 4, False)

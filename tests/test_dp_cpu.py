@@ -34,8 +34,10 @@ def _worker(rank, world, port, sizes, net, fused, B, steps, q):
     L = Lall[rank * B:(rank + 1) * B]
     for _ in range(steps):
         dp.train_step(X, labels=L, lr=0.05, alpha=0.2)
+    # the replica digest is process-independent: identical replicas agree across processes
+    ok = dp.weights_consistent()
     if rank == 0:
-        q.put([w.numpy() for w in m.host_weights()])  # by value: no shared-memory fd
+        q.put((ok, [w.numpy() for w in m.host_weights()]))  # by value: no shared-memory fd
     dist.barrier()
     dist.destroy_process_group()
 
@@ -50,7 +52,8 @@ def test_dp_equals_single(sizes, net, fused):
     procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, net, fused, B, steps, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    ok, got = q.get(timeout=300)
+    assert ok, "weights_consistent() disagrees for identical CPU replicas"
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
