@@ -71,9 +71,12 @@ def main():
                     help="data-parallel gradient exchange: FP32 all-reduce, or BF16 reduce-scatter + sharded "
                          "optimizer step + BF16 weight all-gather (half the bytes; per-layer models only)")
     ap.add_argument("--settle-ms", type=float, default=50.0,
-                    help="untimed steps for about this long before the warmup, so the timed steps see the GPU at "
+                    help="untimed steps for about this long after the warmup, so the timed steps see the GPU at "
                          "its steady clock (the first ~20 ms of steps after idle run 10-20%% slower; "
                          "profiles/r5/SUMMARY.md); 0: off")
+    ap.add_argument("--settle-first", action="store_true",
+                    help="settle before the W warmup steps (default: after them, so the graph the timed "
+                         "steps replay is the one that ran last)")
     ap.add_argument("--replay-trace", default="",
                     help="diagnostics: write the GPU time of every timed graph replay (ms) to this JSON file")
     args = ap.parse_args()
@@ -148,6 +151,24 @@ def main():
             graphs[n] = g
         return graphs[n]
 
+    def leave_xgmi(why):
+        """every rank stops using the xGMI exchange (collective: all ranks call it): RCCL takes
+        the gradients, or torch.distributed when there is no RCCL communicator (rehearsal);
+        the replicas restart from rank 0's weights (reference: the P2P -> CMM -> EXP fallback
+        of libhpnn.c:245-302, decided once and agreed by every rank)"""
+        nonlocal use_graph
+        if rank == 0:
+            print(f"{why}; falling back to {'RCCL' if dp.native.h else 'torch.distributed'}", file=sys.stderr)
+        dp.native.detach_xar()
+        if not dp.native.h:  # xGMI-only (rehearsal): torch.distributed takes the gradients
+            # keep the detached communicator (and its IPC-mapped buffers) alive until every rank
+            # is past the final barrier: a peer may still be inside a timed-out all-reduce
+            # reading them
+            dp._detached_native = dp.native
+            dp.native = None
+            use_graph = bool(args.graph) and args.graph == 2
+        dp.broadcast_parameters()
+
     # one eager step first: when the xGMI all-reduce is in use, every rank checks that its
     # barriers completed and all ranks agree, else all fall back to RCCL before anything
     # is captured or timed
@@ -155,24 +176,21 @@ def main():
     torch.cuda.synchronize()
     if dp.native is not None and dp.native.xar:
         if not dp.all_ok(dp.native.xar_healthy()):
-            if rank == 0:
-                print("xGMI all-reduce barrier timed out on some rank; using RCCL", file=sys.stderr)
-            dp.native.detach_xar()
-            if not dp.native.h:  # xGMI-only (rehearsal): torch.distributed takes the gradients
-                # keep the detached communicator (and its IPC-mapped buffers) alive until
-                # every rank is past the final barrier: a peer may still be inside a
-                # timed-out all-reduce reading them
-                dp._detached_native = dp.native
-                dp.native = None
-                use_graph = bool(args.graph) and args.graph == 2
-            dp.broadcast_parameters()
+            leave_xgmi("xGMI all-reduce barrier timed out on some rank")
 
     # the replicas must hold bitwise-identical weights after the first exchange (a sum that
-    # arrived in time but is wrong shows here, before anything is timed)
+    # arrived in time but is wrong shows here, before anything is timed).  Over xGMI: degrade
+    # to the next exchange, re-broadcast, one more step, check again; no result only if the
+    # fallback disagrees too
     if dp.active and not dp.weights_consistent():
-        if rank == 0:
-            print("replica weights differ after the first step; no result reported", file=sys.stderr)
-        sys.exit(3)
+        if dp.native is not None and dp.native.xar:
+            leave_xgmi("replica weights differ after the first step over xGMI")
+            step(1)
+            torch.cuda.synchronize()
+        if not dp.weights_consistent():
+            if rank == 0:
+                print("replica weights differ after the first step; no result reported", file=sys.stderr)
+            sys.exit(3)
 
     if use_graph:
         s = torch.cuda.Stream()
@@ -213,9 +231,12 @@ def main():
             for i in range(first, first + n):
                 step(i)
 
-    # settle: whole steps for ~settle_ms (the same count on every rank: the steps hold
-    # collectives), then the W warmup steps, then the K timed steps
+    # the W warmup steps, then settle: whole steps for ~settle_ms (the same count on every rank:
+    # the steps hold collectives), then the K timed steps.  (--settle-first: settle before the
+    # warmup, the round-5 order)
     settle = 0
+    if not args.settle_first:
+        run_steps(0, args.warmup)
     if args.settle_ms > 0:
         t_a = time.perf_counter()
         run_steps(0, gsteps)
@@ -227,7 +248,8 @@ def main():
         settle = gsteps * max(0, math.ceil(args.settle_ms * 1e-3 / max(float(est.item()), 1e-6) / gsteps) - 1)
         run_steps(gsteps, settle)
         settle += gsteps
-    run_steps(0, args.warmup)
+    if args.settle_first:
+        run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if world > 1 and rank == world - 1 and native().fault_hit("weights"):
         # test hook (HPNN_FAULT=weights:1): one replica's weights drift from the others'

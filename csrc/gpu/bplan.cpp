@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 namespace hpnn {
 
 namespace {
@@ -121,6 +123,17 @@ int BPlan::configure(const int *sizes, int n_layers, int net_type, int batch_siz
     mode = m;
     if (mode == 't') Bp = pad_to(Bp, TILE_T); /* whole tiles; padded rows are zero and masked by n_valid */
     for (int l = 0; l < L; l++) S[l] = (splits && splits[l] > 0) ? splits[l] : pick_splits(Np[l], Kp[l], Bp);
+    /* modes t / x: the first-layer gradient runs on the fused G0 launch's own tiles (160 or 80
+     * feature columns x 128): about one workgroup per CU of THOSE tiles */
+    if ((mode == 't' || mode == 'x') && !(splits && splits[0] > 0) && !getenv("HPNN_TN_SPLITS")) {
+        const int tiles = hpnn_g0_tiles(1, Np[0], Kp[0]);
+        if (tiles > 0) {
+            int s0 = (256 + tiles / 2) / tiles;
+            if (s0 > Bp / 512) s0 = Bp / 512;
+            if (s0 >= 8) s0 -= s0 % 8;
+            S[0] = s0 < 1 ? 1 : s0;
+        }
+    }
     slab_f = hpnn_mlp3_slab_floats();
     if (mode == 't') mid_grid = device ? hpnn_mlp3_tile_grid(Bp, 0) : 1;
     else if (mode == 'x') mid_grid = device ? hpnn_mlp3_fused_grid(Bp, 0) : 1;
@@ -166,7 +179,7 @@ int BPlan::configure(const int *sizes, int n_layers, int net_type, int batch_siz
     }
     if (mode == 't' || mode == 'x') {
         add("W0f", -1, BD_BF16, {(long)Np[0] * Kp[0]}, true);
-        add("g0cnt", -1, BD_I32, {256}, true); /* fused G0 step: tile counters + error word */
+        add("g0cnt", -1, BD_I32, {HPNN_G0CNT_WORDS}, true); /* fused G0 step: tile counters + error word */
     }
     if (mode == 'w') {
         const long pb = wide_ksplit == 2 ? hpnn_wide2_pbuf_bytes(Bp) : 16;
@@ -381,8 +394,11 @@ int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipSt
         u.xv = *xv;
     }
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
-    u.cnt = g0cnt, u.err = g0cnt + 224;
+    u.cnt = g0cnt, u.err = g0cnt + HPNN_G0_ERR_WORD;
+    u.perm = g0_perm;
     u.fault = hpnn_fault_hit("handoff"); /* HPNN_FAULT=handoff:n: the n-th launch reports a timed-out wait */
+    /* HPNN_FAULT=xsum:n: the n-th exchanging launch of the last rank sums one element wrong */
+    u.xfault = xv && xv->world > 1 && xv->rank == xv->world - 1 && hpnn_fault_hit("xsum");
     u.lr = lr, u.alpha = alpha, u.scale = scale, u.momentum = momentum ? 1 : 0;
     u.mslab = midslab, u.mrows = mid_grid, u.mstride = slab_f, u.n12 = slab_f;
     for (int l = 0; l < 2; l++) {
@@ -531,12 +547,56 @@ int BPlan::xchg_step(const XIn &x, const int *labels, const float *T, int ldt, i
                      float scale, const hpnn_xar_view &xv, hipStream_t s) {
     if (mode != 't' && mode != 'x' && mode != 'm') return -1;
     if (!fm_input(x) || !g0cnt || !g0_fused || !hpnn_gemm_fm_direct_update_ok(Kp[0], Np[0], Kp[0], Bp, S[0]) ||
-        S[0] * ((Kp[0] / 160) * (Np[0] / 128)) > HPNN_XAR_MAX_BLOCKS || (long)goff[L] > xv.half)
+        S[0] * hpnn_g0_tiles(x.u8, Np[0], Kp[0]) > HPNN_XAR_MAX_BLOCKS || (long)goff[L] > xv.half)
         return -1;
     int r;
     if ((r = front(x, labels, T, ldt, n_valid, s))) return r;
     r = g0_fused_step(x, lr, alpha, scale, s, nullptr, nullptr, 0, &xv);
     return r == -1 ? -9 : r; /* covered above: a refusal now is an error, not a fallback */
+}
+
+/* the in-kernel exchange on the real links before it carries a gradient: the fused G0 launch
+ * in self-test mode (no GEMM) exchanges a known rank-dependent pattern over this communicator
+ * and stores the rank-order sums in gflat; they must be exact.  Collective (every rank of the
+ * view launches it); returns the number of wrong floats, < 0 on a launch / copy error, 1 when
+ * the shape does not take the in-kernel exchange at all. */
+int BPlan::xchg_self_test(const hpnn_xar_view &xv, hipStream_t s) {
+    if (mode != 't' && mode != 'x' && mode != 'm') return -1;
+    if (!g0cnt || !g0_fused || !hpnn_gemm_fm_direct_update_ok(Kp[0], Np[0], Kp[0], Bp, S[0]) ||
+        S[0] * hpnn_g0_tiles(1, Np[0], Kp[0]) > HPNN_XAR_MAX_BLOCKS || (long)goff[L] > xv.half)
+        return -1;
+    hpnn_g0_update u;
+    memset(&u, 0, sizeof u);
+    u.xchg = 1;
+    u.xv = xv;
+    u.xtest = 1;
+    u.xres = gflat;
+    u.perm = g0_perm;
+    u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
+    u.cnt = g0cnt, u.err = g0cnt + HPNN_G0_ERR_WORD;
+    u.momentum = momentum ? 1 : 0;
+    u.mslab = midslab, u.mrows = mid_grid, u.mstride = slab_f, u.n12 = slab_f;
+    for (int l = 0; l < 2; l++) {
+        u.W32b[l] = W32[l + 1], u.V32b[l] = V32[l + 1], u.Wbb[l] = Wb[l + 1], u.Wtb[l] = Wt[l + 1];
+        u.Nb[l] = Np[l + 1], u.Kb[l] = Kp[l + 1];
+    }
+    /* one-shot and two-shot both (the step picks by world size; HPNN_XAR_G0_MODE can force) */
+    int bad = 0;
+    const long n = goff[L];
+    std::vector<float> h(n);
+    for (int xm = 1; xm <= 2; xm++) {
+        u.xchg = xm;
+        if (hipMemsetAsync(gflat, 0xff, n * 4, s) != hipSuccess) return -3;
+        const int r = hpnn_gemm_fm_direct_update(D[0], D[0], 1, 1.f, slab[0], Kp[0], Np[0], Kp[0], Bp, S[0], &u, s);
+        if (r) return r < 0 ? r : -r;
+        if (hipMemcpyAsync(h.data(), gflat, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -3;
+        const double tri = 0.5 * xv.world * (xv.world + 1);
+        for (long i = 0; i < n; i++)
+            if (h[i] != (float)(tri * ((i % 97) + 1) * 0.0625)) bad++;
+    }
+    return bad;
 }
 
 int BPlan::grads_slabs(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, SlabSegs *segs,
@@ -589,7 +649,7 @@ int BPlan::predict(const void *X, int n_valid, float *O, int ldo, hipStream_t s)
 }
 
 int BPlan::health_enqueue(hipStream_t s, unsigned int *dst) {
-    if (g0cnt && hipMemcpyAsync(&dst[0], g0cnt + 224, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
+    if (g0cnt && hipMemcpyAsync(&dst[0], g0cnt + HPNN_G0_ERR_WORD, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
     if (tncnt && hipMemcpyAsync(&dst[1], tncnt + 1024 * L, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -7;
     if (wwords && hipMemcpyAsync(&dst[2], wwords + 2 * (Bp / TILE_W), 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return -7;

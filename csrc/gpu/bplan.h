@@ -82,6 +82,7 @@ class BPlan {
     char mode = 0;
     int mid_grid = 0, mid_groups = 1, wide_ksplit = 1, slab_f = 0;
     bool g0_fused = true; /* modes t / x: G0 + reduction + every step in one launch when it applies */
+    int g0_perm = 0;      /* tests: > 0 runs the fused G0 grid in a permuted block -> role order */
     bool tn_update = true; /* the step in the 8-phase TN gradient's epilogue where it applies */
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
@@ -142,6 +143,9 @@ class BPlan {
      * when the fused G0 does not cover the shape or the input. */
     int xchg_step(const XIn &x, const int *labels, const float *T, int ldt, int n_valid, float lr, float alpha,
                   float scale, const hpnn_xar_view &xv, hipStream_t s);
+    /* collective self-test of that in-kernel exchange on xv (known pattern, exact sums checked
+     * on the host): 0 when every float arrived right, > 0 wrong floats, -1 not covered */
+    int xchg_self_test(const hpnn_xar_view &xv, hipStream_t s);
     int update_flat(const float *G, float lr, float alpha, float scale, hipStream_t s);
     /* layer l's weight gradient and step run as ONE 8-phase TN launch */
     bool tn_update_ok(int l) const;

@@ -850,6 +850,32 @@ struct Batched {
         return TRUE;
     }
 
+    /* the replica state (FP32 masters + momentum, padded) as bytes, and back (then the BF16
+     * copies are re-derived): rank 0's state re-broadcast after an exchange fallback */
+    BOOL get_state(std::vector<char> &out) {
+        out.clear();
+        HIPCHK(hipStreamSynchronize(s));
+        for (int l = 0; l < L; l++)
+            for (float *b : {p.W32[l], p.V32[l]}) {
+                if (!b) continue;
+                const size_t n = (size_t)p.Np[l] * p.Kp[l] * 4, o = out.size();
+                out.resize(o + n);
+                HIPCHK(hipMemcpy(out.data() + o, b, n, hipMemcpyDeviceToHost));
+            }
+        return TRUE;
+    }
+    BOOL set_state(const char *in) {
+        size_t o = 0;
+        for (int l = 0; l < L; l++)
+            for (float *b : {p.W32[l], p.V32[l]}) {
+                if (!b) continue;
+                const size_t n = (size_t)p.Np[l] * p.Kp[l] * 4;
+                HIPCHK(hipMemcpy(b, in + o, n, hipMemcpyHostToDevice));
+                o += n;
+            }
+        return p.cast_weights(s) == 0 && hipStreamSynchronize(s) == hipSuccess;
+    }
+
     /* exact resume: BPM momentum k->dw (host FP64) -> padded FP32 V32 */
     BOOL upload_momentum(const kernel_ann *k) {
         if (!k->dw) return TRUE;
@@ -1122,6 +1148,30 @@ struct BatchedFP {
             HIPCHK(hipMemcpy(tmp.data(), V[l], nw * sizeof(T), hipMemcpyDeviceToHost));
             for (size_t i = 0; i < nw; i++) k->dw[l][i] = (DOUBLE)tmp[i];
         }
+        return TRUE;
+    }
+
+    BOOL get_state(std::vector<char> &out) {
+        out.clear();
+        HIPCHK(hipStreamSynchronize(s));
+        for (int l = 0; l < L; l++)
+            for (T *b : {W[l], V[l]}) {
+                if (!b) continue;
+                const size_t n = (size_t)N[l] * M[l] * sizeof(T), o = out.size();
+                out.resize(o + n);
+                HIPCHK(hipMemcpy(out.data() + o, b, n, hipMemcpyDeviceToHost));
+            }
+        return TRUE;
+    }
+    BOOL set_state(const char *in) {
+        size_t o = 0;
+        for (int l = 0; l < L; l++)
+            for (T *b : {W[l], V[l]}) {
+                if (!b) continue;
+                const size_t n = (size_t)N[l] * M[l] * sizeof(T);
+                HIPCHK(hipMemcpy(b, in + o, n, hipMemcpyHostToDevice));
+                o += n;
+            }
         return TRUE;
     }
 
@@ -1654,18 +1704,21 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         const char *xg = getenv("HPNN_XAR_G0");
         if (use_xar && !(xg && xg[0] == '0') && open_xar(count * 4, &xark)) return FALSE;
     }
-    if (!use_xar) {
+    /* collective: the RCCL communicator (rank 0's unique id through the bootstrap) */
+    auto open_rccl = [&]() -> bool {
         unsigned char id[HPNN_COMM_ID_BYTES] = {0};
         std::vector<unsigned char> all((size_t)W * HPNN_COMM_ID_BYTES);
-        if (R == 0 && hpnn_comm_unique_id(id) != 0) return FALSE;
-        if (hpnn_boot_allgather(id, sizeof id, all.data()) != 0) return FALSE;
+        if (R == 0 && hpnn_comm_unique_id(id) != 0) return false;
+        if (hpnn_boot_allgather(id, sizeof id, all.data()) != 0) return false;
         comm = hpnn_comm_init_rank(all.data(), W, R, dev); /* rank 0's id */
-        if (!comm) return FALSE;
+        if (!comm) return false;
         /* BF16 batched engine: the library's overlapped data-parallel step (dp_exchange.h);
          * FP32 / FP64 engines: the bucket loop below */
         if (!net.attach_dpx(comm, bf16rs ? hpnn::DpExchange::BF16RS : hpnn::DpExchange::FP32) && bf16rs)
             NN_WARN(stderr, "bf16rs exchange unavailable for this net: FP32 all-reduce\n");
-    }
+        return true;
+    };
+    if (!use_xar && !open_rccl()) return FALSE;
     NN_OUT(stdout, "data-parallel batched training: %d processes (%s, %s), %d samples per rank per step\n", W,
            use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Net::name(), Bg);
     const int n_batches = (int)((n + B - 1) / B);
@@ -1790,6 +1843,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     hipGraphExec_t gx = nullptr;
     double setup_s = 0.0;
     bool local_ok = true;
+    bool recheck = false; /* digests compared again at the next agreement point (after a fallback) */
     UINT replays = 0;
     for (UINT e = 0; e < E && ok;) {
         if (e == 1 && graphs_enabled() && n_batches <= 4096 && E - 1 >= epg) {
@@ -1831,7 +1885,7 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         pend = lok ? slot : -1;
         local_ok = local_ok && lok;
         const bool first = e == 1, last = e == E;
-        if (!(first || last || metrics || replays % 16 == 0)) continue;
+        if (!(first || last || metrics || recheck || replays % 16 == 0)) continue;
         /* agreement point */
         if (pend >= 0) local_ok = finish_check(pend) && local_ok;
         pend = -1;
@@ -1841,9 +1895,11 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         /* replicas must hold bitwise-identical weights: a wrong-but-timely exchange (a sum that
          * arrived in time but is not every rank's) shows here, after the first epoch and the last */
         unsigned long long dig = 0;
-        const bool check_dig = first || last;
+        const bool check_dig = first || last || recheck;
         if (local_ok && check_dig && !net.digest(&dig)) local_ok = false;
         if (local_ok && check_dig && R == W - 1 && hpnn_fault_hit("digest")) dig ^= 1; /* test hook */
+        if (local_ok && check_dig && first && R == W - 1 && use_xar && hpnn_fault_hit("xdigest"))
+            dig ^= 1; /* test hook: the first xGMI epoch looks wrong on one rank -> fallback */
         struct {
             double loss;
             unsigned long long digest;
@@ -1863,6 +1919,31 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
         if (first && R == 0)
             NN_DBG(stdout, "data-parallel: epoch 1 (eager, with the weight digest) %.3f ms\n",
                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        if (ok && check_dig && !same && first && use_xar) {
+            /* a wrong-but-timely xGMI sum: degrade instead of stopping -- every rank leaves the
+             * xGMI exchange for RCCL, rank 0's weights and momentum are re-broadcast, and the
+             * digests are compared again after the next epoch (a mismatch there stops the run).
+             * Reference: the P2P -> CMM -> EXP fallback chain, libhpnn.c:245-302 */
+            if (R == 0)
+                NN_WARN(stderr, "data-parallel training: the replicas' weights differ after epoch 1 over the "
+                                "xGMI exchange; falling back to RCCL from rank 0's weights\n");
+            std::vector<char> mine_st, all_st;
+            ok = net.get_state(mine_st);
+            if (ok) {
+                all_st.resize(mine_st.size() * (size_t)W);
+                ok = hpnn_boot_allgather(mine_st.data(), mine_st.size(), all_st.data()) == 0 &&
+                     net.set_state(all_st.data()); /* rank 0's block */
+            }
+            if (xark) hpnn_xar_destroy(xark);
+            if (xar) hpnn_xar_destroy(xar);
+            xark = xar = nullptr;
+            use_xar = false;
+            if (ok && !open_rccl()) ok = FALSE;
+            recheck = true;
+            same = true;
+        } else if (ok && check_dig && recheck) {
+            recheck = false;
+        }
         if (ok && check_dig && !same) {
             if (R == 0)
                 NN_ERROR(stderr, "data-parallel training: the replicas' weights differ after epoch %u "

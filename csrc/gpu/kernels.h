@@ -103,7 +103,7 @@ int hpnn_gemm_fm_direct_reduce(const void *Dg, const void *Hg, int h_u8, float h
 typedef struct {
     float *W32, *V32; /* layer 0 [N][M] FP32 master / momentum (V32 NULL for BP) */
     void *Wb, *Wt, *Wf; /* BF16 W [N][M], W^T [M][N], fragment-major copy (may be NULL) */
-    unsigned int *cnt;  /* 256 words, zeroed once: 64-bit tile counters, 32 words apart (monotonic) */
+    unsigned int *cnt;  /* HPNN_G0CNT_WORDS words, zeroed once: 64-bit tile counters, 32 words apart (monotonic) */
     unsigned int *err;  /* set when a wait for the other splits timed out */
     float lr, alpha, scale;
     int momentum;
@@ -130,7 +130,14 @@ typedef struct {
     int proto; /* hand-off diagnostics (HPNN_G0_PROTO, make ABLATIONS=1 builds only): 1 producer agent
                 * release, 2 consumer agent acquire, 4 system-scope (sc0 sc1) partial loads, 8 system
                 * acquire after the exchange barrier, 16 no exchange barrier, 32 one exchange load
-                * block per element (not one for both), 64 no W / V prefetch */
+                * block per element (not one for both), 64 no W / V prefetch; timing ablations (wrong
+                * results): 256 no partial publish, 512 no [G1 | G2] share, 1024 no split-sum loads */
+    /* tests / diagnostics: perm > 0 runs the grid in another block -> role order (reversed,
+     * rotated by perm: results must not change); xtest: self-test of the in-kernel exchange
+     * (no GEMM: a known pattern is exchanged, the sums land in xres, [G0 | G1 | G2] flat);
+     * xfault: corrupt one element of this rank's exchanged sum (HPNN_FAULT=xsum:n) */
+    int perm, xtest, xfault;
+    float *xres;
     int fault; /* test hook (HPNN_FAULT=handoff:n): the split-K wait of that launch reports a
                 * timeout (sets *err) as a real one would */
 } hpnn_g0_update;
@@ -139,6 +146,16 @@ int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float h
 /* 1 when hpnn_gemm_fm_direct_update covers the shape (launch-free check), including the
  * residency its in-kernel hand-offs need: every workgroup of the grid co-resident */
 int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits);
+/* output tiles of the fused G0 launch for these operands (h_u8: 8-bit H), 0 if not covered;
+ * the launch's grid is tiles x splits */
+int hpnn_g0_tiles(int h_u8, int N, int M);
+/* feature columns of that launch's output tile (160, or 80 with HPNN_G0_TILE=80) */
+int hpnn_g0_tile_cols(int M);
+/* hpnn_g0_update.cnt: HPNN_G0CNT_WORDS words, 64-bit tile counters 32 words apart (tile < 
+ * HPNN_G0_MAX_TILES), the error word at HPNN_G0_ERR_WORD */
+#define HPNN_G0CNT_WORDS 1024
+#define HPNN_G0_MAX_TILES 31
+#define HPNN_G0_ERR_WORD 1000
 /* workgroups of `kernel` (threads per workgroup, dynamic LDS bytes) the device can hold at once:
  * the occupancy API's blocks per CU x CUs (cached per kernel).  Kernels whose workgroups wait
  * for each other inside one launch (split-K tickets, tile-pair hand-offs, the in-kernel DP

@@ -67,20 +67,15 @@ using hpnn::st_sc1;
 /* the workgroup's partial product over its split of the batch: on return the waves of group
  * kg == 0 hold the 32 WF x 32 WH tile (wave tile 16 WF x 16 WH) in acc; *tile_, *split_, m0 / n0
  * (this wave's tile origin) are set.  Every wave returns (the caller's barriers need them). */
-template <int WF, int WH, int PD, int KW, bool HU8>
-__device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nbd, const void *__restrict__ Hg, int nbh,
-                                           int ksteps, int splits, int tiles_n, int tiles, int xcd_map,
-                                           f32x4 (&acc)[WF][WH], int &tile, int &split, int &m0, int &n0) {
-    constexpr int R = PD + 1;
-    constexpr int TMF = 32 * WF, TNH = 32 * WH; /* workgroup tile: features x delta columns */
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
+/* workgroup role: (virtual) block b -> output tile and batch split.  xcd_map: the tiles of
+ * one batch slice share b % 8, i.e. one XCD under the observed round-robin placement, so the
+ * slice's Dt rows are fetched once into that L2 -- a speed assumption only: every result is
+ * the same whichever block takes which role (fixed-order sums; tests permute the order).
+ * 8 * (splits / 8) splits map that way; the rest (splits not a multiple of 8) take the last
+ * blocks in plain order */
+__device__ __forceinline__ void fm_role(int b, int splits, int tiles, int xcd_map, int &tile, int &split) {
     if (xcd_map) {
-        /* the tiles of one batch slice on one XCD (workgroup b runs on XCD b % 8): its Dt slice
-         * is fetched once into that L2.  8 * (splits / 8) splits map that way; the rest (splits
-         * not a multiple of 8) take the last workgroups in plain order */
-        const int b = blockIdx.x, main = (splits / 8) * 8 * tiles;
+        const int main = (splits / 8) * 8 * tiles;
         if (b < main) {
             const int xcd = b & 7, j = b >> 3;
             tile = j % tiles;
@@ -90,9 +85,22 @@ __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nb
             split = (splits / 8) * 8 + (b - main) / tiles;
         }
     } else {
-        tile = blockIdx.x % tiles;
-        split = blockIdx.x / tiles;
+        tile = b % tiles;
+        split = b / tiles;
     }
+}
+
+template <int WF, int WH, int PD, int KW, bool HU8, int WM = 2, int WN = 2>
+__device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nbd, const void *__restrict__ Hg, int nbh,
+                                           int ksteps, int splits, int tiles_n, int tiles, int xcd_map, int vb,
+                                           f32x4 (&acc)[WF][WH], int &tile, int &split, int &m0, int &n0) {
+    constexpr int R = PD + 1;
+    constexpr int GW = WM * WN;                   /* waves per k-group */
+    constexpr int TMF = 16 * WF * WM, TNH = 16 * WH * WN; /* workgroup tile: features x delta columns */
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kg = wave / GW, wm = (wave % GW) / WN, wn = wave % WN;
+    fm_role(vb, splits, tiles, xcd_map, tile, split);
     m0 = (tile / tiles_n) * TMF + wm * 16 * WF;
     n0 = (tile % tiles_n) * TNH + wn * 16 * WH;
     const int k0 = (int)((long)split * ksteps / splits), k1 = (int)((long)(split + 1) * ksteps / splits);
@@ -154,29 +162,29 @@ __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nb
     }
 
     if constexpr (KW > 1) { /* groups 1.. hand their partial tiles to group 0 through LDS, in order */
-        __shared__ f32x4 part[4][WF * WH][64];
+        __shared__ f32x4 part[GW][WF * WH][64];
 #pragma unroll
         for (int g = 1; g < KW; g++) {
             if (kg == g) {
 #pragma unroll
                 for (int i = 0; i < WF; i++)
 #pragma unroll
-                    for (int j = 0; j < WH; j++) part[wave & 3][i * WH + j][lane] = acc[i][j];
+                    for (int j = 0; j < WH; j++) part[wave % GW][i * WH + j][lane] = acc[i][j];
             }
             __syncthreads();
             if (kg == 0) {
 #pragma unroll
                 for (int i = 0; i < WF; i++)
 #pragma unroll
-                    for (int j = 0; j < WH; j++) acc[i][j] += part[wave & 3][i * WH + j][lane];
+                    for (int j = 0; j < WH; j++) acc[i][j] += part[wave % GW][i * WH + j][lane];
             }
             if (g + 1 < KW) __syncthreads();
         }
     }
 }
 
-template <int WF, int WH, int PD, int KW, bool HU8 = false>
-__global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
+template <int WF, int WH, int PD, int KW, bool HU8 = false, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN * KW) void gemm_fm_direct_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                                   const void *__restrict__ Hg, int nbh, float hscale,
                                                                   float *__restrict__ slab, int ldg, int N, int ksteps,
                                                                   int splits, int tiles_n, int tiles, int xcd_map,
@@ -187,9 +195,9 @@ __global__ __launch_bounds__(256 * KW) void gemm_fm_direct_kernel(const __bf16 *
     }
     f32x4 acc[WF][WH];
     int tile, split, m0, n0;
-    fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
-                                    n0);
-    if ((threadIdx.x >> 6) >= 4) return;
+    fm_partial<WF, WH, PD, KW, HU8, WM, WN>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map,
+                                            (int)blockIdx.x, acc, tile, split, m0, n0);
+    if ((threadIdx.x >> 6) >= WM * WN) return;
     const int lane = threadIdx.x & 63, r16 = lane & 15, q = lane >> 4;
     float *out = slab + (size_t)split * N * ldg;
 #pragma unroll
@@ -351,9 +359,28 @@ __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
  * exchange and the update need no launch of their own. */
 template <int NT>
 __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsigned int e, int N, int ldg, int e0, int e1,
-                                              int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12) {
+                                              int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12, int b) {
     const hpnn_xar_view &v = u.xv;
-    const int t = threadIdx.x, b = blockIdx.x;
+    const int t = threadIdx.x;
+    /* the exchanged sums: stepped, or (self-test, u.xres) stored at their flat offsets; the
+     * fault hook (u.xfault, tests) corrupts the first G0 element of role 0 on this rank */
+    auto out0 = [&](int c, f32x4 g, bool use, Pre4 pre) {
+        const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
+        if (u.xfault && b == 0 && c == e0) g[0] += 1.0f;
+        if (u.xres) *(f32x4 *)(u.xres + (size_t)(nt0 + row) * ldg + col) = g;
+        else step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
+                        use, pre);
+    };
+    auto out12 = [&](long e4, f32x4 g, bool use, Pre4 pre) {
+        if (u.xres) {
+            *(f32x4 *)(u.xres + (size_t)N * ldg + e4 * 4) = g;
+            return;
+        }
+        int n, k;
+        const int l = g12_elem(u, e4, n, k);
+        step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,
+                   u, use, pre);
+    };
     const long hoff = (e & 1) ? v.half : 0;
     /* flag barrier `which` of workgroup b with every peer: this workgroup's stores to its buffer
      * acknowledged first (uncached memory: no writeback needed) */
@@ -379,7 +406,7 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     };
     auto g0_off = [&](int c) { return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4)); };
-    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = b * nf / nb, c1 = (b + 1) * nf / nb;
+    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = (long)b * nf / nb, c1 = (long)(b + 1) * nf / nb;
     const bool two = u.xchg == 2 && v.world > 1;
     barrier(0);
     if (two) {
@@ -431,17 +458,8 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
                     gb += x[4 + p];
                 }
         }
-        if (h0) {
-            const int c = e0 + t, row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
-            step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, ga, u,
-                       pf && t < 128, pg0);
-        }
-        if (h12) {
-            int n, k;
-            const int l = g12_elem(u, c0 + t, n, k);
-            step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k,
-                       gb, u, pf && t < 16, pg12);
-        }
+        if (h0) out0(e0 + t, ga, pf && t < 128, pg0);
+        if (h12) out12(c0 + t, gb, pf && t < 16, pg12);
         return;
     }
     /* one-shot: the rank-order sum over every peer; two-shot: the owner's sum */
@@ -452,19 +470,18 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(q) : "memory");
         return x;
     };
-    for (int c = e0 + t; c < e1; c += NT) {
-        const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
-        const f32x4 g = fetch(hoff + g0_off(c), c - e0);
-        step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
-                   pf && c == e0 + t && t < 128, pg0);
-    }
-    for (long e4 = c0 + t; e4 < c1; e4 += NT) {
-        const f32x4 g = fetch(hoff + (long)N * ldg + e4 * 4, e4 - c0);
-        int n, k;
-        const int l = g12_elem(u, e4, n, k);
-        step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,
-                   u, pf && e4 == c0 + t && t < 16, pg12);
-    }
+    for (int c = e0 + t; c < e1; c += NT) out0(c, fetch(hoff + g0_off(c), c - e0), pf && c == e0 + t && t < 128, pg0);
+    for (long e4 = c0 + t; e4 < c1; e4 += NT)
+        out12(e4, fetch(hoff + (long)N * ldg + e4 * 4, e4 - c0), pf && e4 == c0 + t && t < 16, pg12);
+}
+
+/* self-test pattern of the in-kernel exchange: rank r, flat gradient index i ->
+ * (r + 1) (i % 97 + 1) / 16 -- every partial sum over <= 8 ranks exact in FP32 */
+__device__ __forceinline__ f32x4 xtest_pattern(int rank, long i) {
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = (float)((rank + 1) * ((i + r) % 97 + 1)) * 0.0625f;
+    return v;
 }
 
 /* HPNN_G0_TRACE=1 (profiling only): s_memtime stamps of every workgroup's thread 0 at the
@@ -472,13 +489,14 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
 constexpr int G0TR_BLOCKS = 512, G0TR_MARKS = 8;
 __device__ unsigned long long g_g0_trace[G0TR_BLOCKS][G0TR_MARKS];
 
-template <int WF, int WH, int PD, int KW, bool HU8, bool TRACE = false>
-__global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
+template <int WF, int WH, int PD, int KW, bool HU8, bool TRACE = false, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                             const void *__restrict__ Hg, int nbh, float hscale,
                                                             float *__restrict__ slab, int ldg, int N, int ksteps,
                                                             int splits, int tiles_n, int tiles, int xcd_map,
                                                             hpnn_g0_update u) {
-    constexpr int NT = 256 * KW, TMF = 32 * WF, TNH = 32 * WH, NE4 = TMF * TNH / 4, PARTS = NT / 128;
+    constexpr int GW = WM * WN, NT = 64 * GW * KW, TMF = 16 * WF * WM, TNH = 16 * WH * WN, NE4 = TMF * TNH / 4,
+                  PARTS = NT / 128;
     auto mark = [&](int i) {
         if constexpr (TRACE) {
             const unsigned long long tt = __builtin_amdgcn_s_memtime();
@@ -489,8 +507,15 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     __shared__ f32x4 red[NT];
     f32x4 acc[WF][WH];
     int tile, split, m0, n0;
-    fm_partial<WF, WH, PD, KW, HU8>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, acc, tile, split, m0,
-                                    n0);
+    const long nb = (long)tiles * splits, nf = u.n12 / 4;
+    /* the workgroup's role: virtual block vb (u.perm > 0, tests: reversed and rotated order --
+     * every result must stay bitwise the same) */
+    const int vb = u.perm > 0 ? (int)((nb - 1 - (long)blockIdx.x + u.perm) % nb) : (int)blockIdx.x;
+    if (u.xtest) /* self-test of the in-kernel exchange: no GEMM (the role only) */
+        fm_role(vb, splits, tiles, xcd_map, tile, split);
+    else
+        fm_partial<WF, WH, PD, KW, HU8, WM, WN>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, vb, acc,
+                                                tile, split, m0, n0);
     mark(1);
     const int t = threadIdx.x, lane = t & 63;
     /* where the reduced gradient goes instead of a step: the plan's buffer, the xGMI
@@ -500,8 +525,8 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     float *gout = u.gout && u.gsel && !(*u.gsel & 1) ? u.gout + u.galt : u.gout;
     if (u.xchg) {
         if (t == 0) {
-            const unsigned int e = u.xv.ep[blockIdx.x] + 1; /* only this workgroup touches it */
-            u.xv.ep[blockIdx.x] = e;
+            const unsigned int e = u.xv.ep[vb] + 1; /* only this workgroup touches it */
+            u.xv.ep[vb] = e;
             xe_s = e;
         }
         __syncthreads();
@@ -512,8 +537,23 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
      * bit 64 turns the prefetch off) */
     const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
     const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
-    const long nb = (long)tiles * splits, nf = u.n12 / 4;
-    const long c0 = blockIdx.x * nf / nb, c1 = (blockIdx.x + 1) * nf / nb;
+    const long c0 = vb * nf / nb, c1 = (vb + 1) * nf / nb;
+    if (u.xtest) {
+        /* the known pattern in place of this workgroup's reduced G0 / [G1 | G2] shares, then the
+         * exchange with its sums stored (u.xres) for the host to check */
+        if (u.xchg) {
+            for (int c = e0 + t; c < e1; c += NT) {
+                const long i = (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4));
+                *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
+            }
+            for (long e4 = c0 + t; e4 < c1; e4 += NT) {
+                const long i = (long)N * ldg + e4 * 4;
+                *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
+            }
+            g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, false, Pre4{}, Pre4{}, vb);
+        }
+        return;
+    }
     const bool steps = !u.gout || u.xchg, pf = steps && !G0_PROTO(u, 64);
     Pre4 pg0 = {}, pg12 = {};
     if (pf && t < 128 && e0 + t < e1) {
@@ -526,14 +566,19 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         pg12 = pre_load(u.W32b[l], u.V32b[l], (size_t)n * u.Kb[l] + k, u.momentum);
     }
     /* publish this split's partial tile (write-through), then one ticket for the workgroup */
-    if ((t >> 6) < 4) {
+    if ((t >> 6) < GW) {
         const int r16 = lane & 15, q = lane >> 4;
         float *out = slab + (size_t)split * N * ldg;
+        if (G0_PROTO(u, 256)) {
+            /* timing ablation: no publish at all (wrong results) */
+        } else {
 #pragma unroll
-        for (int i = 0; i < WF; i++)
+            for (int i = 0; i < WF; i++)
 #pragma unroll
-            for (int j = 0; j < WH; j++)
-                st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q, HU8 ? acc[i][j] * hscale : acc[i][j]);
+                for (int j = 0; j < WH; j++)
+                    st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q,
+                           HU8 ? acc[i][j] * hscale : acc[i][j]);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -547,7 +592,8 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
     }
     mark(2);
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
-    g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
+    if (!G0_PROTO(u, 512)) /* 512: timing ablation, no [G1 | G2] share */
+        g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
     mark(3);
     if (t == 0) {
         /* fault hook: this launch reports a timed-out wait (and, like one, reduces what is there) */
@@ -569,7 +615,7 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         const int e = cc + f;
         const int row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-        if (e < e1) {
+        if (e < e1 && !G0_PROTO(u, 1024)) { /* 1024: timing ablation, no split loads */
             const float *p = slab + (size_t)(nt0 + row) * ldg + col;
             if (G0_PROTO(u, 4))
                 for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8<true>(p + (size_t)s * ss, ss, s1 - s);
@@ -591,19 +637,25 @@ __global__ __launch_bounds__(256 * KW) void g0_fused_kernel(const __bf16 *__rest
         __syncthreads();
     }
     mark(5);
-    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12);
+    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12, vb);
 }
 
-template <int WF, int WH, int PD, int KW, bool HU8 = false>
+template <int WF, int WH, int PD, int KW, bool HU8 = false, int WM = 2, int WN = 2>
 int launch_fm(const void *Dg, const void *Hg, float hscale, float *slab, int ldg, int N, int M, int Bt, int splits,
               hipStream_t s, const TnTail &tail) {
-    constexpr int TMF = 32 * WF, TNH = 32 * WH;
+    constexpr int TMF = 16 * WF * WM, TNH = 16 * WH * WN;
     const int tiles_n = N / TNH, tiles = (M / TMF) * tiles_n;
     const int xcd_map = (splits >= 8 && tiles > 1) ? 1 : 0;
-    hipLaunchKernelGGL((gemm_fm_direct_kernel<WF, WH, PD, KW, HU8>), dim3(tiles * splits + tail.blocks),
-                       dim3(256 * KW), 0, s, (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32,
-                       splits, tiles_n, tiles, xcd_map, tail);
+    hipLaunchKernelGGL((gemm_fm_direct_kernel<WF, WH, PD, KW, HU8, WM, WN>), dim3(tiles * splits + tail.blocks),
+                       dim3(64 * WM * WN * KW), 0, s, (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N,
+                       Bt / 32, splits, tiles_n, tiles, xcd_map, tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* feature columns per workgroup tile of the 8-bit-input G0 (HPNN_G0_TILE=80 | 160) */
+int g0_tile_m(int M) {
+    static const int want = [] { const char *e = getenv("HPNN_G0_TILE"); return e ? atoi(e) : 80; }();
+    return (want == 80 && M % 80 == 0) ? 80 : 160;
 }
 
 int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N, int M, int Bt,
@@ -616,6 +668,10 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
 #define HPNN_FM(...)                                                                                              \
     return h_u8 ? launch_fm<__VA_ARGS__, true>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)                  \
                 : launch_fm<__VA_ARGS__, false>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)
+    if (N % 128 == 0 && g0_tile_m(M) == 80) { /* 80 x 128: four k-interleaved groups of 1 x 2 waves */
+        return h_u8 ? launch_fm<5, 4, 1, 4, true, 1, 2>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t)
+                    : launch_fm<5, 4, 1, 4, false, 1, 2>(Dg, Hg, hscale, slab, ldg, N, M, Bt, splits, s, t);
+    }
     if (M % 160 == 0 && N % 128 == 0) {
         /* 8-bit H: 8 waves (two k-interleaved groups) hide the byte -> bf16 conversion
          * (23.0 / 26.5 us hot / cold vs 27.0 / 27.2 with 4 waves); bf16 H: 4 waves.
@@ -634,12 +690,17 @@ int fm_dispatch(const void *Dg, const void *Hg, int h_u8, float hscale, float *s
 }  // namespace
 
 /* the fused G0 grid (tiles x splits workgroups of 512 threads) fits on the device at once;
- * both instantiations checked (they differ only in the operand conversion) */
+ * every instantiation checked (they differ in the operand conversion and the tile) */
 static bool g0_fused_resident(int blocks) {
     static const int cap = [] {
-        const int a = hpnn_resident_capacity((const void *)g0_fused_kernel<5, 4, 1, 2, true>, 512, 0);
-        const int b = hpnn_resident_capacity((const void *)g0_fused_kernel<5, 4, 1, 2, false>, 512, 0);
-        return a < b ? a : b;
+        int c = hpnn_resident_capacity((const void *)g0_fused_kernel<5, 4, 1, 2, true>, 512, 0);
+        for (const void *k : {(const void *)g0_fused_kernel<5, 4, 1, 2, false>,
+                              (const void *)g0_fused_kernel<5, 4, 1, 4, true, false, 1, 2>,
+                              (const void *)g0_fused_kernel<5, 4, 1, 4, false, false, 1, 2>}) {
+            const int a = hpnn_resident_capacity(k, 512, 0);
+            c = a < c ? a : c;
+        }
+        return c;
     }();
     return blocks <= cap;
 }
@@ -649,17 +710,31 @@ static bool g0_fused_on() {
     return on;
 }
 
+/* the fused launch's tile (TMF feature columns x 128) for these operands */
+static int g0_fused_tm(int h_u8, int M) {
+    (void)h_u8;
+    return g0_tile_m(M);
+}
+
+extern "C" int hpnn_g0_tile_cols(int M) { return g0_tile_m(M); }
+
+extern "C" int hpnn_g0_tiles(int h_u8, int N, int M) {
+    const int tm = g0_fused_tm(h_u8, M);
+    return (M % tm || N % 128) ? 0 : (M / tm) * (N / 128);
+}
+
 extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab,
                                           int ldg, int N, int M, int Bt, int splits, const hpnn_g0_update *u,
                                           hipStream_t stream) {
-    /* the 160 x 128 tile configuration of fm_dispatch (8 waves) */
-    if (!g0_fused_on() || !u || M % 160 || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
+    /* the 8-wave tile configurations of fm_dispatch: 160 x 128, or 80 x 128 for 8-bit H */
+    const int tm = g0_fused_tm(h_u8, M);
+    if (!g0_fused_on() || !u || M % tm || N % 128 || Bt % 32 || splits < 1 || splits > Bt / 32 || ldg != M) return -1;
     if (!u->cnt || !u->err) return -1;
     const bool steps = !u->gout || u->xchg;
     if (u->n12 % 4 || !u->mslab || u->mrows < 1 || (steps && u->momentum && (!u->V32 || !u->V32b[0] || !u->V32b[1])))
         return -2;
-    const int tiles_n = N / 128, tiles = (M / 160) * tiles_n;
-    if (tiles > 7) return -1; /* 64-bit counters 32 words apart in a 256-word block, err at word 224 */
+    const int tiles_n = N / 128, tiles = (M / tm) * tiles_n;
+    if (tiles > HPNN_G0_MAX_TILES) return -1; /* 64-bit counters 32 words apart, below the error word */
     /* every workgroup waits for the other splits of its tile: all must be resident at once
      * (more splits than that, e.g. forced by HPNN_TN_SPLITS, take the slab form instead of
      * stalling to the timeout) */
@@ -679,22 +754,26 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     uu.proto |= proto;
 #endif
     static const bool trace = [] { const char *e = getenv("HPNN_G0_TRACE"); return e && e[0] == '1'; }();
-#define HPNN_G0F(U8_, TR_)                                                                                         \
-    hipLaunchKernelGGL((g0_fused_kernel<5, 4, 1, 2, U8_, TR_>), dim3(tiles * splits), dim3(512), 0, stream,         \
-                       (const __bf16 *)Dg, N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, \
-                       xcd_map, uu)
-    if (h_u8 && trace) HPNN_G0F(true, true);
-    else if (h_u8) HPNN_G0F(true, false);
-    else HPNN_G0F(false, false);
+#define HPNN_G0F(...)                                                                                              \
+    hipLaunchKernelGGL((g0_fused_kernel<__VA_ARGS__>), dim3(tiles * splits), dim3(512), 0, stream, (const __bf16 *)Dg, \
+                       N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, xcd_map, uu)
+    if (tm == 80) {
+        if (h_u8 && trace) HPNN_G0F(5, 4, 1, 4, true, true, 1, 2);
+        else if (h_u8) HPNN_G0F(5, 4, 1, 4, true, false, 1, 2);
+        else HPNN_G0F(5, 4, 1, 4, false, false, 1, 2);
+    } else if (h_u8 && trace) HPNN_G0F(5, 4, 1, 2, true, true);
+    else if (h_u8) HPNN_G0F(5, 4, 1, 2, true, false);
+    else HPNN_G0F(5, 4, 1, 2, false, false);
 #undef HPNN_G0F
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 extern "C" int hpnn_gemm_fm_direct_update_ok(int ldg, int N, int M, int Bt, int splits) {
-    if (!(g0_fused_on() && M % 160 == 0 && N % 128 == 0 && Bt % 32 == 0 && splits >= 1 && splits <= Bt / 32 &&
-          ldg == M && (M / 160) * (N / 128) <= 7))
+    const int tiles = hpnn_g0_tiles(1, N, M);
+    if (!(g0_fused_on() && tiles > 0 && Bt % 32 == 0 && splits >= 1 && splits <= Bt / 32 && ldg == M &&
+          tiles <= HPNN_G0_MAX_TILES))
         return 0;
-    return g0_fused_resident((M / 160) * (N / 128) * splits) ? 1 : 0;
+    return g0_fused_resident(tiles * splits) ? 1 : 0;
 }
 
 extern "C" int hpnn_gemm_fm_direct(const void *Dg, const void *Hg, int h_u8, float hscale, float *slab, int ldg, int N,

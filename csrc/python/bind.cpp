@@ -163,6 +163,12 @@ void bind_plan(py::module_ &m) {
                  if (r != -1) check(r, "BPlan.xchg_step");
                  return r == 0;
              })
+        .def("xchg_self_test",
+             [](BPlan &p, uptr xar, uptr s) {
+                 hpnn_xar_view v;
+                 check(hpnn_xar_view_get((hpnn_xar *)xar, &v), "xar_view_get");
+                 return p.xchg_self_test(v, S(s));
+             })
         .def("update_flat",
              [](BPlan &p, uptr G, float lr, float alpha, float scale, uptr s) {
                  check(p.update_flat((const float *)P(G), lr, alpha, scale, S(s)), "BPlan.update_flat");
@@ -175,6 +181,7 @@ void bind_plan(py::module_ &m) {
                  return d;
              })
         .def_readwrite("g0_fused", &BPlan::g0_fused)
+        .def_readwrite("g0_perm", &BPlan::g0_perm)
         .def_readwrite("tn_update", &BPlan::tn_update)
         .def("tn_update_ok", &BPlan::tn_update_ok)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {

@@ -83,6 +83,16 @@ class DataParallel:
         if (self.native is not None and self.native.xar and _XAR_G0 and getattr(model, "fused_mode", None) in ("x", "t")
                 and model.grad_flat.numel() * 4 <= self.native.xar_max):
             self.xar_k = self.native.attach_xar_kernel(model.grad_flat.numel() * 4)
+            if self.xar_k:
+                # the in-kernel exchange itself on the real links (a known pattern through the
+                # G0 launch's own barrier / peer-sum code, both one- and two-shot), agreed by
+                # every rank before a gradient goes through it; -1: the shape never takes it
+                rc = model.plan.xchg_self_test(self.xar_k, torch.cuda.current_stream().cuda_stream)
+                if rc not in (0, -1):
+                    print(f"rank {self.rank}: in-kernel xGMI exchange self-test failed ({rc}); "
+                          f"using the all-reduce launch", flush=True)
+                if not self.all_ok(rc in (0, -1)):
+                    self.xar_k = 0
         # HPNN_DPX_FORCE=1 (tests): the native exchange even on one rank (with HPNN_DPX_SHARD1=1
         # its BF16 reduce-scatter path too), so a one-GPU box runs its kernels
         dpx_one = os.environ.get("HPNN_DPX_FORCE", "0") == "1"

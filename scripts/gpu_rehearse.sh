@@ -17,6 +17,6 @@ for n in 2; do
 done
 # the driver's exact N > 1 MNIST path (exchange inside the G0 launch, HIP graphs) with 2 ranks:
 # per-rank batch 8192, so both ranks' G0 grids (80 workgroups each) and fronts fit at once
-HPNN_REHEARSE_FUSED=1 timeout -k 10 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 40 --warmup 5 --batch 8192 > gpurun_out/rehearse_fused.log 2>&1 || { tail -30 gpurun_out/rehearse_fused.log; exit 1; }
+HPNN_REHEARSE_FUSED=1 HPNN_SPLITS=8,0,0 timeout -k 10 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 40 --warmup 5 --batch 8192 > gpurun_out/rehearse_fused.log 2>&1 || { tail -30 gpurun_out/rehearse_fused.log; exit 1; }
 grep '"metric"' gpurun_out/rehearse_fused.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("fused", d["n_gpus"], d["config"]["parallelism"], d["config"]["grad_allreduce"], d["config"].get("grad_exchange"), d["config"]["hip_graph"], round(d["ms_per_step"]*1e3,1), "us/step (ranks sharing one GPU, batch 8192 per rank)")'
 grep -i "self-test\|timed out\|error" gpurun_out/rehearse_fused.log | head -5

@@ -206,3 +206,48 @@ def test_tn_update_fused_matches_separate(gpu, momentum):
             assert (a.V32[l] - b.V32[l]).abs().max().item() <= 1e-5 * max(1e-3, b.V32[l].abs().max().item())
         assert torch.equal(a.Wb[l], a.W32[l].bfloat16())
         assert torch.equal(a.Wt[l], a.W32[l].bfloat16().t().contiguous())
+
+
+@pytest.mark.parametrize("momentum", [True, False])
+def test_production_step_matches_oracle(gpu, momentum):
+    """The headline step itself (bench.py's config) against the FP64 oracle: MNIST
+    784-128-64-10 SNN, batch 65 536, 8-bit pixels, the tile front + the fused first-layer
+    gradient launch at its default split count (48: split-K reduction, optimizer steps and
+    the [G1 | G2] share in one launch).  Two steps; the oracle runs in FP64 on the GPU on the
+    same inputs (pixel / 255 rounded to BF16, as the front sees them) and the same initial
+    weights.  Same bounds as test_train_step_matches_oracle.  Reference step math:
+    snn.c:798-1074, batched."""
+    torch.manual_seed(0)
+    sizes, B, lr = [784, 128, 64, 10], 65536, 0.01
+    m = MLP(sizes, "SNN", batch=B, momentum=momentum, seed=10958)
+    assert m.fused_mode == "t"
+    import ctypes
+    from hpnn_amd._lib import lib_path
+    ok = ctypes.CDLL(lib_path()).hpnn_gemm_fm_direct_update_ok
+    assert m.plan.g0_fused and ok(m.Kp[0], m.Np[0], m.Kp[0], m.Bp, m.S[0]) == 1, "the fused G0 launch must run"
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    Xu8 = torch.randint(0, 256, (B, 784), device="cuda", generator=g, dtype=torch.uint8)
+    labels = torch.randint(0, 10, (B,), device="cuda", generator=g, dtype=torch.int32)
+    Xd = m.prepare_input(Xu8)
+    W64 = [w.cuda() for w in m.host_weights()]
+    V64 = [torch.zeros_like(w) for w in W64] if momentum else None
+    W0 = [w.clone() for w in W64]
+    Xb = (Xu8.double() / 255.0).float().bfloat16().double()
+    T = torch.zeros(B, 10, dtype=torch.float64, device="cuda")
+    T[torch.arange(B, device="cuda"), labels.long()] = 1.0
+    loss_total = 0.0
+    m.reset_stats()
+    for _ in range(2):
+        m.train_step(Xd, labels=labels, lr=lr, alpha=0.2)
+        loss_total += ref.batched_step(W64, Xb, T, "SNN", lr, V64, 0.2).item()
+    torch.cuda.synchronize()
+    assert m.healthy()
+    got = [w.cuda() for w in m.host_weights()]
+    for l in range(3):
+        dg, dr = got[l] - W0[l], W64[l] - W0[l]
+        rel = (dg - dr).norm() / (dr.norm() + 1e-30)
+        print(f"production step layer {l}: relative error of the weight change {rel.item():.2e}")
+        assert rel < 0.012, (l, rel.item())
+    lsum, _ = m.read_stats()
+    print(f"loss sum {lsum:.8g} vs oracle {loss_total * B:.8g}")
+    assert lsum == pytest.approx(loss_total * B, rel=6e-3)

@@ -39,7 +39,7 @@ def test_forced_g0_splits_beyond_residency_take_slab_path(gpu):
     X, lab = _batch(ref)
     ref.train_step(X, labels=lab)
     torch.cuda.synchronize()
-    # 64 splits x 5 tiles = 320 workgroups of the fused G0 > 256 resident (one per CU)
+    # 64 splits x 10 tiles = 640 workgroups of the fused G0 > 256 resident (one per CU)
     m = MLP(MNIST, "SNN", batch=65536, momentum=True, fused="t", splits=[64, 0, 0])
     assert m.S[0] == 64
     m.train_step(X, labels=lab)  # first launch (module load) outside the timing
@@ -60,7 +60,7 @@ def test_ticket_counters_past_2pow32(gpu):
     S = a.S[0]
     cnt = b.buf[("g0cnt", -1)].view(torch.int64)  # 64-bit tile counters, 32 words apart
     start = (2 ** 32 // S) * S  # the launches' tickets cross 2^32
-    for tile in range(5):
+    for tile in range(31):  # every tile counter the launch may use (HPNN_G0_MAX_TILES)
         cnt[16 * tile] = start
     X, lab = _batch(a)
     for _ in range(3):
@@ -155,3 +155,79 @@ def test_bench_exits_3_when_a_replica_drifts(gpu):
     assert '"metric"' not in r.stdout
     assert r.returncode != 0
     assert "exitcode: 3" in r.stderr or "exit code: 3" in r.stderr or "exitcode  : 3" in r.stderr, r.stderr[-3000:]
+
+
+def test_g0_role_order_permuted_bitwise(gpu):
+    """the fused G0 launch (split-K tickets, fixed-order split sums, [G1 | G2] share, steps)
+    gives bitwise the same weights whichever workgroup takes which (tile, split) role: the
+    grid run in reversed and rotated block orders.  The XCD-aware role order is a speed
+    assumption, never a correctness one."""
+    runs = {}
+    for perm in (0, 240, 1, 97):  # 240 workgroups: 240 = reversed, 1 / 97 = reversed + rotated
+        m = MLP(MNIST, "SNN", batch=65536, momentum=True, fused="t")
+        assert m.S[0] * 10 == 240 or m.S[0] * 5 == 240, m.S[0]
+        m.plan.g0_perm = perm
+        X, lab = _batch(m)
+        for _ in range(2):
+            m.train_step(X, labels=lab)
+        torch.cuda.synchronize()
+        assert m.healthy()
+        runs[perm] = [t.clone() for t in list(m.W32) + list(m.V32) + list(m.Wb)]
+        del m
+    for perm in (240, 1, 97):
+        for a, b in zip(runs[0], runs[perm]):
+            assert torch.equal(a, b), perm
+
+
+def test_bench_degrades_when_an_in_kernel_sum_is_wrong(gpu):
+    """a cross-rank sum that arrives in time but is wrong (HPNN_FAULT=xsum:1: rank 1's first
+    in-kernel exchange sums one element wrong) no longer kills the run: the replicas disagree
+    after the first step, every rank leaves the xGMI exchange for the next one (RCCL, here
+    torch.distributed: the ranks share one GPU), rank 0's weights are re-broadcast, the
+    replicas agree again and the bench reports a number (reference: the P2P -> CMM -> EXP
+    fallback chain, libhpnn.c:245-302)"""
+    env = _env(HPNN_BENCH_REHEARSE=1, HPNN_REHEARSE_FUSED=1, HPNN_SPLITS="8,0,0", HPNN_FAULT="xsum:1",
+               HPNN_XAR_TIMEOUT_MS=5000)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "4", "--warmup", "2", "--batch", "4096", "--graph-steps", "2", "--settle-ms", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "replica weights differ after the first step over xGMI; falling back" in r.stderr, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    import json
+    out = json.loads(line[0])
+    assert "xgmi" not in out["config"]["grad_allreduce"], out["config"]
+
+
+def test_train_nn_leaves_xgmi_when_replicas_disagree(gpu, tmp_path):
+    """train_dp_mp: a digest mismatch after the first (xGMI) epoch no longer stops the run at
+    once -- the ranks leave the xGMI exchange, re-broadcast rank 0's weights and open RCCL
+    (HPNN_FAULT=xdigest:1 makes the first digest look wrong on one rank).  Here both ranks
+    share one GPU, where RCCL refuses to start, so the run then stops; on one GPU per rank it
+    goes on over RCCL."""
+    _mnist_dir(tmp_path)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    flags = ["-v", "-b", "512", "-e", "2", "nn.conf"]
+    procs = [subprocess.Popen([TN] + flags, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=_env(RANK=r, WORLD_SIZE=2, LOCAL_RANK=0, LOCAL_WORLD_SIZE=2,
+                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                                       HPNN_BOOT_DIR=str(tmp_path / "boot"), HPNN_BOOT_TIMEOUT_S=60,
+                                       HPNN_XAR_TIMEOUT_MS=3000, HPNN_FAULT="xdigest:1"))
+             for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=200)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, o, e))
+    assert "falling back to RCCL from rank 0's weights" in outs[0][2], outs[0][2][-2000:]
