@@ -1347,20 +1347,45 @@ BOOL train_single(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const
     double ep_loss = 0.0;
     unsigned int ep_hits = 0;
     BOOL ok = TRUE;
+    /* hand-off health after every replay (<= ~32 steps): a 12-byte readback enqueued behind the
+     * replay and judged one replay later (the host has already queued the next replay, so the
+     * GPU never waits for the check), plus a final check after the last replay */
+    unsigned int *hw = nullptr;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    if (hipHostMalloc((void **)&hw, 8 * sizeof(unsigned int), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&hev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&hev[1], hipEventDisableTiming) != hipSuccess)
+        ok = FALSE;
+    int pend = -1, slot = 0;
+    auto judge = [&](int sl) -> bool { return hipEventSynchronize(hev[sl]) == hipSuccess && net.health_ok(hw + 4 * sl); };
     for (int e = 0; e < E && ok;) {
         const int ne = std::min(epg, E - e);
         auto g = graphs.find(ne);
         ok = (g != graphs.end() && g->second) ? hipGraphLaunch(g->second, s) == hipSuccess : epochs(ne);
         e += ne;
-        /* hand-off health after every replay (<= ~32 steps): one 12-byte readback */
-        if (ok) ok = net.healthy();
-        if (ok && (metrics || e == E)) ok = net.read_stats(&ep_loss, &ep_hits);
+        if (ok) {
+            unsigned int *d = hw + 4 * slot;
+            d[0] = d[1] = d[2] = 0;
+            ok = net.health_enqueue(d) && hipEventRecord(hev[slot], s) == hipSuccess;
+        }
+        if (ok && pend >= 0) ok = judge(pend);
+        pend = ok ? slot : -1;
+        slot ^= 1;
+        if (ok && (metrics || e == E)) {
+            ok = judge(pend); /* statistics read = a synchronisation anyway: judge this replay now */
+            pend = -1;
+            if (ok) ok = net.read_stats(&ep_loss, &ep_hits);
+        }
         if (ok && metrics)
             hpnn_metrics_epoch("gpu", o->epoch0 + e, ep_loss / (double)n, ep_hits, n,
                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
                                (UINT64)n * e);
     }
+    if (ok && pend >= 0) ok = judge(pend);
     auto t1 = std::chrono::steady_clock::now();
+    for (hipEvent_t ev : hev)
+        if (ev) hipEventDestroy(ev);
+    if (hw) hipHostFree(hw);
     for (auto &g : graphs)
         if (g.second) hipGraphExecDestroy(g.second);
     if (ok) ok = net.download(k);
@@ -1721,6 +1746,10 @@ BOOL train_dp_mp(kernel_ann *k, const DOUBLE *X, const DOUBLE *T, UINT n, const 
     if (!use_xar && !open_rccl()) return FALSE;
     NN_OUT(stdout, "data-parallel batched training: %d processes (%s, %s), %d samples per rank per step\n", W,
            use_xar ? "xGMI all-reduce" : "RCCL all-reduce", Net::name(), Bg);
+    /* the gradient exchange chosen (HPNN_GRAD_COMM; auto picks bf16rs for large per-layer nets) */
+    if (R == 0 && W > 1)
+        NN_OUT(stdout, "data-parallel gradient exchange: %s\n",
+               bf16rs ? "bf16rs (BF16 reduce-scatter, sharded FP32 step, BF16 all-gather)" : "fp32 (all-reduce)");
     const int n_batches = (int)((n + B - 1) / B);
     const int rows_p = n_batches * B + Bg + 128;
     XSet Xd;

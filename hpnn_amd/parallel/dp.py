@@ -14,6 +14,7 @@ bucket.  Small consecutive layers are merged into one bucket (`bucket_bytes`) be
 37 KB all-reduce is latency-bound on xGMI.
 """
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -65,6 +66,9 @@ class DataParallel:
             if getattr(model, "W0f", None) is not None or getattr(model, "fused_mode", None) is not None:
                 raise ValueError("grad_comm='bf16rs' needs the per-layer path (fused=False)")
             self.sharded = {l for l in range(model.L) if model.Np[l] % self.world == 0}
+        if self.active and self.world > 1 and self.rank == 0:
+            # the exchange "auto" chose (bf16rs changes the numerics of large nets)
+            print(f"data-parallel gradient exchange: {grad_comm}", file=sys.stderr, flush=True)
         self.buckets = self._plan(bucket_bytes)
         self.native = None
         self.dpx = None
