@@ -71,12 +71,12 @@ def main():
                     help="data-parallel gradient exchange: FP32 all-reduce, or BF16 reduce-scatter + sharded "
                          "optimizer step + BF16 weight all-gather (half the bytes; per-layer models only)")
     ap.add_argument("--settle-ms", type=float, default=50.0,
-                    help="untimed steps for about this long after the warmup, so the timed steps see the GPU at "
+                    help="untimed steps for about this long before the warmup, so the timed steps see the GPU at "
                          "its steady clock (the first ~20 ms of steps after idle run 10-20%% slower; "
                          "profiles/r5/SUMMARY.md); 0: off")
-    ap.add_argument("--settle-first", action="store_true",
-                    help="settle before the W warmup steps (default: after them, so the graph the timed "
-                         "steps replay is the one that ran last)")
+    ap.add_argument("--warmup-first", action="store_true",
+                    help="the W warmup steps before the settle phase instead of after it (A/B: no measurable "
+                         "difference, profiles/r6/SUMMARY.md)")
     ap.add_argument("--replay-trace", default="",
                     help="diagnostics: write the GPU time of every timed graph replay (ms) to this JSON file")
     args = ap.parse_args()
@@ -231,11 +231,10 @@ def main():
             for i in range(first, first + n):
                 step(i)
 
-    # the W warmup steps, then settle: whole steps for ~settle_ms (the same count on every rank:
-    # the steps hold collectives), then the K timed steps.  (--settle-first: settle before the
-    # warmup, the round-5 order)
+    # settle: whole steps for ~settle_ms (the same count on every rank: the steps hold
+    # collectives), then the W warmup steps, then the K timed steps
     settle = 0
-    if not args.settle_first:
+    if args.warmup_first:
         run_steps(0, args.warmup)
     if args.settle_ms > 0:
         t_a = time.perf_counter()
@@ -248,7 +247,7 @@ def main():
         settle = gsteps * max(0, math.ceil(args.settle_ms * 1e-3 / max(float(est.item()), 1e-6) / gsteps) - 1)
         run_steps(gsteps, settle)
         settle += gsteps
-    if args.settle_first:
+    if not args.warmup_first:
         run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if world > 1 and rank == world - 1 and native().fault_hit("weights"):

@@ -268,8 +268,9 @@ __device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, _
         const size_t fo = (((size_t)(n >> 4) * (K / 32) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
         *(bf16x4 *)(Wf + fo) = wb;
     }
+    if (!G0_PROTO(u, 2048)) /* 2048: timing ablation, no W^T stores */
 #pragma unroll
-    for (int r = 0; r < 4; r++) Wt[(size_t)(k + r) * N + n] = wb[r];
+        for (int r = 0; r < 4; r++) Wt[(size_t)(k + r) * N + n] = wb[r];
 }
 
 /* float4 e4 of [G1 | G2] -> layer l, row n, column k */
@@ -758,6 +759,12 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     hipLaunchKernelGGL((g0_fused_kernel<__VA_ARGS__>), dim3(tiles * splits), dim3(512), 0, stream, (const __bf16 *)Dg, \
                        N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, xcd_map, uu)
     if (tm == 80) {
+        /* HPNN_G0_PD=2 (ABLATIONS builds, tuning): two k-steps of operands in flight */
+#ifdef HPNN_ABLATIONS
+        static const int pd = [] { const char *e = getenv("HPNN_G0_PD"); return e ? atoi(e) : 1; }();
+        if (h_u8 && pd == 2) HPNN_G0F(5, 4, 2, 4, true, false, 1, 2);
+        else
+#endif
         if (h_u8 && trace) HPNN_G0F(5, 4, 1, 4, true, true, 1, 2);
         else if (h_u8) HPNN_G0F(5, 4, 1, 4, true, false, 1, 2);
         else HPNN_G0F(5, 4, 1, 4, false, false, 1, 2);
