@@ -43,7 +43,12 @@ $(BUILD)/%.o: %.cpp $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/%.o: %.hip $(HDRS)
+# device objects depend on the device flags: a change (e.g. make ABLATIONS=1, then plain make)
+# rewrites this stamp at parse time and rebuilds them, so an ablation build never stays behind
+HIPSTAMP  := $(BUILD)/.hipflags
+_stamp    := $(shell mkdir -p $(BUILD); echo '$(HIPFLAGS)' | cmp -s - $(HIPSTAMP) || echo '$(HIPFLAGS)' > $(HIPSTAMP))
+
+$(BUILD)/%.o: %.hip $(HDRS) $(HIPSTAMP)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
