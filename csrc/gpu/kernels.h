@@ -138,6 +138,7 @@ typedef struct {
      * xfault: corrupt one element of this rank's exchanged sum (HPNN_FAULT=xsum:n) */
     int perm, xtest, xfault;
     float *xres;
+    long n12t; /* set by the launcher: [G1 | G2] floats summed by the tail workgroups */
     int fault; /* test hook (HPNN_FAULT=handoff:n): the split-K wait of that launch reports a
                 * timeout (sets *err) as a real one would */
 } hpnn_g0_update;

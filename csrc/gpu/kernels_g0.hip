@@ -38,6 +38,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "kernels.h"
@@ -215,14 +216,19 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void gemm_fm_direct_kernel(const
  * until all `splits` partials of the tile have arrived, reduces its 1/splits share of the
  * tile over the splits in a FIXED order (sc1 loads; bitwise repeatable whatever the arrival
  * order) and applies the BP / BPM step to those elements: FP32 master, momentum, BF16 W,
- * W^T and the fragment-major copy the front reads.  Between its ticket and its wait every
- * workgroup also sums 1/grid of the front's [G1 | G2] block slabs completely (fixed order)
- * and steps layers 1 and 2 there (no tail workgroups: with 88 KB of LDS and 147 VGPRs they
- * could not share a CU with a GEMM workgroup).  Replaces the
- * separate sgd_update_multi launch (6.2 us) and its kernel boundary behind 20 MB of dirty
- * slabs.  All GEMM workgroups are co-resident (grid <= CUs; a wait that times out sets
- * *err instead of hanging).  Reference: the per-layer update of snn_kernel_train_momentum /
- * cuda_snn.cu:2726-3717 (GER into dW, W += dW, dW *= alpha), batched. */
+ * W^T and the fragment-major copy the front reads.  The front's [G1 | G2] block slabs are
+ * summed completely (fixed order) and layers 1 and 2 stepped by TAIL workgroups appended to
+ * the grid, on the CUs the GEMM grid leaves idle (MNIST: 240 GEMM workgroups + 16 tails on 256
+ * CUs): the 9 MB of slab reads run beside the GEMM instead of after every workgroup's publish
+ * (-2.7 us per step on a slow box, profiles/r6); HPNN_G0_TAIL12 < 100 leaves part of the
+ * columns to the GEMM workgroups, between their ticket and their wait.  Tails wait for
+ * nothing, so any dispatch order is deadlock-free.  Output tiles are 80 x 128 (10 tiles x 24
+ * splits on MNIST: half the split-K partial bytes of 160 x 128 x 48, HPNN_G0_TILE=160 the
+ * old form).  Replaces the separate sgd_update_multi launch (6.2 us) and its kernel boundary
+ * behind 20 MB of dirty slabs.  All GEMM workgroups are co-resident (grid <= CUs; a wait that
+ * times out sets *err instead of hanging).  Reference: the per-layer update of
+ * snn_kernel_train_momentum / cuda_snn.cu:2726-3717 (GER into dW, W += dW, dW *= alpha),
+ * batched. */
 constexpr unsigned long long G0_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
 /* the master weight / momentum of the first element a thread steps, loaded right after the
@@ -334,6 +340,49 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
     }
 }
 
+/* [G1 | G2] on the tail workgroups (blocks past the GEMM grid, on the CUs it leaves idle; they
+ * run beside the GEMM instead of after it): float4 columns [c0, c1) summed over all mrows rows,
+ * 32 columns (512 contiguous bytes of a row) x NT / 32 row groups per pass and 16 rows of loads
+ * in flight per thread (latency-bound otherwise: a pass is one memory round trip); the row
+ * groups meet in LDS in a fixed order, then the layer-1/2 step (or the store into g12out) */
+template <int NT>
+__device__ __forceinline__ void g12_share_wide(const hpnn_g0_update &u, long c0, long c1, f32x4 *red, float *g12out) {
+    constexpr int C4 = 32, RG = NT / C4, RB = 16;
+    const int t = threadIdx.x, c = t % C4, rg = t / C4;
+    for (long b0 = c0; b0 < c1; b0 += C4) {
+        const long e4 = b0 + c;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        if (e4 < c1) {
+            const float *col = u.mslab + e4 * 4;
+            for (int r0 = rg; r0 < u.mrows; r0 += RB * RG) {
+                f32x4 v[RB];
+#pragma unroll
+                for (int k = 0; k < RB; k++) {
+                    const int r = r0 + k * RG;
+                    v[k] = r < u.mrows ? *(const f32x4 *)(col + (long)r * u.mstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int k = 0; k < RB; k++) a += v[k];
+            }
+        }
+        red[t] = a;
+        __syncthreads();
+        if (rg == 0 && e4 < c1) {
+            f32x4 g = red[c];
+            for (int r = 1; r < RG; r++) g += red[r * C4 + c];
+            if (g12out) {
+                *(f32x4 *)(g12out + e4 * 4) = g;
+            } else {
+                int n, k;
+                const int l = g12_elem(u, e4, n, k);
+                step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n,
+                           k, g, u);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 /* sum of float4 at offset o over the first `world` ranks' buffers, rank order (identical bits
  * on every rank); all loads in flight at once, system-coherent (sc0 sc1: no cache can serve a
  * stale line, so no acquire fence -- an invalidating acquire per workgroup, while the other
@@ -360,7 +409,8 @@ __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
  * exchange and the update need no launch of their own. */
 template <int NT>
 __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsigned int e, int N, int ldg, int e0, int e1,
-                                              int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12, int b) {
+                                              int nt0, int mt0, int TMF, bool pf, Pre4 pg0, Pre4 pg12, int b, long c0,
+                                              long c1) {
     const hpnn_xar_view &v = u.xv;
     const int t = threadIdx.x;
     /* the exchanged sums: stepped, or (self-test, u.xres) stored at their flat offsets; the
@@ -407,7 +457,6 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     };
     auto g0_off = [&](int c) { return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4)); };
-    const long nb = (long)gridDim.x, nf = u.n12 / 4, c0 = (long)b * nf / nb, c1 = (long)(b + 1) * nf / nb;
     const bool two = u.xchg == 2 && v.world > 1;
     barrier(0);
     if (two) {
@@ -509,6 +558,41 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
     f32x4 acc[WF][WH];
     int tile, split, m0, n0;
     const long nb = (long)tiles * splits, nf = u.n12 / 4;
+    /* [G1 | G2] float4 columns [0, nt4) belong to the tail workgroups (blocks nb..), the rest to
+     * the GEMM workgroups after their publish */
+    const int ntail = (int)gridDim.x - (int)nb;
+    const long nt4 = ntail > 0 ? u.n12t / 4 : 0;
+    if ((long)blockIdx.x >= nb) {
+        const int tb = (int)blockIdx.x - (int)nb;
+        const long tc0 = (long)tb * nt4 / ntail, tc1 = (long)(tb + 1) * nt4 / ntail;
+        __shared__ unsigned int txe_s;
+        float *gout = u.gout && u.gsel && !(*u.gsel & 1) ? u.gout + u.galt : u.gout;
+        if (u.xchg) {
+            if (threadIdx.x == 0) {
+                const unsigned int e = u.xv.ep[blockIdx.x] + 1; /* exchange slot: the block itself */
+                u.xv.ep[blockIdx.x] = e;
+                txe_s = e;
+            }
+            __syncthreads();
+            gout = u.xv.buf[u.xv.rank] + ((txe_s & 1) ? u.xv.half : 0);
+        }
+        if (u.xtest) {
+            if (u.xchg) {
+                for (long e4 = tc0 + threadIdx.x; e4 < tc1; e4 += NT) {
+                    const long i = (long)N * ldg + e4 * 4;
+                    *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
+                }
+                g0_exchange_step<NT>(u, txe_s, N, ldg, 0, 0, 0, 0, TMF, false, Pre4{}, Pre4{}, (int)blockIdx.x, tc0,
+                                     tc1);
+            }
+            return;
+        }
+        g12_share_wide<NT>(u, tc0, tc1, red, gout ? gout + (size_t)N * ldg : nullptr);
+        if (u.xchg)
+            g0_exchange_step<NT>(u, txe_s, N, ldg, 0, 0, 0, 0, TMF, false, Pre4{}, Pre4{}, (int)blockIdx.x, tc0, tc1);
+        mark(6);
+        return;
+    }
     /* the workgroup's role: virtual block vb (u.perm > 0, tests: reversed and rotated order --
      * every result must stay bitwise the same) */
     const int vb = u.perm > 0 ? (int)((nb - 1 - (long)blockIdx.x + u.perm) % nb) : (int)blockIdx.x;
@@ -538,7 +622,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
      * bit 64 turns the prefetch off) */
     const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
     const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
-    const long c0 = vb * nf / nb, c1 = (vb + 1) * nf / nb;
+    const long c0 = nt4 + vb * (nf - nt4) / nb, c1 = nt4 + (vb + 1) * (nf - nt4) / nb;
     if (u.xtest) {
         /* the known pattern in place of this workgroup's reduced G0 / [G1 | G2] shares, then the
          * exchange with its sums stored (u.xres) for the host to check */
@@ -551,7 +635,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                 const long i = (long)N * ldg + e4 * 4;
                 *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
             }
-            g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, false, Pre4{}, Pre4{}, vb);
+            g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, false, Pre4{}, Pre4{}, vb, c0, c1);
         }
         return;
     }
@@ -593,7 +677,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
     }
     mark(2);
     /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
-    if (!G0_PROTO(u, 512)) /* 512: timing ablation, no [G1 | G2] share */
+    if (!G0_PROTO(u, 512) && c1 > c0) /* 512: timing ablation, no [G1 | G2] share */
         g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
     mark(3);
     if (t == 0) {
@@ -638,7 +722,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
         __syncthreads();
     }
     mark(5);
-    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12, vb);
+    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12, vb, c0, c1);
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false, int WM = 2, int WN = 2>
@@ -740,9 +824,31 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
      * (more splits than that, e.g. forced by HPNN_TN_SPLITS, take the slab form instead of
      * stalling to the timeout) */
     if (!g0_fused_resident(tiles * splits)) return -1;
+    /* tail workgroups for the [G1 | G2] share on the CUs the GEMM grid leaves idle (MNIST: 240
+     * GEMM workgroups, 16 tails on a 256-CU MI355X); HPNN_G0_TAILS overrides the count (0: off),
+     * HPNN_G0_TAIL12 the percentage of the [G1 | G2] columns they take (the GEMM workgroups sum
+     * the rest after their publish) */
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        return hipGetDevice(&dev) == hipSuccess &&
+                       hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess
+                   ? n
+                   : 0;
+    }();
+    static const int tails_env = [] { const char *e = getenv("HPNN_G0_TAILS"); return e ? atoi(e) : -1; }();
+    static const int tail_pct = [] { const char *e = getenv("HPNN_G0_TAIL12"); return e ? atoi(e) : 100; }();
+    /* one tail per 16 slab rows (each sums ~16 x the [G1 | G2] block, 563 KB on MNIST), at most
+     * the CUs the GEMM grid leaves idle: ranks sharing one GPU (tests, rehearsals) keep their
+     * grids small enough to co-run */
+    int ntail = tails_env >= 0 ? tails_env : std::min(cus - tiles * splits, std::max(1, u->mrows / 16));
+    if (ntail < 0 || tail_pct <= 0) ntail = 0;
+    if (ntail > 64) ntail = 64;
+    while (ntail > 0 && !g0_fused_resident(tiles * splits + ntail)) ntail--;
+    if (u->xchg && tiles * splits + ntail > HPNN_XAR_MAX_BLOCKS) ntail = HPNN_XAR_MAX_BLOCKS - tiles * splits;
+    if (ntail < 0) ntail = 0;
     if (u->xchg) {
         /* the exchange buffer holds [G0 | G1 | G2]; one epoch / flag slot per workgroup */
-        if (tiles * splits > HPNN_XAR_MAX_BLOCKS || u->xv.world < 1 || u->xv.world > HPNN_XAR_MAX_RANKS ||
+        if (tiles * splits + ntail > HPNN_XAR_MAX_BLOCKS || u->xv.world < 1 || u->xv.world > HPNN_XAR_MAX_RANKS ||
             !u->xv.ep || (long)N * ldg + u->n12 > u->xv.half)
             return -1;
         for (int p = 0; p < u->xv.world; p++)
@@ -750,13 +856,15 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
     }
     const int xcd_map = (splits >= 8 && tiles > 1) ? 1 : 0;
     hpnn_g0_update uu = *u;
+    uu.n12t = ntail ? ((long)(u->n12 / 4) * (tail_pct > 100 ? 100 : tail_pct) / 100) * 4 : 0;
 #ifdef HPNN_ABLATIONS
     static const int proto = [] { const char *e = getenv("HPNN_G0_PROTO"); return e ? atoi(e) : 0; }();
     uu.proto |= proto;
 #endif
     static const bool trace = [] { const char *e = getenv("HPNN_G0_TRACE"); return e && e[0] == '1'; }();
 #define HPNN_G0F(...)                                                                                              \
-    hipLaunchKernelGGL((g0_fused_kernel<__VA_ARGS__>), dim3(tiles * splits), dim3(512), 0, stream, (const __bf16 *)Dg, \
+    hipLaunchKernelGGL((g0_fused_kernel<__VA_ARGS__>), dim3(tiles * splits + ntail), dim3(512), 0, stream,           \
+                       (const __bf16 *)Dg,                                                                         \
                        N / 16, Hg, M / 16, hscale, slab, ldg, N, Bt / 32, splits, tiles_n, tiles, xcd_map, uu)
     if (tm == 80) {
         /* HPNN_G0_PD=2 (ABLATIONS builds, tuning): two k-steps of operands in flight */

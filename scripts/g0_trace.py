@@ -25,9 +25,20 @@ def main():
     for i in range(12):
         m.train_step(Xs[i % 4], labels=lab)
     torch.cuda.synchronize()
-    G = 5 * m.S[0]
-    t = torch.tensor(native().g0_trace(), dtype=torch.float64).view(512, 8)[:G]
+    import ctypes
+    from hpnn_amd._lib import lib_path
+    G = ctypes.CDLL(lib_path()).hpnn_g0_tiles(1, m.Np[0], m.Kp[0]) * m.S[0]
+    ta = torch.tensor(native().g0_trace(), dtype=torch.float64).view(512, 8)
+    t = ta[:G]
     print(f"workgroups {G}; span median {float((t[:, 5] - t[:, 0]).median()):.0f} ticks")
+    # tail workgroups (blocks G..: the [G1 | G2] share beside the GEMM): start -> done
+    tail = ta[G:256]
+    tail = tail[tail[:, 6] > tail[:, 0]]
+    if len(tail):
+        d = tail[:, 6] - tail[:, 0]
+        print(f"tail workgroups {len(tail)}: [G1|G2] share (+ exchange) median {float(d.median()):.0f}  "
+              f"max {float(d.max()):.0f} ticks (GEMM workgroups' span median "
+              f"{float((t[:, 5] - t[:, 0]).median()):.0f})")
     for i, n in enumerate(NAMES):
         d = t[:, i + 1] - t[:, i]
         q = torch.quantile(d, torch.tensor([0.1, 0.5, 0.9], dtype=torch.float64))
