@@ -180,6 +180,9 @@ int BPlan::configure(const int *sizes, int n_layers, int net_type, int batch_siz
     if (mode == 't' || mode == 'x') {
         add("W0f", -1, BD_BF16, {(long)Np[0] * Kp[0]}, true);
         add("g0cnt", -1, BD_I32, {HPNN_G0CNT_WORDS}, true); /* fused G0 step: tile counters + error word */
+        /* its XCD-local first reduction level (HPNN_G0_XCD=1): protocol words + 8 group partials */
+        add("g0xw", -1, BD_I32, {HPNN_G0X_WORDS}, true);
+        add("g0xs", -1, BD_F32, {8, Np[0], Kp[0]}, false);
     }
     if (mode == 'w') {
         const long pb = wide_ksplit == 2 ? hpnn_wide2_pbuf_bytes(Bp) : 16;
@@ -216,6 +219,8 @@ void BPlan::name_pointers() {
     midtmp = (float *)buf("midtmp");
     W0f = buf("W0f");
     g0cnt = (unsigned int *)buf("g0cnt");
+    g0xw = (unsigned int *)buf("g0xw");
+    g0xs = (float *)buf("g0xs");
     tncnt = (unsigned int *)buf("tncnt");
     wpbuf = (float *)buf("wpbuf");
     wwords = (unsigned int *)buf("wwords");
@@ -396,6 +401,7 @@ int BPlan::g0_fused_step(const XIn &x, float lr, float alpha, float scale, hipSt
     u.W32 = W32[0], u.V32 = V32[0], u.Wb = Wb[0], u.Wt = Wt[0], u.Wf = W0f;
     u.cnt = g0cnt, u.err = g0cnt + HPNN_G0_ERR_WORD;
     u.perm = g0_perm;
+    if (g0_xcd && g0xw && g0xs) u.xw = g0xw, u.xslab = g0xs;
     u.fault = hpnn_fault_hit("handoff"); /* HPNN_FAULT=handoff:n: the n-th launch reports a timed-out wait */
     /* HPNN_FAULT=xsum:n: the n-th exchanging launch of the last rank sums one element wrong */
     u.xfault = xv && xv->world > 1 && xv->rank == xv->world - 1 && hpnn_fault_hit("xsum");

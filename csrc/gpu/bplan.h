@@ -29,6 +29,7 @@
 #ifndef HPNN_GPU_BPLAN_H
 #define HPNN_GPU_BPLAN_H
 #include <hip/hip_runtime_api.h>
+#include <stdlib.h>
 
 #include <functional>
 #include <string>
@@ -83,6 +84,8 @@ class BPlan {
     int mid_grid = 0, mid_groups = 1, wide_ksplit = 1, slab_f = 0;
     bool g0_fused = true; /* modes t / x: G0 + reduction + every step in one launch when it applies */
     int g0_perm = 0;      /* tests: > 0 runs the fused G0 grid in a permuted block -> role order */
+    /* the fused G0's XCD-local first reduction level (kernels_g0.hip; HPNN_G0_XCD=1) */
+    bool g0_xcd = [] { const char *e = getenv("HPNN_G0_XCD"); return e && e[0] == '1'; }();
     bool tn_update = true; /* the step in the 8-phase TN gradient's epilogue where it applies */
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
@@ -170,7 +173,8 @@ class BPlan {
     float *Z = nullptr, *stats = nullptr, *gflat = nullptr, *midslab = nullptr, *midtmp = nullptr;
     void *W0f = nullptr;
     float *wpbuf = nullptr;
-    unsigned int *wwords = nullptr, *g0cnt = nullptr, *tncnt = nullptr;
+    unsigned int *wwords = nullptr, *g0cnt = nullptr, *tncnt = nullptr, *g0xw = nullptr;
+    float *g0xs = nullptr;
     int *lab0 = nullptr;
     /* data-parallel BF16 exchange (csrc/dist/dp_exchange.cpp): where grad_layer(reduce) may
      * write layer l's gradient as BF16 instead of FP32 into gflat (NULL: FP32), and whether the

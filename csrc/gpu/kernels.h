@@ -139,6 +139,10 @@ typedef struct {
     int perm, xtest, xfault;
     float *xres;
     long n12t; /* set by the launcher: [G1 | G2] floats summed by the tail workgroups */
+    /* XCD-local first level of the split-K reduction (HPNN_G0_XCD=1): xw = HPNN_G0X_WORDS
+     * protocol words (zeroed once), xslab = 8 partial G0 slabs (one per XCD group); NULL: off */
+    unsigned int *xw;
+    float *xslab;
     int fault; /* test hook (HPNN_FAULT=handoff:n): the split-K wait of that launch reports a
                 * timeout (sets *err) as a real one would */
 } hpnn_g0_update;
@@ -155,6 +159,9 @@ int hpnn_g0_tile_cols(int M);
 /* hpnn_g0_update.cnt: HPNN_G0CNT_WORDS words, 64-bit tile counters 32 words apart (tile < 
  * HPNN_G0_MAX_TILES), the error word at HPNN_G0_ERR_WORD */
 #define HPNN_G0CNT_WORDS 1024
+/* hpnn_g0_update.xw layout: per-role epochs, per-(tile, group) member slots, group and tile
+ * counters (64-bit); see kernels_g0.hip */
+#define HPNN_G0X_WORDS 4096
 #define HPNN_G0_MAX_TILES 31
 #define HPNN_G0_ERR_WORD 1000
 /* workgroups of `kernel` (threads per workgroup, dynamic LDS bytes) the device can hold at once:

@@ -279,13 +279,25 @@ __device__ __forceinline__ void step_elem4(float *W32, float *V32, __bf16 *Wb, _
         for (int r = 0; r < 4; r++) Wt[(size_t)(k + r) * N + n] = wb[r];
 }
 
+/* element i of a small array inside the by-value kernel argument, as a chain of selects: a
+ * DYNAMIC index into the argument makes the compiler copy the whole 440-byte struct into every
+ * thread's scratch at kernel start (seen in the ISA: scratch_store_dwordx4 x 28 per thread) */
+template <class T, int N>
+__device__ __forceinline__ T pick(const T (&a)[N], int i) {
+    T r = a[0];
+#pragma unroll
+    for (int k = 1; k < N; k++) r = i == k ? a[k] : r;
+    return r;
+}
+
 /* float4 e4 of [G1 | G2] -> layer l, row n, column k */
 __device__ __forceinline__ int g12_elem(const hpnn_g0_update &u, long e4, int &n, int &k) {
     long i = e4 * 4;
     const long n1 = (long)u.Nb[0] * u.Kb[0];
     const int l = i < n1 ? 0 : 1;
     if (l) i -= n1;
-    n = (int)(i / u.Kb[l]), k = (int)(i % u.Kb[l]);
+    const int kb = pick(u.Kb, l);
+    n = (int)(i / kb), k = (int)(i % kb);
     return l;
 }
 __device__ __forceinline__ Pre4 pre_load(const float *W32, const float *V32, size_t idx, int momentum) {
@@ -332,7 +344,8 @@ __device__ __forceinline__ void g12_share(const hpnn_g0_update &u, long c0, long
             } else {
                 int n, k;
                 const int l = g12_elem(u, e4, n, k);
-                step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n,
+                step_elem4(pick(u.W32b, l), pick(u.V32b, l), (__bf16 *)pick(u.Wbb, l), (__bf16 *)pick(u.Wtb, l), nullptr,
+                           pick(u.Nb, l), pick(u.Kb, l), n,
                            k, g, u, use && b0 == c0 /* this thread's prefetched element */, pre);
             }
         }
@@ -375,7 +388,8 @@ __device__ __forceinline__ void g12_share_wide(const hpnn_g0_update &u, long c0,
             } else {
                 int n, k;
                 const int l = g12_elem(u, e4, n, k);
-                step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n,
+                step_elem4(pick(u.W32b, l), pick(u.V32b, l), (__bf16 *)pick(u.Wbb, l), (__bf16 *)pick(u.Wtb, l), nullptr,
+                           pick(u.Nb, l), pick(u.Kb, l), n,
                            k, g, u);
             }
         }
@@ -391,7 +405,7 @@ static_assert(HPNN_XAR_MAX_RANKS == 8, "one ld_sc1_x8 per element");
 __device__ __forceinline__ f32x4 xsum_peers(const hpnn_xar_view &v, long o) {
     const float *q[8];
 #pragma unroll
-    for (int p = 0; p < 8; p++) q[p] = v.buf[p < v.world ? p : v.rank] + o; /* spare slots: local */
+    for (int p = 0; p < 8; p++) q[p] = pick(v.buf, p < v.world ? p : v.rank) + o; /* spare slots: local */
     f32x4 x[8];
     hpnn::ld_sc1_x8<true>(x, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
     f32x4 a = x[0];
@@ -415,38 +429,40 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
     const int t = threadIdx.x;
     /* the exchanged sums: stepped, or (self-test, u.xres) stored at their flat offsets; the
      * fault hook (u.xfault, tests) corrupts the first G0 element of role 0 on this rank */
-    auto out0 = [&](int c, f32x4 g, bool use, Pre4 pre) {
+    auto out0 = [&](int c, f32x4 g, bool use, Pre4 pre) __attribute__((always_inline)) {
         const int row = c / (TMF / 4), col = mt0 + 4 * (c % (TMF / 4));
         if (u.xfault && b == 0 && c == e0) g[0] += 1.0f;
         if (u.xres) *(f32x4 *)(u.xres + (size_t)(nt0 + row) * ldg + col) = g;
         else step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
                         use, pre);
     };
-    auto out12 = [&](long e4, f32x4 g, bool use, Pre4 pre) {
+    auto out12 = [&](long e4, f32x4 g, bool use, Pre4 pre) __attribute__((always_inline)) {
         if (u.xres) {
             *(f32x4 *)(u.xres + (size_t)N * ldg + e4 * 4) = g;
             return;
         }
         int n, k;
         const int l = g12_elem(u, e4, n, k);
-        step_elem4(u.W32b[l], u.V32b[l], (__bf16 *)u.Wbb[l], (__bf16 *)u.Wtb[l], nullptr, u.Nb[l], u.Kb[l], n, k, g,
+        step_elem4(pick(u.W32b, l), pick(u.V32b, l), (__bf16 *)pick(u.Wbb, l), (__bf16 *)pick(u.Wtb, l), nullptr,
+                           pick(u.Nb, l), pick(u.Kb, l), n, k, g,
                    u, use, pre);
     };
     const long hoff = (e & 1) ? v.half : 0;
     /* flag barrier `which` of workgroup b with every peer: this workgroup's stores to its buffer
      * acknowledged first (uncached memory: no writeback needed) */
-    auto barrier = [&](int which) {
+    auto barrier = [&](int which) __attribute__((always_inline)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t < v.world && !G0_PROTO(u, 16)) { /* proto & 16: no barrier (one-rank timing ablation only) */
-            unsigned int *const mine = which ? HPNN_XAR_FLAG_B(v.sig[v.rank], b, t) : HPNN_XAR_FLAG_A(v.sig[v.rank], b, t);
-            __hip_atomic_store(which ? HPNN_XAR_FLAG_B(v.sig[t], b, v.rank) : HPNN_XAR_FLAG_A(v.sig[t], b, v.rank), e,
+            unsigned int *const sm = pick(v.sig, v.rank), *const sp = pick(v.sig, t);
+            unsigned int *const mine = which ? HPNN_XAR_FLAG_B(sm, b, t) : HPNN_XAR_FLAG_A(sm, b, t);
+            __hip_atomic_store(which ? HPNN_XAR_FLAG_B(sp, b, v.rank) : HPNN_XAR_FLAG_A(sp, b, v.rank), e,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             const unsigned long long t0 = wall_clock64();
             while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
                 __builtin_amdgcn_s_sleep(1);
                 if (wall_clock64() - t0 > v.timeout) {
-                    __hip_atomic_store(v.sig[v.rank] + HPNN_XAR_ERROR_WORD, 1u, __ATOMIC_RELAXED,
+                    __hip_atomic_store(pick(v.sig, v.rank) + HPNN_XAR_ERROR_WORD, 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
@@ -456,7 +472,9 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         if (G0_PROTO(u, 8)) /* diagnostics: the invalidating system acquire as well */
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     };
-    auto g0_off = [&](int c) { return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4)); };
+    auto g0_off = [&](int c) __attribute__((always_inline)) {
+        return (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4));
+    };
     const bool two = u.xchg == 2 && v.world > 1;
     barrier(0);
     if (two) {
@@ -466,12 +484,12 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         for (int c = e0 + t; c < e1; c += NT)
             if ((c - e0) % v.world == v.rank) {
                 const long o = hoff + g0_off(c);
-                *(f32x4 *)(v.buf[v.rank] + o) = xsum_peers(v, o);
+                *(f32x4 *)(pick(v.buf, v.rank) + o) = xsum_peers(v, o);
             }
         for (long e4 = c0 + t; e4 < c1; e4 += NT)
             if ((int)((e4 - c0) % v.world) == v.rank) {
                 const long o = hoff + (long)N * ldg + e4 * 4;
-                *(f32x4 *)(v.buf[v.rank] + o) = xsum_peers(v, o);
+                *(f32x4 *)(pick(v.buf, v.rank) + o) = xsum_peers(v, o);
             }
         barrier(1);
     }
@@ -483,7 +501,8 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         const long oa = h0 ? hoff + g0_off(e0 + t) : hoff, ob = h12 ? hoff + (long)N * ldg + (c0 + t) * 4 : hoff;
         f32x4 ga, gb;
         if (two) { /* the owners' sums (owner of element j = t: rank t % world) */
-            const float *qa = v.buf[h0 ? t % v.world : v.rank] + oa, *qb = v.buf[h12 ? t % v.world : v.rank] + ob;
+            const float *qa = pick(v.buf, h0 ? t % v.world : v.rank) + oa;
+            const float *qb = pick(v.buf, h12 ? t % v.world : v.rank) + ob;
             asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
                          "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
                          "s_waitcnt vmcnt(0)"
@@ -495,8 +514,8 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
             const float *q[8];
 #pragma unroll
             for (int p = 0; p < 4; p++) {
-                q[p] = v.buf[p < v.world ? p : v.rank] + oa;
-                q[4 + p] = v.buf[p < v.world ? p : v.rank] + ob;
+                q[p] = pick(v.buf, p < v.world ? p : v.rank) + oa;
+                q[4 + p] = pick(v.buf, p < v.world ? p : v.rank) + ob;
             }
             hpnn::ld_sc1_x8<true>(x, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
             ga = x[0];
@@ -513,9 +532,9 @@ __device__ __forceinline__ void g0_exchange_step(const hpnn_g0_update &u, unsign
         return;
     }
     /* one-shot: the rank-order sum over every peer; two-shot: the owner's sum */
-    auto fetch = [&](long o, long j) -> f32x4 {
+    auto fetch = [&](long o, long j) __attribute__((always_inline)) -> f32x4 {
         if (!two) return xsum_peers(v, o);
-        const float *q = v.buf[(int)(j % v.world)] + o;
+        const float *q = pick(v.buf, (int)(j % v.world)) + o;
         f32x4 x; /* one system-coherent load and its wait in one asm block (see ld_sc1_x8) */
         asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(q) : "memory");
         return x;
@@ -534,6 +553,69 @@ __device__ __forceinline__ f32x4 xtest_pattern(int rank, long i) {
     return v;
 }
 
+/* ---- XCD-local first level of the split-K reduction (u.xw, HPNN_G0_XCD=1) -------------
+ * The splits of a tile form 8 static groups g = split % 8 of gsz = splits / 8 members (MNIST:
+ * 24 splits, 3 a group).  Under the round-robin placement a group's members share one XCD, so
+ * they can combine through that XCD's L2 instead of publishing write-through: every member
+ * stores its partial tile PLAIN (it stays in the L2), the group's last arriver sums the gsz
+ * partials (L1-bypassing loads served by the L2) and publishes ONE write-through partial per
+ * (tile, group), and the tile's reducers then read 8 partials instead of `splits`.  The
+ * placement is never assumed: at kernel start every member records (launch epoch, hardware
+ * XCC_ID) in its group slot, and after its GEMM it stores plain only when every member of the
+ * group has recorded this epoch on ITS XCD -- otherwise write-through, which any reader can
+ * see.  All sums keep a fixed order (members, then groups): bitwise the same whichever block
+ * takes which role and whichever store form ran. */
+constexpr int G0X_EP = 0, G0X_SLOTS = 256, G0X_GCNT = 2304, G0X_TCNT = 2816;
+static_assert(G0X_TCNT + 32 * HPNN_G0_MAX_TILES <= HPNN_G0X_WORDS, "xw layout");
+static_assert(G0X_SLOTS + 64 * HPNN_G0_MAX_TILES <= G0X_GCNT && G0X_GCNT + 16 * HPNN_G0_MAX_TILES <= G0X_TCNT,
+              "xw layout");
+
+__device__ __forceinline__ unsigned int xcc_id() {
+    return (unsigned int)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u; /* HW_REG_XCC_ID[3:0] */
+}
+
+/* the group leader: out[e] = sum over members m (in order) of part[m][e], float4 e of the tile
+ * at offsets off(e); NT threads, NE4 float4, G members (static: every index below is
+ * compile-time, no scratch); write-through stores */
+template <int NT, int NE4, int TMF, int G>
+__device__ __forceinline__ void xcd_group_sum_g(const float *slab0, size_t mstride, float *out, int ldg, int nt0,
+                                                int mt0) {
+    constexpr int KE = (NE4 + NT - 1) / NT, EPB = 16 / G; /* float4 per thread, per 16-load batch */
+    const int t = threadIdx.x;
+    auto off = [&](int c) __attribute__((always_inline)) {
+        return (size_t)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4));
+    };
+#pragma unroll
+    for (int k0 = 0; k0 < KE; k0 += EPB) {
+        const float *q[16];
+        f32x4 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int k = k0 + i / G, m = i % G, c = t + k * NT;
+            const bool ok = i < EPB * G && k < KE && c < NE4;
+            q[i] = slab0 + (ok ? off(c) + (size_t)m * mstride : off(t < NE4 ? t : 0)); /* spares: a valid line */
+        }
+        hpnn::ld_sc1_x16(v, q);
+#pragma unroll
+        for (int j = 0; j < EPB; j++) {
+            const int k = k0 + j, c = t + k * NT;
+            if (k < KE && c < NE4) {
+                f32x4 a = v[j * G];
+#pragma unroll
+                for (int m = 1; m < G; m++) a += v[j * G + m];
+                st_sc1(out + off(c), a);
+            }
+        }
+    }
+}
+template <int NT, int NE4, int TMF>
+__device__ __forceinline__ void xcd_group_sum(const float *slab0, size_t mstride, float *out, int gsz, int ldg,
+                                              int nt0, int mt0) {
+    if (gsz == 2) xcd_group_sum_g<NT, NE4, TMF, 2>(slab0, mstride, out, ldg, nt0, mt0);
+    else if (gsz == 3) xcd_group_sum_g<NT, NE4, TMF, 3>(slab0, mstride, out, ldg, nt0, mt0);
+    else xcd_group_sum_g<NT, NE4, TMF, 4>(slab0, mstride, out, ldg, nt0, mt0);
+}
+
 /* HPNN_G0_TRACE=1 (profiling only): s_memtime stamps of every workgroup's thread 0 at the
  * phase boundaries, [block][mark]; read back with hpnn_g0_trace */
 constexpr int G0TR_BLOCKS = 512, G0TR_MARKS = 8;
@@ -547,7 +629,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                                                             hpnn_g0_update u) {
     constexpr int GW = WM * WN, NT = 64 * GW * KW, TMF = 16 * WF * WM, TNH = 16 * WH * WN, NE4 = TMF * TNH / 4,
                   PARTS = NT / 128;
-    auto mark = [&](int i) {
+    auto mark = [&](int i) __attribute__((always_inline)) {
         if constexpr (TRACE) {
             const unsigned long long tt = __builtin_amdgcn_s_memtime();
             if (threadIdx.x == 0 && blockIdx.x < G0TR_BLOCKS) g_g0_trace[blockIdx.x][i] = tt;
@@ -562,6 +644,12 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
      * the GEMM workgroups after their publish */
     const int ntail = (int)gridDim.x - (int)nb;
     const long nt4 = ntail > 0 ? u.n12t / 4 : 0;
+    /* the exchange's parameters, set by whichever path this workgroup takes */
+    bool xdo = false, xpf = false;
+    int xb = 0, xe0 = 0, xe1 = 0, xnt0 = 0, xmt0 = 0;
+    unsigned int xep = 0;
+    long xc0 = 0, xc1 = 0;
+    Pre4 xpg0 = {}, xpg12 = {};
     if ((long)blockIdx.x >= nb) {
         const int tb = (int)blockIdx.x - (int)nb;
         const long tc0 = (long)tb * nt4 / ntail, tc1 = (long)(tb + 1) * nt4 / ntail;
@@ -574,7 +662,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                 txe_s = e;
             }
             __syncthreads();
-            gout = u.xv.buf[u.xv.rank] + ((txe_s & 1) ? u.xv.half : 0);
+            gout = pick(u.xv.buf, u.xv.rank) + ((txe_s & 1) ? u.xv.half : 0);
         }
         if (u.xtest) {
             if (u.xchg) {
@@ -582,147 +670,206 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                     const long i = (long)N * ldg + e4 * 4;
                     *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
                 }
-                g0_exchange_step<NT>(u, txe_s, N, ldg, 0, 0, 0, 0, TMF, false, Pre4{}, Pre4{}, (int)blockIdx.x, tc0,
-                                     tc1);
             }
-            return;
-        }
-        g12_share_wide<NT>(u, tc0, tc1, red, gout ? gout + (size_t)N * ldg : nullptr);
-        if (u.xchg)
-            g0_exchange_step<NT>(u, txe_s, N, ldg, 0, 0, 0, 0, TMF, false, Pre4{}, Pre4{}, (int)blockIdx.x, tc0, tc1);
-        mark(6);
-        return;
-    }
-    /* the workgroup's role: virtual block vb (u.perm > 0, tests: reversed and rotated order --
-     * every result must stay bitwise the same) */
-    const int vb = u.perm > 0 ? (int)((nb - 1 - (long)blockIdx.x + u.perm) % nb) : (int)blockIdx.x;
-    if (u.xtest) /* self-test of the in-kernel exchange: no GEMM (the role only) */
-        fm_role(vb, splits, tiles, xcd_map, tile, split);
-    else
-        fm_partial<WF, WH, PD, KW, HU8, WM, WN>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, vb, acc,
-                                                tile, split, m0, n0);
-    mark(1);
-    const int t = threadIdx.x, lane = t & 63;
-    /* where the reduced gradient goes instead of a step: the plan's buffer, the xGMI
-     * all-reduce's next half (gsel), or -- exchanging here -- this workgroup's epoch's half of
-     * this rank's exchange buffer */
-    __shared__ unsigned int xe_s;
-    float *gout = u.gout && u.gsel && !(*u.gsel & 1) ? u.gout + u.galt : u.gout;
-    if (u.xchg) {
-        if (t == 0) {
-            const unsigned int e = u.xv.ep[vb] + 1; /* only this workgroup touches it */
-            u.xv.ep[vb] = e;
-            xe_s = e;
-        }
-        __syncthreads();
-        gout = u.xv.buf[u.xv.rank] + ((xe_s & 1) ? u.xv.half : 0);
-    }
-    /* this split's share of the tile (float4 [e0, e1)) and of [G1 | G2] ([c0, c1)); the first
-     * element of each that this thread will step: its W / V loads go out now (HPNN_G0_PROTO
-     * bit 64 turns the prefetch off) */
-    const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
-    const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
-    const long c0 = nt4 + vb * (nf - nt4) / nb, c1 = nt4 + (vb + 1) * (nf - nt4) / nb;
-    if (u.xtest) {
-        /* the known pattern in place of this workgroup's reduced G0 / [G1 | G2] shares, then the
-         * exchange with its sums stored (u.xres) for the host to check */
-        if (u.xchg) {
-            for (int c = e0 + t; c < e1; c += NT) {
-                const long i = (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4));
-                *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
-            }
-            for (long e4 = c0 + t; e4 < c1; e4 += NT) {
-                const long i = (long)N * ldg + e4 * 4;
-                *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
-            }
-            g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, false, Pre4{}, Pre4{}, vb, c0, c1);
-        }
-        return;
-    }
-    const bool steps = !u.gout || u.xchg, pf = steps && !G0_PROTO(u, 64);
-    Pre4 pg0 = {}, pg12 = {};
-    if (pf && t < 128 && e0 + t < e1) {
-        const int e = e0 + t, row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
-        pg0 = pre_load(u.W32, u.V32, (size_t)(nt0 + row) * ldg + col, u.momentum);
-    }
-    if (pf && t < 16 && c0 + t < c1) {
-        int n, k;
-        const int l = g12_elem(u, c0 + t, n, k);
-        pg12 = pre_load(u.W32b[l], u.V32b[l], (size_t)n * u.Kb[l] + k, u.momentum);
-    }
-    /* publish this split's partial tile (write-through), then one ticket for the workgroup */
-    if ((t >> 6) < GW) {
-        const int r16 = lane & 15, q = lane >> 4;
-        float *out = slab + (size_t)split * N * ldg;
-        if (G0_PROTO(u, 256)) {
-            /* timing ablation: no publish at all (wrong results) */
         } else {
-#pragma unroll
-            for (int i = 0; i < WF; i++)
-#pragma unroll
-                for (int j = 0; j < WH; j++)
-                    st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q,
-                           HU8 ? acc[i][j] * hscale : acc[i][j]);
+            g12_share_wide<NT>(u, tc0, tc1, red, gout ? gout + (size_t)N * ldg : nullptr);
         }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ unsigned long long want_s;
-    if (t == 0) {
-        if (G0_PROTO(u, 1)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        xdo = u.xchg != 0, xb = (int)blockIdx.x, xep = txe_s, xc0 = tc0, xc1 = tc1;
+    } else {
+        /* the workgroup's role: virtual block vb (u.perm > 0, tests: reversed and rotated order --
+         * every result must stay bitwise the same) */
+        const int vb = u.perm > 0 ? (int)((nb - 1 - (long)blockIdx.x + u.perm) % nb) : (int)blockIdx.x;
+        /* XCD-local first reduction level: this member's (epoch, XCC) in its group slot, before the
+         * GEMM (the members check each other's after theirs) */
+        const int gsz = splits / 8;
+        const bool xg = u.xw && !u.xtest && xcd_map && splits % 8 == 0 && gsz >= 2 && gsz <= 4;
+        unsigned int x_me = 0;
+        if (xg && threadIdx.x == 0) {
+            int tl, sp;
+            fm_role(vb, splits, tiles, xcd_map, tl, sp);
+            const unsigned int ep =
+                __hip_atomic_fetch_add(u.xw + G0X_EP + vb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            x_me = (ep << 4) | xcc_id();
+            __hip_atomic_store(u.xw + G0X_SLOTS + (tl * 8 + (sp & 7)) * 8 + (sp >> 3), x_me, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (u.xtest) /* self-test of the in-kernel exchange: no GEMM (the role only) */
+            fm_role(vb, splits, tiles, xcd_map, tile, split);
+        else
+            fm_partial<WF, WH, PD, KW, HU8, WM, WN>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, vb, acc,
+                                                    tile, split, m0, n0);
+        mark(1);
+        const int t = threadIdx.x, lane = t & 63;
+        /* where the reduced gradient goes instead of a step: the plan's buffer, the xGMI
+         * all-reduce's next half (gsel), or -- exchanging here -- this workgroup's epoch's half of
+         * this rank's exchange buffer */
+        __shared__ unsigned int xe_s;
+        float *gout = u.gout && u.gsel && !(*u.gsel & 1) ? u.gout + u.galt : u.gout;
+        if (u.xchg) {
+            if (t == 0) {
+                const unsigned int e = u.xv.ep[vb] + 1; /* only this workgroup touches it */
+                u.xv.ep[vb] = e;
+                xe_s = e;
+            }
+            __syncthreads();
+            gout = pick(u.xv.buf, u.xv.rank) + ((xe_s & 1) ? u.xv.half : 0);
+        }
+        /* this split's share of the tile (float4 [e0, e1)) and of [G1 | G2] ([c0, c1)); the first
+         * element of each that this thread will step: its W / V loads go out now (HPNN_G0_PROTO
+         * bit 64 turns the prefetch off) */
+        const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
+        const int nt0 = (tile % tiles_n) * TNH, mt0 = (tile / tiles_n) * TMF;
+        const long c0 = nt4 + vb * (nf - nt4) / nb, c1 = nt4 + (vb + 1) * (nf - nt4) / nb;
+        if (u.xtest) {
+            /* the known pattern in place of this workgroup's reduced G0 / [G1 | G2] shares, then the
+             * exchange with its sums stored (u.xres) for the host to check */
+            if (u.xchg) {
+                for (int c = e0 + t; c < e1; c += NT) {
+                    const long i = (long)(nt0 + c / (TMF / 4)) * ldg + mt0 + 4 * (c % (TMF / 4));
+                    *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
+                }
+                for (long e4 = c0 + t; e4 < c1; e4 += NT) {
+                    const long i = (long)N * ldg + e4 * 4;
+                    *(f32x4 *)(gout + i) = xtest_pattern(u.xv.rank, i);
+                }
+                xdo = true, xb = vb, xep = xe_s, xe0 = e0, xe1 = e1, xnt0 = nt0, xmt0 = mt0, xc0 = c0, xc1 = c1;
+            }
+        } else {
+            const bool steps = !u.gout || u.xchg, pf = steps && !G0_PROTO(u, 64);
+            Pre4 pg0 = {}, pg12 = {};
+            if (pf && t < 128 && e0 + t < e1) {
+                const int e = e0 + t, row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
+                pg0 = pre_load(u.W32, u.V32, (size_t)(nt0 + row) * ldg + col, u.momentum);
+            }
+            if (pf && t < 16 && c0 + t < c1) {
+                int n, k;
+                const int l = g12_elem(u, c0 + t, n, k);
+                pg12 = pre_load(pick(u.W32b, l), pick(u.V32b, l), (size_t)n * pick(u.Kb, l) + k, u.momentum);
+            }
+            /* publish this split's partial tile (write-through), then one ticket for the workgroup */
+            __shared__ int xloc_s, xlead_s;
+            const int xgrp = split & 7;
+            if (xg) {
+                if (t == 0) { /* every member of the group recorded this epoch on this XCD? */
+                    bool loc = true;
+                    for (int m = 0; m < gsz; m++)
+                        loc = loc && __hip_atomic_load(u.xw + G0X_SLOTS + (tile * 8 + xgrp) * 8 + m, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) == x_me;
+                    xloc_s = loc;
+                }
+                __syncthreads();
+            }
+            if ((t >> 6) < GW) {
+                const int r16 = lane & 15, q = lane >> 4;
+                float *out = slab + (size_t)split * N * ldg;
+                if (G0_PROTO(u, 256)) {
+                    /* timing ablation: no publish at all (wrong results) */
+                } else if (xg && xloc_s) { /* the group's leader reads it from this XCD's L2 */
+        #pragma unroll
+                    for (int i = 0; i < WF; i++)
+        #pragma unroll
+                        for (int j = 0; j < WH; j++)
+                            *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) =
+                                HU8 ? acc[i][j] * hscale : acc[i][j];
+                } else {
+        #pragma unroll
+                    for (int i = 0; i < WF; i++)
+        #pragma unroll
+                        for (int j = 0; j < WH; j++)
+                            st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q,
+                                   HU8 ? acc[i][j] * hscale : acc[i][j]);
+                }
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        want_s = hpnn::ticket_arrive(u.cnt + 32 * tile, (unsigned)splits); /* this launch's last ticket */
-    }
-    mark(2);
-    /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
-    if (!G0_PROTO(u, 512) && c1 > c0) /* 512: timing ablation, no [G1 | G2] share */
-        g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
-    mark(3);
-    if (t == 0) {
-        /* fault hook: this launch reports a timed-out wait (and, like one, reduces what is there) */
-        if (u.fault) __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else hpnn::ticket_wait(u.cnt + 32 * tile, want_s, u.err, G0_TIMEOUT);
-        if (G0_PROTO(u, 2)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    mark(4);
-    /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
-     * float4, each summing a fixed run of splits; the runs meet in LDS in order */
-    const int f = t % 128, part = t / 128;
-    const int s0 = part * splits / PARTS, s1 = (part + 1) * splits / PARTS;
-    const size_t ss = (size_t)N * ldg;
-    for (int cc = e0; cc < e1; cc += 128) {
-        const int e = cc + f;
-        const int row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
-        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-        if (e < e1 && !G0_PROTO(u, 1024)) { /* 1024: timing ablation, no split loads */
-            const float *p = slab + (size_t)(nt0 + row) * ldg + col;
-            if (G0_PROTO(u, 4))
-                for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8<true>(p + (size_t)s * ss, ss, s1 - s);
-            else
-                for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
-        }
-        red[t] = sum;
-        __syncthreads();
-        if (part == 0 && e < e1) {
-            f32x4 g = red[f];
-#pragma unroll
-            for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
-            if (gout)
-                *(f32x4 *)(gout + (size_t)(nt0 + row) * ldg + col) = g;
-            else
-                step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
-                           pf && cc == e0, pg0);
-        }
-        __syncthreads();
-    }
-    mark(5);
-    if (u.xchg) g0_exchange_step<NT>(u, xe_s, N, ldg, e0, e1, nt0, mt0, TMF, pf, pg0, pg12, vb, c0, c1);
+            __syncthreads();
+            __shared__ unsigned long long want_s;
+            unsigned int *const tcnt = xg ? u.xw + G0X_TCNT + 32 * tile : u.cnt + 32 * tile;
+            if (t == 0) {
+                if (G0_PROTO(u, 1)) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (xg) {
+                    /* group ticket: the last arriver of the launch leads; the tile then waits for its 8
+                     * group partials (both counters monotonic: gsz and 8 per launch) */
+                    unsigned long long *const gc = (unsigned long long *)(u.xw + G0X_GCNT + 2 * (tile * 8 + xgrp));
+                    const unsigned long long old = atomicAdd(gc, 1ull);
+                    xlead_s = (int)(old % gsz) == gsz - 1;
+                    want_s = (old / gsz + 1) * 8ull;
+                } else {
+                    want_s = hpnn::ticket_arrive(u.cnt + 32 * tile, (unsigned)splits); /* this launch's last ticket */
+                }
+            }
+            if (xg) {
+                __syncthreads();
+                if (xlead_s) {
+                    /* the group's partial: its gsz member slots summed in member order (plain-stored ones
+                     * sit in this XCD's L2, write-through ones in memory; both visible to sc1 loads) */
+                    xcd_group_sum<NT, NE4, TMF>(slab + (size_t)xgrp * N * ldg, (size_t)8 * N * ldg,
+                                                u.xslab + (size_t)xgrp * N * ldg, gsz, ldg, nt0, mt0);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (t == 0) atomicAdd((unsigned long long *)tcnt, 1ull);
+                }
+            }
+            mark(2);
+            /* while the other splits finish: this workgroup's share of [G1 | G2] (no dependency on G0) */
+            if (!G0_PROTO(u, 512) && c1 > c0) /* 512: timing ablation, no [G1 | G2] share */
+                g12_share<NT>(u, c0, c1, red, gout ? gout + (size_t)N * ldg : nullptr, pf && t < 16, pg12);
+            mark(3);
+            if (t == 0) {
+                /* fault hook: this launch reports a timed-out wait (and, like one, reduces what is there) */
+                if (u.fault) __hip_atomic_store((gu32 *)u.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else hpnn::ticket_wait(tcnt, want_s, u.err, G0_TIMEOUT);
+                if (G0_PROTO(u, 2)) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            }
+            __syncthreads();
+            mark(4);
+            /* this split's share of the tile: float4 e in [e0, e1), 128 at a time; PARTS threads per
+             * float4, each summing a fixed run of splits; the runs meet in LDS in order */
+            const int f = t % 128, part = t / 128;
+            /* the partials to sum: `splits` split slabs, or the 8 XCD-group partials */
+            const int rn = xg ? 8 : splits;
+            const float *const rbase = xg ? u.xslab : slab;
+            const int s0 = part * rn / PARTS, s1 = (part + 1) * rn / PARTS;
+            const size_t ss = (size_t)N * ldg;
+            for (int cc = e0; cc < e1; cc += 128) {
+                const int e = cc + f;
+                const int row = e / (TMF / 4), col = mt0 + 4 * (e % (TMF / 4));
+                f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+                if (e < e1 && !G0_PROTO(u, 1024)) { /* 1024: timing ablation, no split loads */
+                    const float *p = rbase + (size_t)(nt0 + row) * ldg + col;
+                    if (G0_PROTO(u, 4))
+                        for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8<true>(p + (size_t)s * ss, ss, s1 - s);
+                    else
+                        for (int s = s0; s < s1; s += 8) sum += sum_sc1_x8(p + (size_t)s * ss, ss, s1 - s);
+                }
+                red[t] = sum;
+                __syncthreads();
+                if (part == 0 && e < e1) {
+                    f32x4 g = red[f];
+        #pragma unroll
+                    for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
+                    if (gout)
+                        *(f32x4 *)(gout + (size_t)(nt0 + row) * ldg + col) = g;
+                    else
+                        step_elem4(u.W32, u.V32, (__bf16 *)u.Wb, (__bf16 *)u.Wt, (__bf16 *)u.Wf, N, ldg, nt0 + row, col, g, u,
+                                   pf && cc == e0, pg0);
+                }
+                __syncthreads();
+            }
+            mark(5);
+            xdo = u.xchg != 0, xb = vb, xep = xe_s, xe0 = e0, xe1 = e1, xnt0 = nt0, xmt0 = mt0, xc0 = c0, xc1 = c1;
+            xpf = pf, xpg0 = pg0, xpg12 = pg12;
+        }  /* not the self-test */
+    }  /* GEMM workgroups */
+    /* ONE inlined copy of the exchange for every path (several copies made the compiler keep the
+     * by-value kernel argument in scratch) */
+    if (xdo) g0_exchange_step<NT>(u, xep, N, ldg, xe0, xe1, xnt0, xmt0, TMF, xpf, xpg0, xpg12, xb, xc0, xc1);
+    if ((long)blockIdx.x >= nb) mark(6);
 }
 
 template <int WF, int WH, int PD, int KW, bool HU8 = false, int WM = 2, int WN = 2>

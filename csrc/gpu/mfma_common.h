@@ -283,6 +283,32 @@ __device__ __forceinline__ void ld_sc1_x8(f32x4 (&v)[8], const float *p0, const 
     else HPNN_LDX8("sc1");
 }
 #undef HPNN_LDX8
+/* 16 L1-bypassing (sc1) loads and their drain in one asm block (see ld_sc1_x8) */
+__device__ __forceinline__ void ld_sc1_x16(f32x4 (&v)[16], const float *const (&p)[16]) {
+    asm volatile("global_load_dwordx4 %0, %16, off sc1\n\t"
+                 "global_load_dwordx4 %1, %17, off sc1\n\t"
+                 "global_load_dwordx4 %2, %18, off sc1\n\t"
+                 "global_load_dwordx4 %3, %19, off sc1\n\t"
+                 "global_load_dwordx4 %4, %20, off sc1\n\t"
+                 "global_load_dwordx4 %5, %21, off sc1\n\t"
+                 "global_load_dwordx4 %6, %22, off sc1\n\t"
+                 "global_load_dwordx4 %7, %23, off sc1\n\t"
+                 "global_load_dwordx4 %8, %24, off sc1\n\t"
+                 "global_load_dwordx4 %9, %25, off sc1\n\t"
+                 "global_load_dwordx4 %10, %26, off sc1\n\t"
+                 "global_load_dwordx4 %11, %27, off sc1\n\t"
+                 "global_load_dwordx4 %12, %28, off sc1\n\t"
+                 "global_load_dwordx4 %13, %29, off sc1\n\t"
+                 "global_load_dwordx4 %14, %30, off sc1\n\t"
+                 "global_load_dwordx4 %15, %31, off sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                   "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]),
+                   "=&v"(v[14]), "=&v"(v[15])
+                 : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8]),
+                   "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15])
+                 : "memory");
+}
 /* sum over n <= 8 consecutive slabs (stride ss floats) of the float4 at p, via ld_sc1_x8:
  * the slots past n load slab 0 again and are dropped after the wait */
 template <bool SYS = false>

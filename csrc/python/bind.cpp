@@ -182,6 +182,7 @@ void bind_plan(py::module_ &m) {
              })
         .def_readwrite("g0_fused", &BPlan::g0_fused)
         .def_readwrite("g0_perm", &BPlan::g0_perm)
+        .def_readwrite("g0_xcd", &BPlan::g0_xcd)
         .def_readwrite("tn_update", &BPlan::tn_update)
         .def("tn_update_ok", &BPlan::tn_update_ok)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {

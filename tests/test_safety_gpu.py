@@ -57,6 +57,7 @@ def test_forced_g0_splits_beyond_residency_take_slab_path(gpu):
 def test_ticket_counters_past_2pow32(gpu):
     a = MLP(MNIST, "SNN", batch=16384, momentum=True, fused="t")
     b = MLP(MNIST, "SNN", batch=16384, momentum=True, fused="t")
+    a.plan.g0_xcd = b.plan.g0_xcd = False  # the flat reduction's tile counters (the XCD level has its own)
     S = a.S[0]
     cnt = b.buf[("g0cnt", -1)].view(torch.int64)  # 64-bit tile counters, 32 words apart
     start = (2 ** 32 // S) * S  # the launches' tickets cross 2^32
@@ -231,3 +232,28 @@ def test_train_nn_leaves_xgmi_when_replicas_disagree(gpu, tmp_path):
             raise
         outs.append((p.returncode, o, e))
     assert "falling back to RCCL from rank 0's weights" in outs[0][2], outs[0][2][-2000:]
+
+
+def test_g0_xcd_local_level_bitwise(gpu):
+    """the XCD-local first level of the fused G0's split-K reduction (plan.g0_xcd: members of a
+    group combine through their XCD's L2, one write-through partial per (tile, group)): the
+    same weights as the flat reduction up to FP32 summation order, and bitwise the same in a
+    permuted block -> role order (the group's store form depends on where its members landed,
+    read from the hardware XCC_ID; the sums keep one fixed order)"""
+    runs = {}
+    for key, xcd, perm in (("flat", False, 0), ("xcd", True, 0), ("xcd_perm", True, 97), ("xcd_rev", True, 240)):
+        m = MLP(MNIST, "SNN", batch=65536, momentum=True, fused="t")
+        m.plan.g0_xcd = xcd
+        m.plan.g0_perm = perm
+        X, lab = _batch(m)
+        for _ in range(3):
+            m.train_step(X, labels=lab)
+        torch.cuda.synchronize()
+        assert m.healthy()
+        runs[key] = [t.clone() for t in list(m.W32) + list(m.V32)]
+        del m
+    for k in ("xcd_perm", "xcd_rev"):
+        for a, b in zip(runs["xcd"], runs[k]):
+            assert torch.equal(a, b), k
+    for a, b in zip(runs["xcd"], runs["flat"]):
+        torch.testing.assert_close(a, b, rtol=0, atol=2e-6)
