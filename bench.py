@@ -74,6 +74,10 @@ def main():
                     help="untimed steps for about this long before the warmup, so the timed steps see the GPU at "
                          "its steady clock (the first ~20 ms of steps after idle run 10-20%% slower; "
                          "profiles/r5/SUMMARY.md); 0: off")
+    ap.add_argument("--eager-warmup", type=int, default=1,
+                    help="1 (default): the W warmup steps as eager launches, so the run captures ONE graph -- a "
+                         "second captured graph (W %% graph-steps steps) made the timed replay 4-5 us per step "
+                         "slower on the GPU (profiles/r6/SUMMARY.md); 0: a graph of W %% graph-steps steps")
     ap.add_argument("--warmup-first", action="store_true",
                     help="the W warmup steps before the settle phase instead of after it (A/B: no measurable "
                          "difference, profiles/r6/SUMMARY.md)")
@@ -137,6 +141,8 @@ def main():
     # --graph 2 forces capture with torch.distributed collectives too
     use_graph = bool(args.graph) and (not dp.active or dp.native is not None or args.graph == 2)
     gsteps = max(1, args.graph_steps)
+    if args.steps % gsteps and args.steps <= 5 * gsteps:
+        gsteps = args.steps  # one graph for the timed steps (and the settle phase), no remainder graph
     graphs = {}
 
     def capture(n):
@@ -204,7 +210,8 @@ def main():
         # never ran, so the ranks stay in step)
         ok = True
         try:
-            for n in {gsteps, args.steps % gsteps, args.warmup % gsteps} - {0}:
+            wn = 0 if args.eager_warmup else args.warmup % gsteps
+            for n in {gsteps, args.steps % gsteps, wn} - {0}:
                 capture(n)
         except Exception as e:  # noqa: BLE001
             ok = False
@@ -218,8 +225,8 @@ def main():
 
     marks = []  # --replay-trace: one event after each timed replay
 
-    def run_steps(first, n, trace=False):
-        if use_graph:
+    def run_steps(first, n, trace=False, eager=False):
+        if use_graph and not eager:
             for _ in range(n // gsteps):
                 graphs[gsteps].replay()
                 if trace:
@@ -235,7 +242,7 @@ def main():
     # collectives), then the W warmup steps, then the K timed steps
     settle = 0
     if args.warmup_first:
-        run_steps(0, args.warmup)
+        run_steps(0, args.warmup, eager=bool(args.eager_warmup))
     if args.settle_ms > 0:
         t_a = time.perf_counter()
         run_steps(0, gsteps)
@@ -248,7 +255,7 @@ def main():
         run_steps(gsteps, settle)
         settle += gsteps
     if not args.warmup_first:
-        run_steps(0, args.warmup)
+        run_steps(0, args.warmup, eager=bool(args.eager_warmup))
     torch.cuda.synchronize()
     if world > 1 and rank == world - 1 and native().fault_hit("weights"):
         # test hook (HPNN_FAULT=weights:1): one replica's weights drift from the others'
