@@ -43,9 +43,14 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
         sharded_[l] = (world_ > 1 || one) && p_->Np[l] % world_ == 0;
         if (sharded_[l]) mx = mx > (size_t)p_->Np[l] * p_->Kp[l] ? mx : (size_t)p_->Np[l] * p_->Kp[l];
     }
-    if (mx && (hpnn_dev_malloc(&send16_, mx * 2) != hipSuccess ||
-               hpnn_dev_malloc(&recv16_, mx * 2 / world_ + 64) != hipSuccess))
-        return -7;
+    /* the BF16 send staging buffer is only for sharded layers whose gradient the 8-phase TN GEMM
+     * cannot write in BF16 itself (split-K, or a shape it does not take): cast from FP32 */
+    size_t mx_cast = 0;
+    for (int l = 0; l < p_->L; l++)
+        if (sharded_[l] && !(p_->S[l] == 1 && hpnn_gemm_tn8_bf16out_ok(p_->Np[l], p_->Kp[l], p_->Bp, p_->Np[l], p_->Kp[l])))
+            mx_cast = mx_cast > (size_t)p_->Np[l] * p_->Kp[l] ? mx_cast : (size_t)p_->Np[l] * p_->Kp[l];
+    if (mx_cast && hpnn_dev_malloc(&send16_, mx_cast * 2) != hipSuccess) return -7;
+    if (mx && hpnn_dev_malloc(&recv16_, mx * 2 / world_ + 64) != hipSuccess) return -7;
     /* one BF16 gradient buffer per sharded layer: the plan's TN GEMM writes it directly (no
      * FP32 round trip and cast), the side stream reduce-scatters it while the next layer's
      * gradient goes into its own buffer */
@@ -75,6 +80,7 @@ int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, i
         const void *src = send16_;
         int r = 0;
         if (p_->g16[l] && p_->g16_used[l]) src = p_->g16[l]; /* the GEMM wrote BF16 already */
+        else if (!send16_) r = -9; /* init judged this layer's gradient to come in BF16 */
         else r = hpnn_cast_f32_bf16(p_->gflat + p_->goff[l], send16_, (long)N * K, side);
         if (!r) r = hpnn_comm_reduce_scatter(c_, src, recv16_, cnt, HPNN_DT_BF16, HPNN_OP_SUM, side);
         if (!r)

@@ -54,6 +54,7 @@ int hpnn_gemm_nt8_splitk_bf16(const void *A, int lda, const void *B, int ldb, vo
  * 8-phase TN kernel's epilogue (no gradient in memory): the step of hpnn_sgd_update with one
  * slab.  N % 256 == 0, M % 256 == 0, Bt % 128 == 0, else -1. */
 /* G = D^T H (one split) rounded to BF16 into G16 [N][ldg] (8-phase kernel); -1: shape not covered */
+int hpnn_gemm_tn8_bf16out_ok(int N, int M, int Bt, int ldd, int ldh);
 int hpnn_gemm_tn8_bf16out(const void *D, int ldd, const void *H, int ldh, void *G16, int ldg, int N, int M, int Bt,
                           hipStream_t stream);
 int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, float *W32, float *V32,
@@ -170,6 +171,10 @@ int hpnn_g0_tile_cols(int M);
  * exchange) refuse grids above it: the first wave of workgroups would spin on partners that
  * cannot be scheduled until the wait times out. */
 int hpnn_resident_capacity(const void *kernel, int threads, size_t dyn_lds);
+/* (Best effort: the count assumes the launch has the device to itself.  Kernels of another
+ * stream or process on the same GPU -- a side-stream collective, ranks sharing one GPU in
+ * tests / rehearsals -- can hold CUs meanwhile; a waiting grid then stretches until they
+ * finish, and a wait that outlives its bound sets the error word read by BPlan::health.) */
 /* *out += order-independent 64-bit digest of the nbytes / 4 words at p (word index offset by
  * base, so several buffers can be folded into one digest); *out must be initialised */
 int hpnn_hash_words(const void *p, long nbytes, long base, unsigned long long *out, hipStream_t stream);

@@ -733,6 +733,12 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* the shape check of hpnn_gemm_tn8_bf16out (without the pointer alignment): 1 when it fits */
+extern "C" int hpnn_gemm_tn8_bf16out_ok(int N, int M, int Bt, int ldd, int ldh) {
+    if (N % 256 || M % 256 || Bt % 128 || ldd % 8 || ldh % 8 || (Bt / 64) % 2) return 0;
+    return (size_t)ldd * 2 * 64 < (1u << 31) && (size_t)ldh * 2 * 64 < (1u << 31);
+}
+
 /* G = D^T H over the whole batch (one split), rounded to BF16 into G16 [N][ldg]: -1 when the
  * shape does not fit the 8-phase kernel */
 extern "C" int hpnn_gemm_tn8_bf16out(const void *D, int ldd, const void *H, int ldh, void *G16, int ldg, int N, int M,

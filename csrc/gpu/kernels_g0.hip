@@ -91,7 +91,7 @@ __device__ __forceinline__ void fm_role(int b, int splits, int tiles, int xcd_ma
     }
 }
 
-template <int WF, int WH, int PD, int KW, bool HU8, int WM = 2, int WN = 2>
+template <int WF, int WH, int PD, int KW, bool HU8, int WM = 2, int WN = 2, bool X16 = false>
 __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nbd, const void *__restrict__ Hg, int nbh,
                                            int ksteps, int splits, int tiles_n, int tiles, int xcd_map, int vb,
                                            f32x4 (&acc)[WF][WH], int &tile, int &split, int &m0, int &n0) {
@@ -123,8 +123,21 @@ __device__ __forceinline__ void fm_partial(const __bf16 *__restrict__ Dg, int nb
     bf16x8 rb[R][WH];
     auto load = [&](int slot_, int t) __attribute__((always_inline)) {
         const int tc = t < nk - 1 ? t : nk - 1; /* clamped: the ring tail re-reads the last step */
+        if constexpr (X16 && HU8) {
+            /* timing ablation (make ABLATIONS=1, HPNN_G0_X16=1; wrong results): fragment pairs
+             * through one 16-byte load per lane instead of two 8-byte loads */
+            typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 #pragma unroll
-        for (int i = 0; i < WF; i++) ra[slot_][i] = *(const HT *)(pa + i * 512 * ES + (size_t)tc * step_a);
+            for (int i = 0; i + 1 < WF; i += 2) {
+                const u32x4 v = *(const u32x4 *)(pa - lane * 8 + lane * 16 + i * 512 + (size_t)tc * step_a);
+                ra[slot_][i] = HT{v.x, v.y};
+                ra[slot_][i + 1] = HT{v.z, v.w};
+            }
+            if constexpr (WF % 2) ra[slot_][WF - 1] = *(const HT *)(pa + (WF - 1) * 512 + (size_t)tc * step_a);
+        } else {
+#pragma unroll
+            for (int i = 0; i < WF; i++) ra[slot_][i] = *(const HT *)(pa + i * 512 * ES + (size_t)tc * step_a);
+        }
 #pragma unroll
         for (int j = 0; j < WH; j++) rb[slot_][j] = *(const bf16x8 *)(pb + j * 512 + (size_t)tc * step_b);
     };
@@ -621,7 +634,7 @@ __device__ __forceinline__ void xcd_group_sum(const float *slab0, size_t mstride
 constexpr int G0TR_BLOCKS = 512, G0TR_MARKS = 8;
 __device__ unsigned long long g_g0_trace[G0TR_BLOCKS][G0TR_MARKS];
 
-template <int WF, int WH, int PD, int KW, bool HU8, bool TRACE = false, int WM = 2, int WN = 2>
+template <int WF, int WH, int PD, int KW, bool HU8, bool TRACE = false, int WM = 2, int WN = 2, bool X16 = false>
 __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf16 *__restrict__ Dg, int nbd,
                                                             const void *__restrict__ Hg, int nbh, float hscale,
                                                             float *__restrict__ slab, int ldg, int N, int ksteps,
@@ -696,7 +709,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
         if (u.xtest) /* self-test of the in-kernel exchange: no GEMM (the role only) */
             fm_role(vb, splits, tiles, xcd_map, tile, split);
         else
-            fm_partial<WF, WH, PD, KW, HU8, WM, WN>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, vb, acc,
+            fm_partial<WF, WH, PD, KW, HU8, WM, WN, X16>(Dg, nbd, Hg, nbh, ksteps, splits, tiles_n, tiles, xcd_map, vb, acc,
                                                     tile, split, m0, n0);
         mark(1);
         const int t = threadIdx.x, lane = t & 63;
@@ -765,16 +778,16 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                 if (G0_PROTO(u, 256)) {
                     /* timing ablation: no publish at all (wrong results) */
                 } else if (xg && xloc_s) { /* the group's leader reads it from this XCD's L2 */
-        #pragma unroll
+#pragma unroll
                     for (int i = 0; i < WF; i++)
-        #pragma unroll
+#pragma unroll
                         for (int j = 0; j < WH; j++)
                             *(f32x4 *)(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q) =
                                 HU8 ? acc[i][j] * hscale : acc[i][j];
                 } else {
-        #pragma unroll
+#pragma unroll
                     for (int i = 0; i < WF; i++)
-        #pragma unroll
+#pragma unroll
                         for (int j = 0; j < WH; j++)
                             st_sc1(out + (size_t)(n0 + j * 16 + r16) * ldg + m0 + i * 16 + 4 * q,
                                    HU8 ? acc[i][j] * hscale : acc[i][j]);
@@ -851,7 +864,7 @@ __global__ __launch_bounds__(64 * WM * WN * KW) void g0_fused_kernel(const __bf1
                 __syncthreads();
                 if (part == 0 && e < e1) {
                     f32x4 g = red[f];
-        #pragma unroll
+#pragma unroll
                     for (int pp = 1; pp < PARTS; pp++) g += red[pp * 128 + f];
                     if (gout)
                         *(f32x4 *)(gout + (size_t)(nt0 + row) * ldg + col) = g;
@@ -1017,7 +1030,9 @@ extern "C" int hpnn_gemm_fm_direct_update(const void *Dg, const void *Hg, int h_
         /* HPNN_G0_PD=2 (ABLATIONS builds, tuning): two k-steps of operands in flight */
 #ifdef HPNN_ABLATIONS
         static const int pd = [] { const char *e = getenv("HPNN_G0_PD"); return e ? atoi(e) : 1; }();
+        static const bool x16 = [] { const char *e = getenv("HPNN_G0_X16"); return e && e[0] == '1'; }();
         if (h_u8 && pd == 2) HPNN_G0F(5, 4, 2, 4, true, false, 1, 2);
+        else if (h_u8 && x16) HPNN_G0F(5, 4, 1, 4, true, false, 1, 2, true);
         else
 #endif
         if (h_u8 && trace) HPNN_G0F(5, 4, 1, 4, true, true, 1, 2);
