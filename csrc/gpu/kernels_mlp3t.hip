@@ -101,7 +101,7 @@ constexpr int TR_BLOCKS = 1024, TR_MARKS = 12;
 __device__ unsigned long long g_tile_trace[TR_BLOCKS][TR_MARKS];
 
 template <int TYPE, bool LABELS, int KS, bool XU8, int D, bool TRACE = false, int ABL = 0, bool EARLY = true,
-          bool TRADE = false, bool XORD = false, int IL = 1>
+          bool TRADE = false, bool XORD = false, int IL = 1, bool CB = false>
 __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__ Xg, float xscale,
                                                             const __bf16 *__restrict__ W0f,
                                                             const __bf16 *__restrict__ W1,
@@ -418,7 +418,11 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             }
         }
         mark(7);
-        wave_lds_fence();
+        /* CB: phase C's barrier (every wave's delta2 in the D2 image) already here, so each wave
+         * runs P4 and phase C back to back (neither writes LDS) instead of waiting for the
+         * slowest wave's P4 */
+        if constexpr (CB) lds_barrier();
+        else wave_lds_fence();
         /* P4: delta1 [sample][h1] = (delta2 W1) * f'(H1) -> HBM, fragment-major:
          * chunk (32-sample row, h1 block) = [g][r][j] = delta1[32 t + 8 g + j][16 hb + r] */
         {
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(512) void mlp3_tile_kernel(const void *__restrict__
             }
         }
         mark(8);
-        lds_barrier();
+        if constexpr (!CB) lds_barrier();
 
         /* ================= phase C: G1, G2 over the tile's 256 samples ================= */
         /* [G1 (H2 x H1) | G2 (NO x H2)] slab.  G1: wave w owns the 2 x 2 output tiles h1 tiles
@@ -585,6 +589,9 @@ int launch_tile(const void *Xg, float xscale, const void *W0f, const void *W1, c
         if (late) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, false>, 512);
         if (trade) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, true>, 512);
         if (xord) return go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, true>, 512);
+        static const bool cb = [] { const char *e = getenv("HPNN_TILE_CB"); return e && e[0] == '1'; }();
+        if (cb) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, 0, true, false, false, 1, true>, 512)
+                             : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, 0, true, false, false, 1, true>, 512);
 #define HPNN_TABL(N_)                                                                                               \
         if (g_tile_abl == N_) return trace ? go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, true, N_>, 512)          \
                                            : go(mlp3_tile_kernel<TYPE, LABELS, KS, XU8, 3, false, N_>, 512);
