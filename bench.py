@@ -349,6 +349,10 @@ def main():
             },
             "train_loss_mean": loss_sum / max(1, samples // world),
         }
+        emu = os.environ.get("HPNN_DPX_EMULATE_WORLD")
+        if emu and dp.sharded:
+            # one rank ran the sharded step at that world's per-rank sizes (timing only)
+            out["config"]["dpx_emulated_world"] = int(emu)
         print(json.dumps(out))
     if dp.active:
         dist.barrier()

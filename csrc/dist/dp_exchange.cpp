@@ -17,6 +17,7 @@ DpExchange::~DpExchange() {
     hpnn_dev_free(grad16_);
     hpnn_dev_free(send16_);
     hpnn_dev_free(recv16_);
+    hpnn_dev_free(emu16_);
 }
 
 int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
@@ -27,6 +28,16 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
     world_ = hpnn_comm_size(comm);
     mode_ = mode == BF16RS ? BF16RS : FP32;
     sharded_.assign(p_->L, false);
+    vw_ = world_;
+    if (const char *e = getenv("HPNN_DPX_EMULATE_WORLD")) {
+        const int w = atoi(e);
+        if (w > 1 && world_ == 1 && mode_ == BF16RS) {
+            vw_ = w;
+            emu_ = true;
+            NN_WARN(stderr, "HPNN_DPX_EMULATE_WORLD=%d: one rank runs the sharded step at %d-rank sizes "
+                            "(timing only, not a training run)\n", w, w);
+        }
+    }
     if (mode_ == FP32) return 0;
     if (p_->mode) {
         NN_ERROR(stderr, "BF16 reduce-scatter exchange needs the per-layer plan (mode %c)\n", p_->mode);
@@ -40,7 +51,7 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
     for (int l = 0; l < p_->L; l++) {
         /* rows split evenly over the ranks (any block height: the transpose runs on the whole
          * all-gathered matrix) */
-        sharded_[l] = (world_ > 1 || one) && p_->Np[l] % world_ == 0;
+        sharded_[l] = (vw_ > 1 || one) && p_->Np[l] % vw_ == 0;
         if (sharded_[l]) mx = mx > (size_t)p_->Np[l] * p_->Kp[l] ? mx : (size_t)p_->Np[l] * p_->Kp[l];
     }
     /* the BF16 send staging buffer is only for sharded layers whose gradient the 8-phase TN GEMM
@@ -50,7 +61,8 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
         if (sharded_[l] && !(p_->S[l] == 1 && hpnn_gemm_tn8_bf16out_ok(p_->Np[l], p_->Kp[l], p_->Bp, p_->Np[l], p_->Kp[l])))
             mx_cast = mx_cast > (size_t)p_->Np[l] * p_->Kp[l] ? mx_cast : (size_t)p_->Np[l] * p_->Kp[l];
     if (mx_cast && hpnn_dev_malloc(&send16_, mx_cast * 2) != hipSuccess) return -7;
-    if (mx && hpnn_dev_malloc(&recv16_, mx * 2 / world_ + 64) != hipSuccess) return -7;
+    if (mx && hpnn_dev_malloc(&recv16_, mx * 2 / vw_ + 64) != hipSuccess) return -7;
+    if (emu_ && mx && hpnn_dev_malloc(&emu16_, mx * 2) != hipSuccess) return -7;
     /* one BF16 gradient buffer per sharded layer: the plan's TN GEMM writes it directly (no
      * FP32 round trip and cast), the side stream reduce-scatters it while the next layer's
      * gradient goes into its own buffer */
@@ -75,7 +87,7 @@ int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, i
         /* on the side stream, after the compute stream's work so far (this gradient) */
         hipStream_t side = hpnn_comm_fork(c_, s);
         if (!side) return -2;
-        const int N = p_->Np[l], K = p_->Kp[l], rp = N / world_;
+        const int N = p_->Np[l], K = p_->Kp[l], rp = N / vw_;
         const long cnt = (long)rp * K, off = (long)rank_ * cnt;
         const void *src = send16_;
         int r = 0;
@@ -86,7 +98,11 @@ int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, i
         if (!r)
             r = hpnn_sgd_update_rows_bf16g(p_->W32[l] + off, p_->V32[l] ? p_->V32[l] + off : nullptr, recv16_, cnt, lr,
                                            alpha, scale, mom, (char *)p_->Wb[l] + off * 2, side);
-        if (!r) r = hpnn_comm_all_gather(c_, (char *)p_->Wb[l] + off * 2, p_->Wb[l], cnt, HPNN_DT_BF16, side);
+        if (!r && emu_) /* the (W-1) / W of the rows a rank receives, as a local copy */
+            r = hipMemcpyAsync(emu16_, (const char *)p_->Wb[l] + cnt * 2, (size_t)(vw_ - 1) * cnt * 2,
+                               hipMemcpyDeviceToDevice, side) == hipSuccess ? 0 : -5;
+        else if (!r)
+            r = hpnn_comm_all_gather(c_, (char *)p_->Wb[l] + off * 2, p_->Wb[l], cnt, HPNN_DT_BF16, side);
         if (!r) r = hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], N, K, side);
         const int rd = hpnn_comm_fork_done(c_);
         return r ? r : rd;
@@ -121,6 +137,7 @@ int DpExchange::gather_masters(hipStream_t s) {
     if (mode_ != BF16RS) return 0;
     for (int l = 0; l < p_->L; l++) {
         if (!sharded_[l]) continue;
+        if (emu_) return 0; /* an emulated run has no other ranks' rows to gather */
         const long cnt = (long)(p_->Np[l] / world_) * p_->Kp[l], off = (long)rank_ * cnt;
         float *bufs[2] = {p_->W32[l], p_->V32[l]};
         for (float *b : bufs) {

@@ -45,6 +45,13 @@ class DpExchange {
     BPlan *p_ = nullptr;
     hpnn_comm *c_ = nullptr;
     int rank_ = 0, world_ = 1;
+    /* shard count: world_, or HPNN_DPX_EMULATE_WORLD on one rank (emu_): that rank runs the
+     * sharded step at that world's per-rank sizes -- 1/W of the rows reduce-scattered and
+     * stepped, the all-gather's receive bytes copied locally -- for timing the per-rank
+     * compute of a W-GPU run on one GPU (timing only: the other rows are never updated) */
+    int vw_ = 1;
+    bool emu_ = false;
+    void *emu16_ = nullptr;
     Mode mode_ = FP32;
     std::vector<bool> sharded_;
     void *send16_ = nullptr, *recv16_ = nullptr;

@@ -425,6 +425,20 @@ bool BPlan::tn_update_ok(int l) const {
 /* from the last layer to the first: gradient + step per layer (the deltas were all computed
  * with the pre-update weights already) */
 int BPlan::grad_and_update_layers(const XIn &x, float lr, float alpha, float scale, hipStream_t s) {
+    /* a two-layer net (RRUFF): layer 1's gradient + step ride in layer 0's fused launch as its
+     * side job (bitwise the separate gemm_tn + update launches; HPNN_TN8_SIDE=0: off) */
+    if (L == 2 && tn8_side && tncnt && g0_fused && S[0] > 1 && !W0f) {
+        hpnn_tn8_side sd = {D[1], H[0], Np[1], Kp[1], slab[1], Np[1], Kp[1], S[1],
+                            W32[1], V32[1], Wb[1], Wt[1], tncnt + 1024 * L + 64};
+        const int r = hpnn_gemm_tn8_fused_update_side(D[0], Np[0], x.x, Kp[0], Np[0], Kp[0], Bp, S[0], slab[0], W32[0],
+                                                      V32[0], Wb[0], Wt[0], lr, alpha, scale, momentum ? 1 : 0, tncnt,
+                                                      tncnt + 1024 * L, &sd, s);
+        if (r == 0) {
+            side_launches++;
+            return 0;
+        }
+        if (r != -1 && r != -2) return r;
+    }
     for (int l = L - 1; l >= 0; l--) {
         const void *Hin = l ? H[l - 1] : x.x;
         if (tn_update_ok(l) && hpnn_gemm_tn8_update(D[l], Np[l], Hin, Kp[l], Np[l], Kp[l], Bp, W32[l], V32[l], Wb[l],

@@ -87,6 +87,9 @@ class BPlan {
     /* the fused G0's XCD-local first reduction level (kernels_g0.hip; HPNN_G0_XCD=1) */
     bool g0_xcd = [] { const char *e = getenv("HPNN_G0_XCD"); return e && e[0] == '1'; }();
     bool tn_update = true; /* the step in the 8-phase TN gradient's epilogue where it applies */
+    /* two-layer nets: layer 1's gradient + step as the side job of layer 0's fused TN launch */
+    bool tn8_side = [] { const char *e = getenv("HPNN_TN8_SIDE"); return !(e && e[0] == '0'); }();
+    long side_launches = 0; /* launches issued with that side job (tests) */
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
 

@@ -65,8 +65,29 @@ int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int ldh, int N, 
 int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, int splits,
                                float *slab, float *W32, float *V32, void *Wbf, void *Wt, float lr, float alpha,
                                float scale, int momentum, unsigned int *cnt, unsigned int *err, hipStream_t stream);
+/* the next layer's weight gradient D^T H (N x M over the same Bt rows, S splits of 64 x 64
+ * pieces into slab [S][N][M], the pieces of gemm_tn_pipe at 64 x 64) and its step (same lr /
+ * alpha / scale / momentum), carried by the fused launch above (kernels_8ph.hip): bitwise the
+ * result of hpnn_gemm_tn_bf16 + hpnn_sgd_update.  cnt: a 64-bit counter zeroed once, used by
+ * this launch shape only. */
+typedef struct {
+    const void *D, *H;
+    int ldd, ldh;
+    float *slab;
+    int N, M, S;
+    float *W32, *V32;
+    void *Wb, *Wt;
+    unsigned int *cnt;
+} hpnn_tn8_side;
+/* hpnn_gemm_tn8_fused_update plus that side job: -1 as above, -2 when the side job does not
+ * fit this grid (its pieces must split evenly over the half-workgroups) */
+int hpnn_gemm_tn8_fused_update_side(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt, int splits,
+                                    float *slab, float *W32, float *V32, void *Wbf, void *Wt, float lr, float alpha,
+                                    float scale, int momentum, unsigned int *cnt, unsigned int *err,
+                                    const hpnn_tn8_side *side, hipStream_t stream);
 void hpnn_gemm_nt_set_8ph(int on);
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
+void hpnn_gemm_nt_set_pp(int on);  /* the pipelined 128 x 128 NT kernel for under-filled grids */
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
                        int M, int N, int K, int epi, int c_f32, hipStream_t stream);
 int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C, int ldc, int M, int N, int K,
@@ -313,6 +334,7 @@ int hpnn_wide2_ksplit(int Bp, int K0);
 long hpnn_wide2_pbuf_bytes(int Bp);
 /* profiling (HPNN_WIDE_TRACE=1): per-workgroup s_memtime stamps [512][12] */
 int hpnn_wide2_trace(unsigned long long *out);
+int hpnn_tn8_trace(unsigned long long *out); /* HPNN_TN8_TRACE=1: [512][8] MODE-2 phase stamps */
 /* ---- FP64 / FP32 batched engine (kernels_fp.hip): f64 selects double, else float ----
  * gemm_fp: C[M x N] (ldc) = sum_k A(m, k) B(n, k) with A(m, k) = A[m*lda + k] (ta = 0) or
  * A[k*lda + m] (ta = 1), B(n, k) = B[n*ldb + k] (tb = 0) or B[k*ldb + n] (tb = 1), on the FP64 /

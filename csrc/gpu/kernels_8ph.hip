@@ -287,6 +287,168 @@ struct Tn8Upd {
 
 constexpr unsigned long long TN8_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~10 s) */
 
+/* MODE 2 side job (hpnn_gemm_tn8_fused_update_side): the NEXT layer's weight gradient
+ * G1 = D^T H of a two-layer net (RRUFF: 230 x 230 over the batch) and its step, carried
+ * by the layer-0 launch instead of a gradient launch + an update launch of their own.
+ * The gradient is cut exactly as gemm_tn_pipe_kernel<64, 64, 32, ...> (kernels_mfma.hip)
+ * cuts it for the separate path: 64 x 64 tiles x S splits of units / S 64-row units; each
+ * piece runs on one half of a workgroup (waves 0-3 / 4-7, an LDS ring each) with that
+ * kernel's staging, fragment reads and MFMA order, so the partial slabs are bitwise the
+ * separate launch's.  The pieces run before the layer-0 GEMM and are published
+ * write-through; one ticket per workgroup; each workgroup then reduces 1 / grid of G1 over
+ * the S slabs in the summation order of sgd_tile (kernels_misc.hip) and applies the step,
+ * while it waits for the other splits of its own layer-0 tile. */
+struct Tn8Side {
+    const __bf16 *D, *H;
+    float *slab; /* [S][N][M] */
+    float *W32, *V32;
+    __bf16 *Wb, *Wt;
+    unsigned int *cnt; /* 64-bit arrival counter (one ticket per workgroup per launch) */
+    int ldd, ldh, N, M, units, S, tiles_n, tiles, jobs, on;
+};
+
+/* 64-row stages (16 KiB per half: 64 H + 64 D columns), a 5-stage ring per half -- all
+ * 160 KiB of the CU's LDS for MODE 2 -- and ONE barrier per stage: the pieces are bound by
+ * their per-stage overhead (32-row stages with two barriers each: 25.9K ticks for a
+ * workgroup's pieces, raw_s6_tr1) */
+constexpr int SJ_BKR = 64, SJ_ST = 5, SJ_STAGE = SJ_BKR * 128 * 2, SJ_LPS = 4;
+constexpr int TN8_LDS2 = 2 * SJ_ST * SJ_STAGE; /* MODE 2's LDS */
+static_assert(TN8_LDS2 >= 2 * KBUF && TN8_LDS2 <= 160 * 1024, "side-job rings fit the CU's LDS");
+
+__device__ __forceinline__ void sj_wait(int rem) { /* SJ_LPS LDS-DMA loads per wave per stage */
+    static_assert(SJ_ST <= 5 && SJ_LPS == 4, "counted waits below");
+    if (rem >= 4) vm_wait<16>();
+    else if (rem == 3) vm_wait<12>();
+    else if (rem == 2) vm_wait<8>();
+    else if (rem == 1) vm_wait<4>();
+    else vm_wait<0>();
+}
+
+/* the pieces first, first + step, ... < end of this half (w4: wave within the half); every
+ * half of the grid runs the same number of pieces of the same length (host-checked), so the
+ * halves meet the workgroup barriers in step.  Staging pieces and fragment reads are those of
+ * gemm_tn_pipe_kernel<64, 64, 64, ...> and the MFMAs run in the same k order as its 32-row form:
+ * the same partial sums bit for bit. */
+__device__ __forceinline__ void side_jobs(const Tn8Side &s, char *ring, int w4, int lane, int first, int step,
+                                          int end) {
+    const int wm = w4 >> 1, wn = w4 & 1, r16 = lane & 15, q = lane >> 4;
+    const int upj = s.units / s.S, KT = upj * (64 / SJ_BKR);
+    const size_t ldh_b = (size_t)s.ldh * 2, ldd_b = (size_t)s.ldd * 2;
+    for (int j = first; j < end; j += step) {
+        const int tile = j % s.tiles, split = j / s.tiles;
+        const int m0 = (tile / s.tiles_n) * 64, n0 = (tile % s.tiles_n) * 64;
+        const size_t b0 = (size_t)split * upj * 64;
+        const char *Hg = (const char *)(s.H + b0 * s.ldh + m0);
+        const char *Dg = (const char *)(s.D + b0 * s.ldd + n0);
+        auto issue = [&](int kt) __attribute__((always_inline)) {
+            char *sh = ring + (kt % SJ_ST) * SJ_STAGE, *sd = sh + SJ_BKR * 64 * 2;
+            const char *gh = Hg + (size_t)kt * SJ_BKR * ldh_b, *gd = Dg + (size_t)kt * SJ_BKR * ldd_b;
+#pragma unroll
+            for (int i = 0; i < SJ_LPS; i++) { /* pieces 0-7 H, 8-15 D */
+                const int c = w4 + 4 * i;
+                if (c < 8) hpnn::glds_t32_piece<SJ_BKR>(gh, ldh_b, sh, c, lane);
+                else hpnn::glds_t32_piece<SJ_BKR>(gd, ldd_b, sd, c - 8, lane);
+            }
+        };
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int jj = 0; jj < 2; jj++) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < SJ_ST - 1; st++)
+            if (st < KT) issue(st);
+        for (int kt = 0; kt < KT; kt++) {
+            sj_wait((kt + SJ_ST - 2 < KT - 1 ? kt + SJ_ST - 2 : KT - 1) - kt);
+            /* stage kt landed everywhere; every wave's reads of stage kt - 1 retired (its MFMAs
+             * consumed them), so its slot can be refilled */
+            __builtin_amdgcn_s_barrier();
+            if (kt + SJ_ST - 1 < KT) issue(kt + SJ_ST - 1);
+            const char *sh = ring + (kt % SJ_ST) * SJ_STAGE, *sd = sh + SJ_BKR * 64 * 2;
+#pragma unroll
+            for (int kk = 0; kk < SJ_BKR / 32; kk++) {
+                bf16x8 fh[2], fd[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) fh[i] = hpnn::frag_tr<SJ_BKR>(sh, kk * 32, wm * 32 + i * 16, lane);
+#pragma unroll
+                for (int jj = 0; jj < 2; jj++) fd[jj] = hpnn::frag_tr<SJ_BKR>(sd, kk * 32, wn * 32 + jj * 16, lane);
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int jj = 0; jj < 2; jj++)
+                        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], fd[jj], acc[i][jj], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier(); /* the ring is free for the next piece */
+        float *out = s.slab + (size_t)split * s.N * s.M;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int jj = 0; jj < 2; jj++)
+                hpnn::st_sc1(out + (size_t)(n0 + wn * 32 + jj * 16 + r16) * s.M + m0 + wm * 32 + i * 16 + 4 * q,
+                             acc[i][jj]);
+        /* the stores count in vmcnt: drain them before the next piece's counted waits */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+/* workgroup b's share of G1 (E4 / G float4s): the S partial slabs summed in sgd_tile's order
+ * (slab 0; slabs 1.. in four interleaved chains while four remain; the rest into chain 0;
+ * chain 0 + ((1 + 2) + 3)), then the step of hpnn_sgd_update */
+__device__ __forceinline__ void side_reduce_step(const Tn8Side &s, const Tn8Upd &u, int b, int G) {
+    const int E4 = s.N * s.M / 4, per = (E4 + G - 1) / G, m4 = s.M / 4;
+    const int e0 = b * per, e1 = min(E4, e0 + per);
+    const size_t ss = (size_t)s.N * s.M;
+    const int gend = 1 + 4 * ((s.S - 1) / 4);
+    for (int e = e0 + (int)threadIdx.x; e < e1; e += (int)blockDim.x) {
+        const int n = e / m4, m = 4 * (e % m4);
+        const size_t idx = (size_t)n * s.M + m;
+        f32x4 ww = *(const f32x4 *)(s.W32 + idx), vv = {0.f, 0.f, 0.f, 0.f}; /* under the slab loads */
+        if (u.momentum) vv = *(const f32x4 *)(s.V32 + idx);
+        f32x4 g = {0.f, 0.f, 0.f, 0.f}, g1 = g, g2 = g, g3 = g;
+        for (int s0 = 0; s0 < s.S; s0 += 16) {
+            f32x4 v[16];
+            const float *p[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) p[j] = s.slab + (size_t)(s0 + j < s.S ? s0 + j : s0) * ss + idx;
+            hpnn::ld_sc1_x16(v, p);
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int k = s0 + j, c = (k - 1) & 3;
+                const f32x4 x = v[j];
+                if (k < s.S) {
+                    if (k == 0) g = x;
+                    else if (k >= gend || c == 0) g += x;
+                    else if (c == 1) g1 += x;
+                    else if (c == 2) g2 += x;
+                    else g3 += x;
+                }
+            }
+        }
+        g += (g1 + g2) + g3;
+        if (u.momentum) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                vv[r] += u.lr * (g[r] * u.scale);
+                ww[r] += vv[r];
+                vv[r] *= u.alpha;
+            }
+            *(f32x4 *)(s.V32 + idx) = vv;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) ww[r] += u.lr * (g[r] * u.scale);
+        }
+        *(f32x4 *)(s.W32 + idx) = ww;
+        bf16x4 wb;
+#pragma unroll
+        for (int r = 0; r < 4; r++) wb[r] = (__bf16)ww[r];
+        *(bf16x4 *)(s.Wb + idx) = wb;
+#pragma unroll
+        for (int r = 0; r < 4; r++) s.Wt[(size_t)(m + r) * s.N + n] = wb[r];
+    }
+}
+
 /* MODE 0: split-K slabs; 3: one split, the product rounded to BF16 into upd.Wb [N][ldg] (the
  * data-parallel exchange's send buffer: no FP32 gradient round trip); 1: one split, the
  * optimizer step in the epilogue; 2: several splits,
@@ -294,17 +456,25 @@ constexpr unsigned long long TN8_TIMEOUT = 1000000000ULL; /* wall-clock ticks (~
  * of the tile has arrived -- reduces 1/splits of the tile over the splits in a fixed order
  * and applies the step there (the split-K reduction and the update launch of the RRUFF-shaped
  * first layer move into this launch; the protocol of kernels_g0.hip g0_fused_kernel) */
-template <int MODE>
+/* HPNN_TN8_TRACE=1 (profiling only, MODE 2): s_memtime of every workgroup's thread 0 at the
+ * phase boundaries, [block][mark]; read back with hpnn_tn8_trace */
+constexpr int TN8_TR_BLOCKS = 512, TN8_TR_MARKS = 8;
+__device__ unsigned long long g_tn8_trace[TN8_TR_BLOCKS][TN8_TR_MARKS];
+
+/* TM: output-tile width along H (256, or 128 for MODE 2: 256 x 128 tiles -- twice the tiles at
+ * half the splits for the same grid, so half the split-K partial bytes; the waves of M-half wm
+ * then own H columns 64 wm.. of the one H half-tile, and an iteration has 4 phases) */
+template <int MODE, bool TRACE = false, int TM = 256>
 __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict__ D, int ldd,
                                                        const __bf16 *__restrict__ H, int ldh,
                                                        float *__restrict__ slab, int ldg, int N, int units,
                                                        int splits, int tiles_n, int ntiles, hpnn::TnTail tail,
-                                                       Tn8Upd upd) {
+                                                       Tn8Upd upd, Tn8Side side) {
     if ((int)blockIdx.x >= ntiles * splits) {
         if (threadIdx.x < 256) hpnn::tn_tail_reduce(tail, (int)blockIdx.x - ntiles * splits);
         return;
     }
-    __shared__ __attribute__((aligned(16))) char lds[2 * KBUF];
+    __shared__ __attribute__((aligned(16))) char lds[MODE == 2 ? TN8_LDS2 : 2 * KBUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -314,16 +484,44 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
         tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
         split = 0;
     } else {
-        tile = blockIdx.x % ntiles;
-        split = blockIdx.x / ntiles;
+        /* XCD-aware, bijective (as gemm_nt8_kernel): each XCD takes a contiguous run of
+         * split-major work items, i.e. whole K slices for every tile, so a slice of D (shared
+         * by all tiles) is fetched into one XCD's L2 once instead of into every XCD's */
+        const int total = ntiles * splits, bid = blockIdx.x, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
+        const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        tile = w % ntiles;
+        split = w / ntiles;
     }
+    static_assert(TM == 256 || (TM == 128 && MODE == 2), "tile width");
     const int tn = tile % tiles_n, tm = tile / tiles_n;
-    const int m0 = tm * 256, n0 = tn * 256;
+    const int m0 = tm * TM, n0 = tn * 256;
     const int u0 = (int)((long)split * units / splits), u1 = (int)((long)(split + 1) * units / splits);
     const int KT = u1 - u0; /* 64-row K-tiles, even */
     const size_t ldh_b = (size_t)ldh * 2, ldd_b = (size_t)ldd * 2;
     const char *Hg = (const char *)(H + (size_t)u0 * 64 * ldh + m0);
     const char *Dg = (const char *)(D + (size_t)u0 * 64 * ldd + n0);
+
+    auto mark = [&](int i) __attribute__((always_inline)) {
+        if constexpr (TRACE) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (tid == 0 && blockIdx.x < TN8_TR_BLOCKS) g_tn8_trace[blockIdx.x][i] = t;
+        }
+    };
+    mark(0);
+    unsigned long long want1 = 0; /* the side job's arrival target (thread 0) */
+    if constexpr (MODE == 2) {
+        if (side.on) {
+            const int G = ntiles * splits, bid = blockIdx.x;
+            /* the XCD's workgroups take a contiguous, split-major run of pieces (whole K slices
+             * of D and H into that XCD's L2 once); host-checked G % 8 == 0 */
+            const int per = side.jobs / 8, x0 = (bid & 7) * per;
+            side_jobs(side, lds + (wave >> 2) * (SJ_ST * SJ_STAGE), wave & 3, lane, x0 + 2 * (bid >> 3) + (wave >> 2),
+                      2 * (G / 8), x0 + per);
+            __syncthreads(); /* every piece published; the rings are free for the GEMM */
+            if (tid == 0) want1 = hpnn::ticket_arrive(side.cnt, (unsigned)G);
+        }
+    }
+    mark(1);
 
     unsigned int voh[2], vod[2];
     int dsto[2];
@@ -377,11 +575,13 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
     };
     bf16x8 rh[4][2], rd0[2][2], rd1[2][2];
     auto read_h = [&](const char *buf, int mi) __attribute__((always_inline)) {
-        const char *img = buf + wm * HALF;
+        /* TM 128: one H half-tile, M-half wm owns its columns 64 wm.. (mi unused) */
+        const char *img = buf + (TM == 256 ? wm * HALF : 0);
+        const int c0 = TM == 256 ? mi * 64 : wm * 64;
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int kk = 0; kk < 2; kk++) rh[i][kk] = ftr(img, kk * 32, mi * 64 + i * 16);
+            for (int kk = 0; kk < 2; kk++) rh[i][kk] = ftr(img, kk * 32, c0 + i * 16);
     };
     auto read_d = [&](const char *buf, int ni, bf16x8 (&rd)[2][2]) __attribute__((always_inline)) {
         const char *img = buf + (2 + (wn >> 1)) * HALF;
@@ -410,7 +610,7 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 
     /* the schedule of gemm_nt8_kernel with H in the role of A and D in that of B */
     stage(0, 0);
-    stage(1, 0);
+    if constexpr (TM == 256) stage(1, 0);
     stage(2, 0);
     stage(3, 0);
     stage(2, 1);
@@ -419,6 +619,47 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
     __builtin_amdgcn_s_barrier();
     if (wm == 1) __builtin_amdgcn_s_barrier();
 
+    if constexpr (TM == 128) {
+        /* 4 phases per 2 K-tiles, quadrants (0,0) (0,1) of the one M-quadrant; H(o) is restaged
+         * at the top (its O slot was last read two phases before the previous iteration's
+         * end), D(e+2) after the even phases, H(e+2) once the odd H is read, D(o+2) last; the
+         * counted waits leave only the D pieces just issued in flight */
+        for (int e = 0; e < KT; e += 2) {
+            const int o = e + 1;
+            const bool ne = e + 2 < KT, no = o + 2 < KT;
+            const char *bE = lds + (e & 1) * KBUF, *bO = lds + (o & 1) * KBUF;
+            read_h(bE, 0);
+            read_d(bE, 0, rd0);
+            stage(0, o);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(0, 0, rd0);
+            read_d(bE, 1, rd1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(0, 1, rd1);
+            if (ne) {
+                stage(2, e + 2);
+                stage(3, e + 2);
+                vm_wait<4>();
+            } else {
+                vm_wait<0>();
+            }
+            read_h(bO, 0);
+            read_d(bO, 0, rd0);
+            if (ne) stage(0, e + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(0, 0, rd0);
+            read_d(bO, 1, rd1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(0, 1, rd1);
+            if (no) {
+                stage(2, o + 2);
+                stage(3, o + 2);
+                vm_wait<4>();
+            } else {
+                vm_wait<0>();
+            }
+        }
+    } else
     for (int e = 0; e < KT; e += 2) {
         const int o = e + 1;
         const bool ne = e + 2 < KT, no = o + 2 < KT;
@@ -469,12 +710,13 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
         mma(1, 0, rd0);
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
+    mark(2);
 
     float *out = slab + (size_t)split * N * ldg;
     const int r16 = lane & 15, q = lane >> 4;
     if constexpr (MODE == 2) {
 #pragma unroll
-        for (int mi = 0; mi < 2; mi++)
+        for (int mi = 0; mi < TM / 128; mi++)
 #pragma unroll
             for (int ni = 0; ni < 2; ni++)
 #pragma unroll
@@ -482,28 +724,54 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 #pragma unroll
                     for (int j = 0; j < 2; j++) {
                         const int n = n0 + wn * 64 + ni * 32 + j * 16 + r16;
-                        const int m = m0 + wm * 128 + mi * 64 + i * 16 + 4 * q;
+                        const int m = m0 + wm * (TM / 2) + mi * 64 + i * 16 + 4 * q;
                         hpnn::st_sc1(out + (size_t)n * ldg + m, acc[mi][ni][i][j]);
                     }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) { /* 64-bit tickets (mfma_common.h): no wrap */
-            const unsigned long long want = hpnn::ticket_arrive(upd.cnt + 32 * tile, (unsigned)splits);
-            hpnn::ticket_wait(upd.cnt + 32 * tile, want, upd.err, TN8_TIMEOUT);
+        /* 64-bit tickets (mfma_common.h): no wrap */
+        unsigned long long want = 0;
+        if (tid == 0) want = hpnn::ticket_arrive(upd.cnt + 32 * tile, (unsigned)splits);
+        mark(3);
+        if (side.on) { /* G1's share while the tile's other splits finish */
+            if (tid == 0) hpnn::ticket_wait(side.cnt, want1, upd.err, TN8_TIMEOUT);
+            __syncthreads();
+            mark(4);
+            side_reduce_step(side, upd, (int)blockIdx.x, ntiles * splits);
         }
+        mark(5);
+        if (tid == 0) hpnn::ticket_wait(upd.cnt + 32 * tile, want, upd.err, TN8_TIMEOUT);
         __syncthreads();
-        constexpr int NE4 = 256 * 256 / 4;
+        mark(6);
+        constexpr int NE4 = 256 * TM / 4, R4 = TM / 4;
         const int e0 = (int)((long)split * NE4 / splits), e1 = (int)((long)(split + 1) * NE4 / splits);
         const size_t ss = (size_t)N * ldg;
         for (int e = e0 + tid; e < e1; e += 512) {
-            const int n = n0 + e / 64, m = m0 + 4 * (e % 64);
+            const int n = n0 + e / R4, m = m0 + 4 * (e % R4);
             const float *p = slab + (size_t)n * ldg + m;
-            f32x4 g = {0.f, 0.f, 0.f, 0.f};
-            for (int s0 = 0; s0 < splits; s0 += 8) g += hpnn::sum_sc1_x8(p + (size_t)s0 * ss, ss, splits - s0);
             const size_t idx = (size_t)n * ldg + m;
-            f32x4 ww = *(const f32x4 *)(upd.W32 + idx);
+            /* the step's operands first, then every split's partial in ONE batch of 16 loads
+             * (one memory round trip per element instead of three) */
+            f32x4 ww = *(const f32x4 *)(upd.W32 + idx), vv = {0.f, 0.f, 0.f, 0.f};
+            if (upd.momentum) vv = *(const f32x4 *)(upd.V32 + idx);
+            f32x4 g = {0.f, 0.f, 0.f, 0.f};
+            for (int s0 = 0; s0 < splits; s0 += 16) {
+                f32x4 v[16];
+                const float *q[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) q[j] = p + (size_t)(s0 + j < splits ? s0 + j : s0) * ss;
+                hpnn::ld_sc1_x16(v, q);
+#pragma unroll
+                for (int h = 0; h < 2; h++) /* groups of 8 summed first: the order of sum_sc1_x8 */
+                    if (s0 + 8 * h < splits) {
+                        f32x4 t = v[8 * h];
+#pragma unroll
+                        for (int j = 1; j < 8; j++)
+                            if (s0 + 8 * h + j < splits) t += v[8 * h + j];
+                        g += t;
+                    }
+            }
             if (upd.momentum) {
-                f32x4 vv = *(const f32x4 *)(upd.V32 + idx);
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     vv[r] += upd.lr * (g[r] * upd.scale);
@@ -523,6 +791,7 @@ __global__ __launch_bounds__(512) void gemm_tn8_kernel(const __bf16 *__restrict_
 #pragma unroll
             for (int r = 0; r < 4; r++) upd.Wt[(size_t)(m + r) * N + n] = wb[r];
         }
+        mark(7);
     } else if constexpr (MODE == 1) {
         /* W [N][ldg]: W32 / V32 / Wb row-major, Wt [ldg][N].  Per quadrant: all loads
          * first (8 fragments in flight), then the step, then the stores -- a load / use /
@@ -729,7 +998,7 @@ int hpnn_gemm_tn8_launch(const void *D, int ldd, const void *H, int ldh, float *
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
     hipLaunchKernelGGL(gemm_tn8_kernel<0>, dim3(ntiles * splits + tail.blocks), dim3(512), 0, stream,
                        (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, ldg, N, units, splits, tiles_n, ntiles,
-                       tail, Tn8Upd{});
+                       tail, Tn8Upd{}, Tn8Side{});
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -751,7 +1020,7 @@ extern "C" int hpnn_gemm_tn8_bf16out(const void *D, int ldd, const void *H, int 
     Tn8Upd u{};
     u.Wb = (__bf16 *)G16;
     hipLaunchKernelGGL(gemm_tn8_kernel<3>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
-                       (const __bf16 *)H, ldh, nullptr, ldg, N, units, 1, tiles_n, ntiles, hpnn::TnTail{}, u);
+                       (const __bf16 *)H, ldh, nullptr, ldg, N, units, 1, tiles_n, ntiles, hpnn::TnTail{}, u, Tn8Side{});
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -770,7 +1039,7 @@ extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int l
     const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
     const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, nullptr, nullptr};
     hipLaunchKernelGGL(gemm_tn8_kernel<1>, dim3(ntiles), dim3(512), 0, stream, (const __bf16 *)D, ldd,
-                       (const __bf16 *)H, ldh, nullptr, M, N, Bt / 64, 1, tiles_n, ntiles, hpnn::TnTail{}, u);
+                       (const __bf16 *)H, ldh, nullptr, M, N, Bt / 64, 1, tiles_n, ntiles, hpnn::TnTail{}, u, Tn8Side{});
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -778,10 +1047,10 @@ extern "C" int hpnn_gemm_tn8_update(const void *D, int ldd, const void *H, int l
  * (MODE 2 above): slab is the scratch the partials are published through ([splits][N][M]).
  * -1: shape not covered, or more workgroups than the device holds at once (every split of a
  * tile waits for the others: hpnn_resident_capacity), or HPNN_TN8_FUSED=0. */
-extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt,
-                                          int splits, float *slab, float *W32, float *V32, void *Wbf, void *Wt,
-                                          float lr, float alpha, float scale, int momentum, unsigned int *cnt,
-                                          unsigned int *err, hipStream_t stream) {
+extern "C" int hpnn_gemm_tn8_fused_update_side(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt,
+                                               int splits, float *slab, float *W32, float *V32, void *Wbf, void *Wt,
+                                               float lr, float alpha, float scale, int momentum, unsigned int *cnt,
+                                               unsigned int *err, const hpnn_tn8_side *sd, hipStream_t stream) {
     static const bool on = [] { const char *e = getenv("HPNN_TN8_FUSED"); return !(e && e[0] == '0'); }();
     /* every split of a tile waits for the others: the whole grid must be resident at once */
     static const int cap = hpnn_resident_capacity((const void *)gemm_tn8_kernel<2>, 512, 0);
@@ -797,16 +1066,53 @@ extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H,
     if ((size_t)ldd * 2 * 64 >= (1u << 31) || (size_t)ldh * 2 * 64 >= (1u << 31)) return -1;
     const int units = Bt / 64;
     if (units % splits || (units / splits) % 2) return -1;
-    const int tiles_n = N / 256, ntiles = tiles_n * (M / 256);
-    /* 64-bit tickets: 32 words apart in 1024 (a block the caller keeps for this GEMM shape: the
+    /* 256 x 128 tiles at half the splits (HPNN_TN8_TM=128; same grid, half the partial bytes) */
+    static const int tm_req = [] { const char *e = getenv("HPNN_TN8_TM"); return e ? atoi(e) : 256; }();
+    const bool t128 = tm_req == 128 && splits % 2 == 0 && (units / (splits / 2)) % 2 == 0;
+    if (t128) splits /= 2;
+    const int TMv = t128 ? 128 : 256;
+    if (M % TMv) return -1;
+    const int tiles_n = N / 256, ntiles = tiles_n * (M / TMv);
+    /* 64-bit tickets: 32 words apart in 1024, up to 32 tiles (a block the caller keeps for this GEMM shape: the
      * counters are monotonic, every launch must add `splits` per tile); at least min_wg workgroups (HPNN_TN8_MINWG, default
      * half the CUs: fewer splits leave the chip idle while each reduces a larger share) */
     static const int min_wg = [] { const char *e = getenv("HPNN_TN8_MINWG"); return e ? atoi(e) : 0; }();
-    if (ntiles > 31 || ntiles * splits > cap || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;
+    if (ntiles > 32 || ntiles * splits > cap || ntiles * splits < (min_wg > 0 ? min_wg : cus / 2)) return -1;
     const Tn8Upd u{W32, V32, (__bf16 *)Wbf, (__bf16 *)Wt, lr, alpha, scale, momentum, cnt, err};
-    hipLaunchKernelGGL(gemm_tn8_kernel<2>, dim3(ntiles * splits), dim3(512), 0, stream, (const __bf16 *)D, ldd,
-                       (const __bf16 *)H, ldh, slab, M, N, units, splits, tiles_n, ntiles, hpnn::TnTail{}, u);
+    Tn8Side side{};
+    if (sd) { /* the next layer's gradient + step as the side job: -2 when it does not fit */
+        const int G = ntiles * splits, su = Bt / 64;
+        if (!sd->D || !sd->H || !sd->slab || !sd->W32 || !sd->Wb || !sd->Wt || !sd->cnt || (momentum && !sd->V32))
+            return -2;
+        if (sd->N % 64 || sd->M % 64 || sd->S < 1 || su % sd->S || sd->ldd % 8 || sd->ldh % 8) return -2;
+        if (((uintptr_t)sd->W32 | (uintptr_t)(momentum ? sd->V32 : sd->W32) | (uintptr_t)sd->slab | (uintptr_t)sd->Wb) &
+            15)
+            return -2;
+        const int tiles = (sd->N / 64) * (sd->M / 64), jobs = tiles * sd->S;
+        /* every half-workgroup must run the same number of pieces (they share the barriers) */
+        if (G % 8 || jobs % (2 * G)) return -2;
+        side = Tn8Side{(const __bf16 *)sd->D, (const __bf16 *)sd->H, sd->slab, sd->W32, sd->V32, (__bf16 *)sd->Wb,
+                       (__bf16 *)sd->Wt, sd->cnt, sd->ldd, sd->ldh, sd->N, sd->M, su, sd->S, sd->N / 64, tiles, jobs, 1};
+    }
+    static const bool trace = [] { const char *e = getenv("HPNN_TN8_TRACE"); return e && e[0] == '1'; }();
+    auto kern = t128 ? (trace ? gemm_tn8_kernel<2, true, 128> : gemm_tn8_kernel<2, false, 128>)
+                     : (trace ? gemm_tn8_kernel<2, true> : gemm_tn8_kernel<2, false>);
+    hipLaunchKernelGGL(kern, dim3(ntiles * splits), dim3(512), 0, stream, (const __bf16 *)D, ldd, (const __bf16 *)H, ldh, slab, M, N, units, splits, tiles_n,
+                       ntiles, hpnn::TnTail{}, u, side);
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* HPNN_TN8_TRACE=1 stamps: out[512][8] shader-clock ticks (thread 0 of each workgroup) */
+extern "C" int hpnn_tn8_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tn8_trace), sizeof(g_tn8_trace)) == hipSuccess ? 0 : -5;
+}
+
+extern "C" int hpnn_gemm_tn8_fused_update(const void *D, int ldd, const void *H, int ldh, int N, int M, int Bt,
+                                          int splits, float *slab, float *W32, float *V32, void *Wbf, void *Wt,
+                                          float lr, float alpha, float scale, int momentum, unsigned int *cnt,
+                                          unsigned int *err, hipStream_t stream) {
+    return hpnn_gemm_tn8_fused_update_side(D, ldd, H, ldh, N, M, Bt, splits, slab, W32, V32, Wbf, Wt, lr, alpha, scale,
+                                           momentum, cnt, err, nullptr, stream);
 }
 
 /* split-K form for GEMMs with too few 256x256 tiles to fill the chip (the RRUFF-shaped

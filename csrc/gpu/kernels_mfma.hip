@@ -209,6 +209,131 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_pipe_kernel(const __bf16
     }
 }
 
+/* 128 x 128 NT tiles for grids of about one tile per CU (the 8 x 4096 net at its 8-GPU shard,
+ * M = 1024: 256 tiles), software-pipelined: gemm_nt_pipe_kernel<128, 128, 64, 2, 4, ...>
+ * passes two barriers per 64-wide K-step and reads a step's fragments only after its
+ * barrier, so every wave idles through the LDS read latency twice per step.  Here the
+ * fragments of each 32-wide half-step go to their own register set, read while the MFMAs of
+ * the other set run:
+ *     [top of step kt]  issue stage kt + ST - 1 (the slot of kt - 1: every wave is past it)
+ *                       read (kt, k32 1) -> R1;  16 MFMAs on R0 = (kt, k32 0)
+ *                       counted vmcnt for stage kt + 1; lgkmcnt(0); ONE barrier
+ *                       read (kt + 1, k32 0) -> R0;  16 MFMAs on R1
+ * Same MFMA order per accumulator as gemm_nt_pipe_kernel: bitwise the same products. */
+template <int EPI, bool CF32, int ST>
+__global__ __launch_bounds__(512) void gemm_nt_pp_kernel(const __bf16 *__restrict__ A, int lda,
+                                                         const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
+                                                         int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
+                                                         int tiles_n) {
+    constexpr int BM = 128, BN = 128, BK = 64, WN = 4, CPR = 8, RB = BK * 2;
+    constexpr int A_PIECES = BM / 8, PIECES = A_PIECES + BN / 8, LPS = PIECES / 8; /* 4 per wave */
+    constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
+    static_assert(ST >= 2 && ST * STAGE <= 160 * 1024 && LPS * (ST - 1) < 64, "ring");
+    __shared__ __attribute__((aligned(16))) char lds[ST * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN; /* wave tile 64 x 32 */
+    const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int KT = K / BK;
+    const char *Ag = (const char *)(A + (size_t)m0 * lda);
+    const char *Bg = (const char *)(B + (size_t)n0 * ldb);
+    const size_t lda_b = (size_t)lda * 2, ldb_b = (size_t)ldb * 2;
+    const int r16 = lane & 15, q = lane >> 4;
+
+    auto issue = [&](int kt) __attribute__((always_inline)) {
+        char *sa = lds + (kt % ST) * STAGE, *sb = sa + A_BYTES;
+        const char *ga = Ag + (size_t)kt * RB, *gb = Bg + (size_t)kt * RB;
+#pragma unroll
+        for (int i = 0; i < LPS; i++) {
+            const int c = wave + 8 * i; /* wave-uniform: pieces 0-15 A, 16-31 B */
+            if (c < A_PIECES) glds_piece<BK>(ga, lda_b, sa + c * 1024, c * 8, lane);
+            else glds_piece<BK>(gb, ldb_b, sb + (c - A_PIECES) * 1024, (c - A_PIECES) * 8, lane);
+        }
+    };
+    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+    auto read = [&](int kt, int kk, bf16x8 (&fa)[4], bf16x8 (&fb)[2]) __attribute__((always_inline)) {
+        const char *sa = lds + (kt % ST) * STAGE, *sb = sa + A_BYTES;
+        const int ch = kk * 4 + q;
+#pragma unroll
+        for (int j = 0; j < 4; j++) fa[j] = *(const bf16x8 *)(sa + nt_off<CPR>(wm * 64 + j * 16 + r16, ch));
+#pragma unroll
+        for (int i = 0; i < 2; i++) fb[i] = *(const bf16x8 *)(sb + nt_off<CPR>(wn * 32 + i * 16 + r16, ch));
+    };
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    /* EPI_DACT: the epilogue's f'(h) operand loaded now, under the main loop (16 VGPRs): read at
+     * the end, its 8 strided loads per lane cost every workgroup ~15 us at M = 1024 */
+    bf16x4 hv[2][4];
+    if constexpr (EPI == HPNN_EPI_DACT) {
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                hv[i][j] = *(const bf16x4 *)(aux + (size_t)(m0 + wm * 64 + j * 16 + r16) * ldaux + n0 + wn * 32 +
+                                             i * 16 + 4 * q);
+    }
+    auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    };
+
+#pragma unroll
+    for (int st = 0; st < ST - 1; st++)
+        if (st < KT) issue(st);
+    wait_stage<LPS, ST>((ST - 2 < KT - 1 ? ST - 2 : KT - 1));
+    __builtin_amdgcn_s_barrier();
+    read(0, 0, fa0, fb0);
+    for (int kt = 0; kt < KT; kt++) {
+        const int nxt = kt + ST - 1;
+        if (nxt < KT) issue(nxt);
+        read(kt, 1, fa1, fb1);
+        mma(fa0, fb0);
+        if (kt + 1 < KT) {
+            const int last = nxt < KT ? nxt : KT - 1;
+            wait_stage<LPS, ST>(last - (kt + 1));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            read(kt + 1, 0, fa0, fb0);
+        }
+        mma(fa1, fb1);
+    }
+
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int b = m0 + wm * 64 + j * 16 + r16;
+            const int f = n0 + wn * 32 + i * 16 + 4 * q;
+            f32x4 v = acc[i][j];
+            if constexpr (EPI == HPNN_EPI_ACT) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[r] = bipolar(v[r]);
+            } else if constexpr (EPI == HPNN_EPI_DACT) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float y = (float)hv[i][j][r];
+                    v[r] *= -0.5f * (y * y - 1.0f);
+                }
+            }
+            if constexpr (CF32) {
+                *(f32x4 *)((float *)C + (size_t)b * ldc + f) = v;
+            } else {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[r] = (__bf16)v[r];
+                *(bf16x4 *)((__bf16 *)C + (size_t)b * ldc + f) = o;
+            }
+        }
+    }
+}
+
 /* ---------------------------------------------------------------------- */
 /* TN GEMM (weight gradient)                                               */
 /* ---------------------------------------------------------------------- */
@@ -367,6 +492,8 @@ int launch_nt_big(const void *A, int lda, const void *B, int ldb, void *C, int l
 int g_nt8 = [] { const char *e = getenv("HPNN_NT_8PH"); return !(e && e[0] == '0'); }();
 /* large weight gradients on the 8-phase TN kernel (HPNN_TN_8PH=0 keeps the 4-stage kernel) */
 int g_tn8 = [] { const char *e = getenv("HPNN_TN_8PH"); return !(e && e[0] == '0'); }();
+/* the software-pipelined 128 x 128 NT kernel for grids under two tiles per CU */
+int g_ntpp = [] { const char *e = getenv("HPNN_NT_PP"); return !(e && e[0] == '0'); }();
 
 template <int EPI, bool CF32>
 int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux, int M,
@@ -393,6 +520,12 @@ int launch_nt_epi(const void *A, int lda, const void *B, int ldb, void *C, int l
     static const bool small_off = [] { const char *e = getenv("HPNN_NT_SMALL"); return e && e[0] == '0'; }();
     if (!small_off && k64 && M % 128 == 0 && N % 128 == 0 && (long)(M / 128) * (N / 128) < 512) {
         const int tiles_n = N / 128, tiles_m = M / 128;
+        if (g_ntpp) { /* the software-pipelined form (HPNN_NT_PP=0: the kernel below) */
+            hipLaunchKernelGGL((gemm_nt_pp_kernel<EPI, CF32, 5>), dim3(tiles_m * tiles_n), dim3(512), 0, s,
+                               (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux, K,
+                               tiles_n);
+            return hipGetLastError() == hipSuccess ? 0 : -5;
+        }
         hipLaunchKernelGGL((gemm_nt_pipe_kernel<128, 128, 64, 2, 4, 3, EPI, CF32>), dim3(tiles_m * tiles_n), dim3(512),
                            0, s, (const __bf16 *)A, lda, (const __bf16 *)B, ldb, C, ldc, (const __bf16 *)aux, ldaux,
                            K, tiles_n);
@@ -477,6 +610,7 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
 
 extern "C" void hpnn_gemm_nt_set_8ph(int on) { g_nt8 = on ? 1 : 0; }
 extern "C" void hpnn_gemm_tn_set_8ph(int on) { g_tn8 = on ? 1 : 0; }
+extern "C" void hpnn_gemm_nt_set_pp(int on) { g_ntpp = on ? 1 : 0; }
 
 extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {

@@ -184,6 +184,8 @@ void bind_plan(py::module_ &m) {
         .def_readwrite("g0_perm", &BPlan::g0_perm)
         .def_readwrite("g0_xcd", &BPlan::g0_xcd)
         .def_readwrite("tn_update", &BPlan::tn_update)
+        .def_readwrite("tn8_side", &BPlan::tn8_side)
+        .def_readwrite("side_launches", &BPlan::side_launches)
         .def("tn_update_ok", &BPlan::tn_update_ok)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {
             check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
@@ -263,6 +265,7 @@ PYBIND11_MODULE(_native, m) {
               "gemm_nt8_splitk_bf16");
     });
     m.def("gemm_tn_set_8ph", [](int on) { hpnn_gemm_tn_set_8ph(on); });
+    m.def("gemm_nt_set_pp", [](int on) { hpnn_gemm_nt_set_pp(on); });
     m.def(
         "gemm_nt8_bf16",
         [](uptr A, int lda, uptr B, int ldb, uptr C, int ldc, uptr aux, int ldaux, int M, int N, int K, int epi,
@@ -360,6 +363,11 @@ PYBIND11_MODULE(_native, m) {
         a.loss_acc = (float *)P(loss), a.correct = (unsigned int *)P(correct);
         a.Bp = Bp, a.n_valid = n_valid, a.n_out = n_out, a.type = type, a.ksplit = ksplit;
         check(hpnn_wide2_front(&a, S(stream)), "wide2_front");
+    });
+    m.def("tn8_trace", []() {
+        std::vector<unsigned long long> v(512 * 8);
+        check(hpnn_tn8_trace(v.data()), "tn8_trace");
+        return v;
     });
     m.def("wide2_ksplit", [](int Bp, int K0) { return hpnn_wide2_ksplit(Bp, K0); });
     m.def("wide2_pbuf_bytes", [](int Bp) { return hpnn_wide2_pbuf_bytes(Bp); });

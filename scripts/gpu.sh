@@ -11,6 +11,7 @@
 #   rruff / synth / synth1k   bench.py --model rruff | synth | synth at batch 1024
 #   dpforce               the N > 1 MNIST path with one rank under torchrun
 #   dpforce_synth1k[_bf16]  the same for synth at batch 1024 (FP32 exchange / the BF16 reduce-scatter path)
+#   dpemu8_synth1k / prof_dpemu8   one rank running the sharded step at 8-rank sizes (HPNN_DPX_EMULATE_WORLD=8)
 #   trace                 tile-front phase trace (HPNN_TILE_TRACE=1)
 #   prof / prof_rruff     rocprofv3 kernel table (--graph 0)
 #   pmc / pmc_rruff       PMC passes of the step (scripts/pmc_step.sh); pmc_d8: 8 cycled batches
@@ -57,6 +58,8 @@ for spec in "$@"; do
     dpforce) HPNN_DP_FORCE=1 step dpforce 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --steps 200 --warmup 20 ;;
     dpforce_synth1k) HPNN_DP_FORCE=1 step dpforce_synth1k 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --model synth --batch 1024 --steps 50 --warmup 10 ;;
     dpforce_synth1k_bf16) HPNN_DP_FORCE=1 HPNN_DPX_FORCE=1 HPNN_DPX_SHARD1=1 step dpforce_synth1k_bf16 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --model synth --batch 1024 --steps 50 --warmup 10 --grad-comm bf16rs ;;
+    dpemu8_synth1k) HPNN_DP_FORCE=1 HPNN_DPX_FORCE=1 HPNN_DPX_EMULATE_WORLD=8 step dpemu8_synth1k 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --model synth --batch 1024 --steps 50 --warmup 10 --grad-comm bf16rs ;;
+    prof_dpemu8) HPNN_DP_FORCE=1 HPNN_DPX_FORCE=1 HPNN_DPX_EMULATE_WORLD=8 step rocprof_dpemu8 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_dpemu8 -o run -- python3 -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port bench.py --model synth --batch 1024 --steps 20 --warmup 5 --graph 0 --grad-comm bf16rs ;;
     trace) HPNN_TILE_TRACE=1 step tile_trace 200 python scripts/tile_trace.py ;;
     trace1) HPNN_TILE_TRACE=1 step tile_trace_d1 200 python scripts/tile_trace.py 1 ;;
     g0trace) HPNN_G0_TRACE=1 step g0_trace 200 python scripts/g0_trace.py ;;

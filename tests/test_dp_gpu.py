@@ -123,6 +123,41 @@ def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
 
 
 @pytest.mark.gpu
+def test_native_dp_exchange_emulated_world(gpu, monkeypatch):
+    """HPNN_DPX_EMULATE_WORLD=8 on one rank (csrc/dist/dp_exchange.cpp): the sharded BF16 step
+    at 8-rank sizes -- rank 0's 1/8 of every layer's rows reduce-scattered (a copy on one rank)
+    and stepped, the all-gather's receive bytes copied locally.  Those rows follow the plain
+    step within the BF16 rounding of the gradient; every other row keeps its initial master
+    (the timing knob for the per-rank compute of the 8-GPU strong-scaling shard)."""
+    monkeypatch.setenv("HPNN_DPX_FORCE", "1")
+    monkeypatch.setenv("HPNN_DPX_EMULATE_WORLD", "8")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        sizes, B = [2048, 1024, 512, 64], 1024
+        g = torch.Generator(device=dev).manual_seed(6)
+        Xr = torch.rand(B, sizes[0], device=dev, generator=g)
+        L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
+        a = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        b = MLP(sizes, "SNN", batch=B, device=dev, momentum=True, seed=3, fused=False)
+        w0 = [w.clone() for w in a.W32]
+        dp = DataParallel(a, comm="native", grad_comm="bf16rs")
+        assert dp.dpx is not None and dp.sharded == set(range(3))
+        dp.train_step(a.prepare_input(Xr), labels=L, lr=0.05, alpha=0.2)
+        b.train_step(b.prepare_input(Xr), labels=L, lr=0.05, alpha=0.2)
+        dp.gather_masters()  # nothing to gather: no error
+        torch.cuda.synchronize()
+        for l in range(3):
+            r = a.W32[l].shape[0] // 8
+            da, db = a.W32[l][:r] - w0[l][:r], b.W32[l][:r] - w0[l][:r]
+            rel = ((da - db).norm() / db.norm()).item()
+            assert rel < 1e-2, (l, rel)
+            assert torch.equal(a.W32[l][r:], w0[l][r:]), l
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sizes,expect", [([2048, 1024, 10], "bf16rs"), ([300, 96, 64, 7], "fp32"),
                                           ([4096, 4096, 32], "bf16rs")])
 def test_native_dp_exchange_auto_default(gpu, monkeypatch, sizes, expect):

@@ -74,6 +74,35 @@ def test_gemm_nt_big_tile(gpu, M, N, K, epi):
         assert err <= tol * max(1.0, scale), (f32, err, scale)
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (1024, 512, 64), (384, 256, 128), (128, 128, 192)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nt_pipelined_128(gpu, M, N, K, epi):
+    """grids under two 128 x 128 tiles per CU take the software-pipelined kernel
+    (kernels_mfma.hip gemm_nt_pp_kernel): against the FP32 reference, and BITWISE against the
+    two-barrier kernel it replaces (same MFMA order per accumulator); K from one 64-wide step
+    (no steady state) to 64 steps; padded row strides"""
+    from hpnn_amd._lib import native
+    torch.manual_seed(M + N + K + epi)
+    A = _rand(M, K + 64).bfloat16()[:, :K]
+    B = (_rand(N, K + 32) + torch.arange(N, device="cuda")[:, None] * 0.001).bfloat16()[:, :K]
+    aux = _rand(M, N + 32).bfloat16()[:, :N] if epi == ops.EPI_DACT else None
+    for f32 in (False, True):
+        outs = []
+        for pp in (1, 0):
+            native().gemm_nt_set_pp(pp)
+            try:
+                out = torch.empty(M, N + 64, dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")[:, :N]
+                outs.append(ops.gemm_nt(A, B, epi, aux=aux, out_f32=f32, out=out))
+            finally:
+                native().gemm_nt_set_pp(1)
+        R = ops.ref_gemm_nt(A, B, epi, aux)
+        tol = 2e-2 if not f32 else 2e-3
+        err = (outs[0].float() - R).abs().max().item()
+        scale = R.abs().max().item() + 1e-6
+        assert err <= tol * max(1.0, scale), (f32, err, scale)
+        assert torch.equal(outs[0], outs[1]), f32
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 384), (256, 1024, 1152),
                                    (2304, 256, 640)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])

@@ -171,3 +171,36 @@ def test_rruff_fused_tn8_update_matches_separate_update(gpu, B):
         dw = (b.W32[l] - runs["sep"][1][l]).abs().max().item()
         assert (a.W32[l] - b.W32[l]).abs().max().item() <= 1e-4 * dw + 1e-7, l
         assert torch.equal(a.Wb[l], a.W32[l].bfloat16()) and torch.equal(a.Wt[l], a.W32[l].bfloat16().t())
+
+
+@pytest.mark.parametrize("B,momentum", [(16384, True), (8192, False)])
+def test_rruff_layer1_side_job_bitwise(gpu, B, momentum):
+    """layer 1's gradient + step carried by layer 0's fused TN launch as its side job
+    (kernels_8ph.hip side_jobs / side_reduce_step) == the separate gemm_tn + update launches,
+    BITWISE: the same 64 x 64 split-K pieces, the slab sum in sgd_tile's order.  Checks that the
+    side path ran (plan.side_launches) and that the separate run did not take it."""
+    sizes = [4096, 230, 230]
+    runs = {}
+    for tag, side in (("side", True), ("sep", False)):
+        torch.manual_seed(5)
+        m = MLP(sizes, "SNN", batch=B, momentum=momentum, seed=9)
+        assert m.fused_mode == "w"
+        m.plan.tn8_side = side
+        X = m.prepare_input(torch.rand(B, sizes[0]).cuda())
+        for _ in range(3):
+            lab = torch.randint(0, sizes[-1], (B,), dtype=torch.int32, device="cuda")
+            m.train_step(X, labels=lab, lr=0.01, alpha=0.2)
+        torch.cuda.synchronize()
+        assert m.plan.health(torch.cuda.current_stream().cuda_stream) == 0
+        runs[tag] = m
+    a, b = runs["side"], runs["sep"]
+    assert b.plan.side_launches == 0
+    if a.plan.side_launches == 0:
+        pytest.skip(f"side job does not fit this grid (B={B}, splits {list(a.S)})")
+    assert a.plan.side_launches == 3
+    for l in range(2):
+        assert torch.equal(a.W32[l], b.W32[l]), l
+        if momentum:
+            assert torch.equal(a.V32[l], b.V32[l]), l
+        assert torch.equal(a.Wb[l], b.Wb[l]) and torch.equal(a.Wt[l], b.Wt[l]), l
+        assert torch.equal(a.Wt[l], a.W32[l].bfloat16().t()), l
