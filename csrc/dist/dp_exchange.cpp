@@ -6,6 +6,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <libhpnn.h>
 #include <libhpnn/devmem.h>
 
@@ -13,7 +15,14 @@ namespace hpnn {
 
 DpExchange::~DpExchange() {
     if (p_)
-        for (int l = 0; l < p_->L; l++) p_->g16[l] = nullptr;
+        for (int l = 0; l < p_->L; l++) {
+            p_->g16[l] = nullptr;
+            if (l < (int)nn_.size() && nn_[l]) { /* the plan goes back to W^T: make it current */
+                p_->nn_bwd[l] = false;
+                (void)hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], p_->Np[l], p_->Kp[l], nullptr);
+            }
+        }
+    if (p_ && std::find(nn_.begin(), nn_.end(), true) != nn_.end()) (void)hipDeviceSynchronize();
     hpnn_dev_free(grad16_);
     hpnn_dev_free(send16_);
     hpnn_dev_free(recv16_);
@@ -75,6 +84,16 @@ int DpExchange::init(BPlan *plan, hpnn_comm *comm, int mode) {
             p_->g16[l] = (char *)grad16_ + o * 2;
             o += (size_t)p_->Np[l] * p_->Kp[l];
         }
+    /* the delta GEMM of a sharded layer reads the all-gathered W directly (NN form, same bits),
+     * so the step needs no W^T rebuild (a 2 x P-byte transpose per layer; HPNN_DPX_NN=0: keep
+     * it); W^T is made current again by gather_masters and when the exchange goes away */
+    const char *nn = getenv("HPNN_DPX_NN");
+    nn_.assign(p_->L, false);
+    for (int l = 1; l < p_->L; l++)
+        if (sharded_[l] && !(nn && nn[0] == '0') &&
+            hpnn_gemm_nn_ok(p_->Bp, p_->Np[l - 1], p_->Np[l], p_->Np[l], p_->Kp[l], p_->Np[l - 1]) &&
+            p_->Kp[l] == p_->Np[l - 1])
+            nn_[l] = p_->nn_bwd[l] = true;
     return 0;
 }
 
@@ -103,7 +122,7 @@ int DpExchange::step(const XIn &x, const int *labels, const float *T, int ldt, i
                                hipMemcpyDeviceToDevice, side) == hipSuccess ? 0 : -5;
         else if (!r)
             r = hpnn_comm_all_gather(c_, (char *)p_->Wb[l] + off * 2, p_->Wb[l], cnt, HPNN_DT_BF16, side);
-        if (!r) r = hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], N, K, side);
+        if (!r && !nn_[l]) r = hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], N, K, side);
         const int rd = hpnn_comm_fork_done(c_);
         return r ? r : rd;
     };
@@ -137,7 +156,9 @@ int DpExchange::gather_masters(hipStream_t s) {
     if (mode_ != BF16RS) return 0;
     for (int l = 0; l < p_->L; l++) {
         if (!sharded_[l]) continue;
-        if (emu_) return 0; /* an emulated run has no other ranks' rows to gather */
+        /* W^T current for the readers outside the step (checkpoints, tests, digests) */
+        if (nn_[l] && hpnn_transpose_bf16(p_->Wb[l], p_->Wt[l], p_->Np[l], p_->Kp[l], s)) return -3;
+        if (emu_) continue; /* an emulated run has no other ranks' rows to gather */
         const long cnt = (long)(p_->Np[l] / world_) * p_->Kp[l], off = (long)rank_ * cnt;
         float *bufs[2] = {p_->W32[l], p_->V32[l]};
         for (float *b : bufs) {

@@ -54,6 +54,7 @@ class DpExchange {
     void *emu16_ = nullptr;
     Mode mode_ = FP32;
     std::vector<bool> sharded_;
+    std::vector<bool> nn_; /* sharded layers whose delta GEMM reads W (no W^T rebuild per step) */
     void *send16_ = nullptr, *recv16_ = nullptr;
     void *grad16_ = nullptr; /* per-layer BF16 gradients written by the plan's TN GEMM (sharded layers) */
 };

@@ -291,6 +291,9 @@ int BPlan::output(const int *labels, const float *T, int ldt, int n_valid, float
 /* D[l-1] = (D[l] . W_l) * f'(H[l-1]) with the pre-update W_l^T ([Kp[l] x Np[l]]) */
 int BPlan::backward_layer(int l, hipStream_t s) {
     if (l < 1 || l >= L) return -1;
+    if (nn_bwd[l])
+        return hpnn_gemm_nn_bf16(D[l], Np[l], Wb[l], Kp[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp, Np[l - 1],
+                                 Np[l], HPNN_EPI_DACT, 0, s);
     return hpnn_gemm_nt_bf16(D[l], Np[l], Wt[l], Np[l], D[l - 1], Np[l - 1], H[l - 1], Np[l - 1], Bp, Np[l - 1], Np[l],
                              HPNN_EPI_DACT, 0, s);
 }

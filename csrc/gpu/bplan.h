@@ -90,6 +90,9 @@ class BPlan {
     /* two-layer nets: layer 1's gradient + step as the side job of layer 0's fused TN launch */
     bool tn8_side = [] { const char *e = getenv("HPNN_TN8_SIDE"); return !(e && e[0] == '0'); }();
     long side_launches = 0; /* launches issued with that side job (tests) */
+    /* per-layer: the delta GEMM reads W (NN form, hpnn_gemm_nn_bf16) instead of W^T, which is
+     * then not kept current (the sharded data-parallel step sets it: no transpose per update) */
+    bool nn_bwd[16] = {false};
     size_t goff[17] = {0};
     std::vector<BufSpec> specs;
 

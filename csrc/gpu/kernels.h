@@ -88,6 +88,11 @@ int hpnn_gemm_tn8_fused_update_side(const void *D, int ldd, const void *H, int l
 void hpnn_gemm_nt_set_8ph(int on);
 void hpnn_gemm_tn_set_8ph(int on); /* same switch for the large weight-gradient GEMMs */
 void hpnn_gemm_nt_set_pp(int on);  /* the pipelined 128 x 128 NT kernel for under-filled grids */
+/* C[M x N] = epi(A[M x K] . W[K x N]), W row-major [K][N]: the NT product on W^T without the
+ * transposed copy (same bits); M, N % 128, K % 64, else -1.  _ok: 1 when the shape fits */
+int hpnn_gemm_nn_ok(int M, int N, int K, int lda, int ldw, int ldc);
+int hpnn_gemm_nn_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc, const void *aux, int ldaux,
+                      int M, int N, int K, int epi, int c_f32, hipStream_t stream);
 int hpnn_gemm_nt8_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux, int ldaux,
                        int M, int N, int K, int epi, int c_f32, hipStream_t stream);
 int hpnn_gemm_nt_ws_bf16(const void *X, int ldx, const void *W, int ldw, void *C, int ldc, int M, int N, int K,

@@ -219,8 +219,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_pipe_kernel(const __bf16
  *                       read (kt, k32 1) -> R1;  16 MFMAs on R0 = (kt, k32 0)
  *                       counted vmcnt for stage kt + 1; lgkmcnt(0); ONE barrier
  *                       read (kt + 1, k32 0) -> R0;  16 MFMAs on R1
- * Same MFMA order per accumulator as gemm_nt_pipe_kernel: bitwise the same products. */
-template <int EPI, bool CF32, int ST>
+ * Same MFMA order per accumulator as gemm_nt_pipe_kernel: bitwise the same products.
+ * BT ("NN"): B given as B^T, i.e. [K][N] row-major (a weight matrix W [N_out][K_in] used as
+ * the delta GEMM's right operand without its transposed copy): staged as a T32 image and read
+ * with the transposing ds_read_b64_tr_b16, the operands the MFMAs see -- and so the result
+ * bits -- are those of the NT form on W^T. */
+template <int EPI, bool CF32, int ST, bool BT = false>
 __global__ __launch_bounds__(512) void gemm_nt_pp_kernel(const __bf16 *__restrict__ A, int lda,
                                                          const __bf16 *__restrict__ B, int ldb, void *__restrict__ C,
                                                          int ldc, const __bf16 *__restrict__ aux, int ldaux, int K,
@@ -238,17 +242,18 @@ __global__ __launch_bounds__(512) void gemm_nt_pp_kernel(const __bf16 *__restric
     const int m0 = tm * BM, n0 = tn * BN;
     const int KT = K / BK;
     const char *Ag = (const char *)(A + (size_t)m0 * lda);
-    const char *Bg = (const char *)(B + (size_t)n0 * ldb);
+    const char *Bg = (const char *)(BT ? B + n0 : B + (size_t)n0 * ldb);
     const size_t lda_b = (size_t)lda * 2, ldb_b = (size_t)ldb * 2;
     const int r16 = lane & 15, q = lane >> 4;
 
     auto issue = [&](int kt) __attribute__((always_inline)) {
         char *sa = lds + (kt % ST) * STAGE, *sb = sa + A_BYTES;
-        const char *ga = Ag + (size_t)kt * RB, *gb = Bg + (size_t)kt * RB;
+        const char *ga = Ag + (size_t)kt * RB, *gb = BT ? Bg + (size_t)kt * BK * ldb_b : Bg + (size_t)kt * RB;
 #pragma unroll
         for (int i = 0; i < LPS; i++) {
             const int c = wave + 8 * i; /* wave-uniform: pieces 0-15 A, 16-31 B */
             if (c < A_PIECES) glds_piece<BK>(ga, lda_b, sa + c * 1024, c * 8, lane);
+            else if constexpr (BT) hpnn::glds_t32_piece<BK>(gb, ldb_b, sb, c - A_PIECES, lane);
             else glds_piece<BK>(gb, ldb_b, sb + (c - A_PIECES) * 1024, (c - A_PIECES) * 8, lane);
         }
     };
@@ -259,7 +264,10 @@ __global__ __launch_bounds__(512) void gemm_nt_pp_kernel(const __bf16 *__restric
 #pragma unroll
         for (int j = 0; j < 4; j++) fa[j] = *(const bf16x8 *)(sa + nt_off<CPR>(wm * 64 + j * 16 + r16, ch));
 #pragma unroll
-        for (int i = 0; i < 2; i++) fb[i] = *(const bf16x8 *)(sb + nt_off<CPR>(wn * 32 + i * 16 + r16, ch));
+        for (int i = 0; i < 2; i++) {
+            if constexpr (BT) fb[i] = hpnn::frag_tr<BK>(sb, kk * 32, wn * 32 + i * 16, lane);
+            else fb[i] = *(const bf16x8 *)(sb + nt_off<CPR>(wn * 32 + i * 16 + r16, ch));
+        }
     };
     f32x4 acc[2][4];
 #pragma unroll
@@ -611,6 +619,33 @@ int gemm_tn_dispatch(const void *D, int ldd, const void *H, int ldh, float *slab
 extern "C" void hpnn_gemm_nt_set_8ph(int on) { g_nt8 = on ? 1 : 0; }
 extern "C" void hpnn_gemm_tn_set_8ph(int on) { g_tn8 = on ? 1 : 0; }
 extern "C" void hpnn_gemm_nt_set_pp(int on) { g_ntpp = on ? 1 : 0; }
+
+/* C[M x N] = epi(A[M x K] . W[K x N]) with W row-major [K][N] (the NT GEMM on W^T without the
+ * transposed copy; gemm_nt_pp_kernel<..., BT>): M, N multiples of 128, K of 64 */
+extern "C" int hpnn_gemm_nn_ok(int M, int N, int K, int lda, int ldw, int ldc) {
+    return M > 0 && N > 0 && K > 0 && M % 128 == 0 && N % 128 == 0 && K % 64 == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+           ldc % 8 == 0 && (size_t)ldw * 2 * 64 < (1u << 31);
+}
+extern "C" int hpnn_gemm_nn_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc, const void *aux,
+                                 int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {
+    if (!hpnn_gemm_nn_ok(M, N, K, lda, ldw, ldc)) return -1;
+    if (epi == HPNN_EPI_DACT && (!aux || ldaux % 4)) return -3;
+    const int tiles_n = N / 128, grid = (M / 128) * tiles_n;
+#define HPNN_NN(E, F)                                                                                              \
+    hipLaunchKernelGGL((gemm_nt_pp_kernel<E, F, 5, true>), dim3(grid), dim3(512), 0, stream, (const __bf16 *)A, lda, \
+                       (const __bf16 *)W, ldw, C, ldc, (const __bf16 *)aux, ldaux, K, tiles_n)
+    if (c_f32) {
+        if (epi == HPNN_EPI_NONE) HPNN_NN(HPNN_EPI_NONE, true);
+        else if (epi == HPNN_EPI_ACT) HPNN_NN(HPNN_EPI_ACT, true);
+        else HPNN_NN(HPNN_EPI_DACT, true);
+    } else {
+        if (epi == HPNN_EPI_NONE) HPNN_NN(HPNN_EPI_NONE, false);
+        else if (epi == HPNN_EPI_ACT) HPNN_NN(HPNN_EPI_ACT, false);
+        else HPNN_NN(HPNN_EPI_DACT, false);
+    }
+#undef HPNN_NN
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 extern "C" int hpnn_gemm_nt_bf16(const void *A, int lda, const void *B, int ldb, void *C, int ldc, const void *aux,
                                  int ldaux, int M, int N, int K, int epi, int c_f32, hipStream_t stream) {

@@ -186,6 +186,7 @@ void bind_plan(py::module_ &m) {
         .def_readwrite("tn_update", &BPlan::tn_update)
         .def_readwrite("tn8_side", &BPlan::tn8_side)
         .def_readwrite("side_launches", &BPlan::side_launches)
+        .def_property_readonly("nn_bwd", [](const BPlan &p) { return std::vector<bool>(p.nn_bwd, p.nn_bwd + 16); })
         .def("tn_update_ok", &BPlan::tn_update_ok)
         .def("predict", [](BPlan &p, uptr X, int n_valid, uptr O, int ldo, uptr s) {
             check(p.predict(P(X), n_valid, (float *)P(O), ldo, S(s)), "BPlan.predict");
@@ -274,6 +275,14 @@ PYBIND11_MODULE(_native, m) {
                   "gemm_nt8_bf16");
         },
         "C = epi(A . B^T), bf16 MFMA");
+    m.def(
+        "gemm_nn_bf16",
+        [](uptr A, int lda, uptr W, int ldw, uptr C, int ldc, uptr aux, int ldaux, int M, int N, int K, int epi,
+           int c_f32, uptr stream) {
+            check(hpnn_gemm_nn_bf16(P(A), lda, P(W), ldw, P(C), ldc, P(aux), ldaux, M, N, K, epi, c_f32, S(stream)),
+                  "gemm_nn_bf16");
+        },
+        "C = epi(A . W), W row-major [K][N], bf16 MFMA");
     m.def("reduce_slabs", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
         check(hpnn_reduce_slabs((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)), "reduce_slabs");
     });

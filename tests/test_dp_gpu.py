@@ -80,20 +80,23 @@ def test_native_comm_primitives_single_rank(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("grad_comm", ["fp32", "bf16rs"])
-def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
+@pytest.mark.parametrize("grad_comm,sizes", [("fp32", [300, 96, 64, 7]), ("bf16rs", [300, 96, 64, 7]),
+                                             ("bf16rs", [1024, 512, 256, 10])])
+def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm, sizes):
     """the library's data-parallel step (csrc/dist/dp_exchange.cpp, hpnn::DpExchange) forced
     onto a one-rank RCCL group (HPNN_DPX_FORCE / HPNN_DPX_SHARD1): fp32 = per-layer bucket
     all-reduce on the communicator's side stream + one update; bf16rs = per-layer BF16 cast ->
     reduce-scatter -> row step of the FP32 masters -> in-place BF16 all-gather -> W^T rebuild.
     Against the plain step: fp32 to summation order, bf16rs within the BF16 rounding of the
-    gradient (relative error of the weight change < 1e-2)."""
+    gradient (relative error of the weight change < 1e-2).  [1024, 512, 256, 10]: layer 1's delta
+    GEMM reads the all-gathered W (NN form) and skips the W^T rebuild; gather_masters makes W^T
+    current again."""
     monkeypatch.setenv("HPNN_DPX_FORCE", "1")
     monkeypatch.setenv("HPNN_DPX_SHARD1", "1")
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
     try:
-        sizes, B = [300, 96, 64, 7], 2048
+        B = 2048
         g = torch.Generator(device=dev).manual_seed(5)
         Xr = torch.rand(B, sizes[0], device=dev, generator=g)
         L = torch.randint(0, sizes[-1], (B,), device=dev, generator=g, dtype=torch.int32)
@@ -104,6 +107,7 @@ def test_native_dp_exchange_single_rank(gpu, monkeypatch, grad_comm):
         assert dp.dpx is not None
         if grad_comm == "bf16rs":
             assert dp.sharded == set(range(3))
+            assert list(a.plan.nn_bwd[:3]) == ([False, True, False] if sizes[0] == 1024 else [False] * 3)
         Xa, Xb = a.prepare_input(Xr), b.prepare_input(Xr)
         for _ in range(3):
             dp.train_step(Xa, labels=L, lr=0.05, alpha=0.2)
@@ -145,9 +149,11 @@ def test_native_dp_exchange_emulated_world(gpu, monkeypatch):
         assert dp.dpx is not None and dp.sharded == set(range(3))
         dp.train_step(a.prepare_input(Xr), labels=L, lr=0.05, alpha=0.2)
         b.train_step(b.prepare_input(Xr), labels=L, lr=0.05, alpha=0.2)
-        dp.gather_masters()  # nothing to gather: no error
+        dp.gather_masters()  # nothing to gather; W^T of the NN-form layers made current
         torch.cuda.synchronize()
+        assert list(a.plan.nn_bwd[:3]) == [False, True, True]
         for l in range(3):
+            assert torch.equal(a.Wt[l], a.W32[l].bfloat16().t()), l
             r = a.W32[l].shape[0] // 8
             da, db = a.W32[l][:r] - w0[l][:r], b.W32[l][:r] - w0[l][:r]
             rel = ((da - db).norm() / db.norm()).item()

@@ -103,6 +103,30 @@ def test_gemm_nt_pipelined_128(gpu, M, N, K, epi):
         assert torch.equal(outs[0], outs[1]), f32
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (1024, 512, 64), (384, 256, 128), (2048, 1024, 512)])
+@pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
+def test_gemm_nn_matches_nt_on_transpose(gpu, M, N, K, epi):
+    """C = epi(A . W) with W row-major [K][N] (kernels_mfma.hip gemm_nt_pp_kernel<..., BT>: W staged
+    as a T32 image, read with the transposing LDS read) == the NT GEMM on the explicit W^T,
+    BITWISE (the delta GEMM of the sharded data-parallel step reads W without its transposed
+    copy); padded row strides"""
+    from hpnn_amd._lib import native
+    torch.manual_seed(M + N + K + epi)
+    A = _rand(M, K + 64).bfloat16()[:, :K]
+    W = (_rand(K, N + 32) + torch.arange(N + 32, device="cuda")[None, :] * 0.001).bfloat16()[:, :N]
+    Wt = W.t().contiguous()
+    aux = _rand(M, N + 32).bfloat16()[:, :N] if epi == ops.EPI_DACT else None
+    s = torch.cuda.current_stream().cuda_stream
+    for f32 in (False, True):
+        dt = torch.float32 if f32 else torch.bfloat16
+        C = torch.empty(M, N + 64, dtype=dt, device="cuda")[:, :N]
+        native().gemm_nn_bf16(A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), C.data_ptr(), C.stride(0),
+                              aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+                              M, N, K, epi, int(f32), s)
+        R = ops.gemm_nt(A, Wt, epi, aux=aux, out_f32=f32)
+        assert torch.equal(C, R), f32
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 384), (256, 1024, 1152),
                                    (2304, 256, 640)])
 @pytest.mark.parametrize("epi", [ops.EPI_NONE, ops.EPI_ACT, ops.EPI_DACT])
