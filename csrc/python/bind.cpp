@@ -283,6 +283,9 @@ PYBIND11_MODULE(_native, m) {
                   "gemm_nn_bf16");
         },
         "C = epi(A . W), W row-major [K][N], bf16 MFMA");
+    m.def("transpose_bf16", [](uptr Wb, uptr Wt, int N, int K, uptr stream) {
+        check(hpnn_transpose_bf16(P(Wb), P(Wt), N, K, S(stream)), "transpose_bf16");
+    });
     m.def("reduce_slabs", [](uptr slab, int Sn, long stride, long n, uptr out, uptr stream) {
         check(hpnn_reduce_slabs((const float *)P(slab), Sn, stride, n, (float *)P(out), S(stream)), "reduce_slabs");
     });
